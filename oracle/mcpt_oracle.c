@@ -1,0 +1,1312 @@
+/* TEST INFRASTRUCTURE ONLY -- see mcpt_oracle.h for scope and the parity pin.
+ *
+ * Every function cites the reference file:line it restates.  Arithmetic is fp64 in the
+ * reference's evaluation order (vec.cpp / matrix3d.cpp operator semantics), compiled with
+ * -ffp-contract=off so that no FMA contraction changes a rounding.
+ */
+#define _GNU_SOURCE
+#include "mcpt_oracle.h"
+
+#include <ctype.h>
+#include <float.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define EPS 1e-8 /* vec.h:7, Myobj.h:69, Mylight.h:101, BRDF.cpp:8 */
+#define PI 3.141592653589793 /* std::numbers::pi */
+#define P_RR 0.6             /* main.cpp:375,429 */
+#define COUNTER_MAX_DEPTH 48 /* counter-RNG trees: nodes deeper than this return 0 */
+
+static __thread char g_err[512];
+const char* orc_last_error(void) { return g_err; }
+static void set_err(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * vec / matrix3d semantics (vec.cpp:38-103, matrix3d.cpp:8-40)                              */
+typedef struct { double x, y, z; } v3;
+static inline v3 mk(double a, double b, double c) { v3 r = {a, b, c}; return r; }
+static inline v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vmul(v3 a, double c) { return mk(a.x * c, a.y * c, a.z * c); }
+static inline double vdot(v3 a, v3 b) {  /* vec.cpp:73-81: ans = 0; ans += ... */
+    double s = 0;
+    s += a.x * b.x;
+    s += a.y * b.y;
+    s += a.z * b.z;
+    return s;
+}
+static inline v3 vcross(v3 a, v3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline double vnorm(v3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+static inline v3 vnormalized(v3 a) {  /* vec.cpp:99-103, no zero guard */
+    double l = vnorm(a);
+    return mk(a.x / l, a.y / l, a.z / l);
+}
+static inline double vdet(v3 a, v3 b, v3 c) { return vdot(vcross(a, b), c); } /* vec.cpp:84-87 */
+/* matrix3d(c0,c1,c2) * x with the vectors as COLUMNS (matrix3d.cpp:8-40) */
+static inline v3 mat_cols_mul(v3 c0, v3 c1, v3 c2, v3 x) {
+    double b0 = 0, b1 = 0, b2 = 0;
+    b0 += c0.x * x.x; b0 += c1.x * x.y; b0 += c2.x * x.z;
+    b1 += c0.y * x.x; b1 += c1.y * x.y; b1 += c2.y * x.z;
+    b2 += c0.z * x.x; b2 += c1.z * x.y; b2 += c2.z * x.z;
+    return mk(b0, b1, b2);
+}
+static inline v3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
+static inline void st3(double* p, v3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+
+/* ------------------------------------------------------------------------------------------
+ * scene                                                                                      */
+typedef struct { char name[128]; float kd[3], ks[3], ns; } material;
+
+struct orc_scene {
+    int F, M, NL;
+    float* v;        /* F*9  (tinyobj real_t = float) */
+    float* vn;       /* F*9 */
+    int* mat;        /* F */
+    int* light_of;   /* F -> light-table index or -1 */
+    double* un;      /* F*3 unique normal (Myobj.cpp:680-709) */
+    material* mtl;   /* M */
+    int* lfacet;     /* NL, reference order */
+    double* larea;   /* NL */
+    double* lrad;    /* NL*3 */
+    double* lsum;    /* NL: RadianceRGB::sum() */
+    int has_cam;
+    orc_camera cam;
+    /* uniform grid */
+    int grid_ok;
+    double mm[3][2], d, inv_d;
+    int lim[3], gd[3];
+    int* cell_start; /* gd0*gd1*gd2 + 1 */
+    int* cell_tri;
+};
+
+static inline v3 fvert(const orc_scene* s, int f, int k) {
+    const float* p = s->v + 9 * f + 3 * k;
+    return mk(p[0], p[1], p[2]);
+}
+static inline v3 fnorm(const orc_scene* s, int f, int k) {
+    const float* p = s->vn + 9 * f + 3 * k;
+    return mk(p[0], p[1], p[2]);
+}
+
+/* ---- tinyobjloader number parser, restated (tiny_obj_loader.h:897-1038) ------------------ */
+static int tobj_parse_double(const char* s, const char* e, double* result) {
+    static const double lut[] = {1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001};
+    if (s >= e) return 0;
+    double mant = 0.0;
+    int expo = 0, read = 0, lead_dot = 0;
+    char sign = '+', esign = '+';
+    const char* c = s;
+    if (*c == '+' || *c == '-') {
+        sign = *c++;
+        if (c != e && *c == '.') lead_dot = 1;
+    } else if (isdigit((unsigned char)*c)) {
+    } else if (*c == '.') {
+        lead_dot = 1;
+    } else {
+        return 0;
+    }
+    if (!lead_dot) {
+        while (c != e && isdigit((unsigned char)*c)) {
+            mant *= 10;
+            mant += (int)(*c - '0');
+            c++;
+            read++;
+        }
+        if (read == 0) return 0;
+    }
+    if (c == e) goto assemble;
+    if (*c == '.') {
+        c++;
+        read = 1;
+        while (c != e && isdigit((unsigned char)*c)) {
+            mant += (int)(*c - '0') * (read < 8 ? lut[read] : pow(10.0, -read));
+            read++;
+            c++;
+        }
+    } else if (*c == 'e' || *c == 'E') {
+    } else {
+        goto assemble;
+    }
+    if (c == e) goto assemble;
+    if (*c == 'e' || *c == 'E') {
+        c++;
+        if (c != e && (*c == '+' || *c == '-')) {
+            esign = *c++;
+        } else if (c != e && isdigit((unsigned char)*c)) {
+        } else {
+            return 0;
+        }
+        read = 0;
+        while (c != e && isdigit((unsigned char)*c)) {
+            if (expo > 2147483647 / 10) return 0;
+            expo *= 10;
+            expo += (int)(*c - '0');
+            c++;
+            read++;
+        }
+        expo *= (esign == '+' ? 1 : -1);
+        if (read == 0) return 0;
+    }
+assemble:
+    *result = (sign == '+' ? 1 : -1) * (expo ? ldexp(mant * pow(5.0, expo), expo) : mant);
+    return 1;
+}
+/* parseReal: skip " \t", token up to " \t\r", default on failure, cast to float */
+static float tobj_real(const char** tok, double dflt) {
+    *tok += strspn(*tok, " \t");
+    const char* end = *tok + strcspn(*tok, " \t\r\n");
+    double val = dflt;
+    tobj_parse_double(*tok, end, &val);
+    *tok = end;
+    return (float)val;
+}
+
+static char* read_file(const char* path, size_t* len) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return NULL;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    char* b = (char*)malloc((size_t)n + 2);
+    if (n > 0 && fread(b, 1, (size_t)n, f) != (size_t)n) { fclose(f); free(b); return NULL; }
+    fclose(f);
+    b[n] = '\n';
+    b[n + 1] = 0;
+    if (len) *len = (size_t)n;
+    return b;
+}
+
+typedef struct { void* p; size_t n, cap, el; } vecbuf;
+static void vb_push(vecbuf* b, const void* x) {
+    if (b->n == b->cap) {
+        b->cap = b->cap ? 2 * b->cap : 1024;
+        b->p = realloc(b->p, b->cap * b->el);
+    }
+    memcpy((char*)b->p + b->n * b->el, x, b->el);
+    b->n++;
+}
+
+/* MTL subset of tinyobj LoadMtl: newmtl / Kd / Ks / Ns (defaults of InitMaterial,
+ * tiny_obj_loader.h:1386-1420: kd = ks = 0, Ns = 1) */
+static int load_mtl(const char* path, vecbuf* mats) {
+    char* buf = read_file(path, NULL);
+    if (!buf) return 0;
+    material cur;
+    memset(&cur, 0, sizeof cur);
+    cur.ns = 1.0f;
+    int have = 0;
+    for (char* line = buf; *line;) {
+        char* nl = strchr(line, '\n');
+        *nl = 0;
+        const char* t = line + strspn(line, " \t");
+        if (!strncmp(t, "newmtl", 6) && (t[6] == ' ' || t[6] == '\t')) {
+            if (have && cur.name[0]) vb_push(mats, &cur);
+            memset(&cur, 0, sizeof cur);
+            cur.ns = 1.0f;
+            t += 7;
+            t += strspn(t, " \t");
+            size_t k = strcspn(t, "\r\n");
+            while (k > 0 && (t[k - 1] == ' ' || t[k - 1] == '\t')) k--;
+            if (k >= sizeof cur.name) k = sizeof cur.name - 1;
+            memcpy(cur.name, t, k);
+            cur.name[k] = 0;
+            have = 1;
+        } else if (t[0] == 'K' && t[1] == 'd' && (t[2] == ' ' || t[2] == '\t')) {
+            t += 2;
+            for (int c = 0; c < 3; c++) cur.kd[c] = tobj_real(&t, 0.0);
+        } else if (t[0] == 'K' && t[1] == 's' && (t[2] == ' ' || t[2] == '\t')) {
+            t += 2;
+            for (int c = 0; c < 3; c++) cur.ks[c] = tobj_real(&t, 0.0);
+        } else if (t[0] == 'N' && t[1] == 's' && (t[2] == ' ' || t[2] == '\t')) {
+            t += 2;
+            cur.ns = tobj_real(&t, 0.0);
+        }
+        line = nl + 1;
+    }
+    if (have && cur.name[0]) vb_push(mats, &cur);
+    free(buf);
+    return 1;
+}
+
+static int fix_index(long idx, long n, long* out) { /* tinyobj fixIndex */
+    if (idx > 0) { *out = idx - 1; return 1; }
+    if (idx == 0) return 0;
+    *out = n + idx;
+    return 1;
+}
+
+typedef struct { float v[9], n[9]; int mat; } facet_rec;
+
+/* OBJ subset of tinyobj LoadObj (tiny_obj_loader.h:2600-3140): v, vn, f, usemtl, mtllib; faces
+ * in file order (= the reference's (shape, face) order); quads split on the shorter diagonal
+ * (tiny_obj_loader.h:1509-1605); larger polygons fan-triangulated (documented deviation). */
+static int load_obj(orc_scene* s, const char* path) {
+    char* buf = read_file(path, NULL);
+    if (!buf) { set_err("cannot open %s", path); return 0; }
+    char dir[1024] = "";
+    const char* sl = strrchr(path, '/');
+    if (sl) { size_t k = (size_t)(sl - path + 1); if (k >= sizeof dir) k = sizeof dir - 1; memcpy(dir, path, k); dir[k] = 0; }
+    vecbuf V = {0, 0, 0, sizeof(float) * 3}, N = {0, 0, 0, sizeof(float) * 3};
+    vecbuf FAC = {0, 0, 0, sizeof(facet_rec)}, MAT = {0, 0, 0, sizeof(material)};
+    int cur_mat = -1, ok = 1;
+    for (char* line = buf; *line && ok;) {
+        char* nl = strchr(line, '\n');
+        *nl = 0;
+        const char* t = line + strspn(line, " \t");
+        if (t[0] == 'v' && (t[1] == ' ' || t[1] == '\t')) {
+            t += 2;
+            float p[3];
+            for (int c = 0; c < 3; c++) p[c] = tobj_real(&t, 0.0);
+            vb_push(&V, p);
+        } else if (t[0] == 'v' && t[1] == 'n' && (t[2] == ' ' || t[2] == '\t')) {
+            t += 3;
+            float p[3];
+            for (int c = 0; c < 3; c++) p[c] = tobj_real(&t, 0.0);
+            vb_push(&N, p);
+        } else if (t[0] == 'f' && (t[1] == ' ' || t[1] == '\t')) {
+            t += 2;
+            long vi[64], ni[64];
+            int nv = 0;
+            while (*t && nv < 64) {
+                t += strspn(t, " \t");
+                if (!*t || *t == '\r') break;
+                char* endp;
+                long a = strtol(t, &endp, 10), c = 0;
+                t = endp;
+                if (*t == '/') {
+                    t++;
+                    if (*t != '/') { strtol(t, &endp, 10); t = endp; }
+                    if (*t == '/') { t++; c = strtol(t, &endp, 10); t = endp; }
+                }
+                t += strcspn(t, " \t\r");
+                if (!fix_index(a, (long)V.n, &vi[nv]) || c == 0 || !fix_index(c, (long)N.n, &ni[nv])) {
+                    set_err("%s: face without vertex normal (the reference needs normal_index >= 0)", path);
+                    ok = 0;
+                    break;
+                }
+                nv++;
+            }
+            if (!ok) break;
+            if (nv < 3) goto next;
+            int tris[64][3], nt = 0;
+            if (nv == 3) {
+                tris[0][0] = 0; tris[0][1] = 1; tris[0][2] = 2; nt = 1;
+            } else if (nv == 4) {
+                const float* P = (const float*)V.p;
+                float e02x = P[3 * vi[2] + 0] - P[3 * vi[0] + 0], e02y = P[3 * vi[2] + 1] - P[3 * vi[0] + 1],
+                      e02z = P[3 * vi[2] + 2] - P[3 * vi[0] + 2];
+                float e13x = P[3 * vi[3] + 0] - P[3 * vi[1] + 0], e13y = P[3 * vi[3] + 1] - P[3 * vi[1] + 1],
+                      e13z = P[3 * vi[3] + 2] - P[3 * vi[1] + 2];
+                float sq02 = e02x * e02x + e02y * e02y + e02z * e02z;
+                float sq13 = e13x * e13x + e13y * e13y + e13z * e13z;
+                if (sq02 < sq13) {
+                    int a[2][3] = {{0, 1, 2}, {0, 2, 3}};
+                    memcpy(tris, a, sizeof a);
+                } else {
+                    int a[2][3] = {{0, 1, 3}, {1, 2, 3}};
+                    memcpy(tris, a, sizeof a);
+                }
+                nt = 2;
+            } else {
+                for (int k = 1; k + 1 < nv; k++) { tris[nt][0] = 0; tris[nt][1] = k; tris[nt][2] = k + 1; nt++; }
+            }
+            for (int q = 0; q < nt; q++) {
+                facet_rec fr;
+                for (int k = 0; k < 3; k++) {
+                    memcpy(fr.v + 3 * k, (const float*)V.p + 3 * vi[tris[q][k]], 12);
+                    memcpy(fr.n + 3 * k, (const float*)N.p + 3 * ni[tris[q][k]], 12);
+                }
+                fr.mat = cur_mat;
+                vb_push(&FAC, &fr);
+            }
+        } else if (!strncmp(t, "usemtl", 6) && (t[6] == ' ' || t[6] == '\t')) {
+            t += 7;
+            t += strspn(t, " \t");
+            size_t k = strcspn(t, " \t\r\n");
+            cur_mat = -1;
+            for (size_t m = 0; m < MAT.n; m++) {
+                const material* mm = (const material*)MAT.p + m;
+                if (strlen(mm->name) == k && !strncmp(mm->name, t, k)) { cur_mat = (int)m; break; }
+            }
+        } else if (!strncmp(t, "mtllib", 6) && (t[6] == ' ' || t[6] == '\t')) {
+            t += 7;
+            t += strspn(t, " \t");
+            char fn[1024];
+            size_t k = strcspn(t, " \t\r\n");
+            snprintf(fn, sizeof fn, "%s%.*s", dir, (int)k, t);
+            load_mtl(fn, &MAT);
+        }
+    next:
+        line = nl + 1;
+    }
+    free(buf);
+    free(V.p);
+    free(N.p);
+    if (!ok) { free(FAC.p); free(MAT.p); return 0; }
+    s->F = (int)FAC.n;
+    s->M = (int)MAT.n;
+    s->mtl = (material*)MAT.p;
+    s->v = (float*)malloc(sizeof(float) * 9 * (s->F + 1));
+    s->vn = (float*)malloc(sizeof(float) * 9 * (s->F + 1));
+    s->mat = (int*)malloc(sizeof(int) * (s->F + 1));
+    for (int f = 0; f < s->F; f++) {
+        const facet_rec* fr = (const facet_rec*)FAC.p + f;
+        memcpy(s->v + 9 * f, fr->v, 36);
+        memcpy(s->vn + 9 * f, fr->n, 36);
+        s->mat[f] = fr->mat;
+    }
+    free(FAC.p);
+    return 1;
+}
+
+/* pugixml subset: attributes of top-level <light .../> (Mylight.cpp:21-28) and the <camera>
+ * block of the scene XML (README.md:339-343, ignored by the reference main.cpp:507-510). */
+static int xml_attr(const char* tag, const char* tag_end, const char* name, char* out, size_t cap) {
+    size_t nlen = strlen(name);
+    for (const char* p = tag; p + nlen < tag_end; p++) {
+        if (!strncmp(p, name, nlen) && (p == tag || isspace((unsigned char)p[-1]))) {
+            const char* q = p + nlen;
+            q += strspn(q, " \t\r\n");
+            if (*q != '=') continue;
+            q++;
+            q += strspn(q, " \t\r\n");
+            char quote = *q;
+            if (quote != '"' && quote != '\'') continue;
+            q++;
+            const char* e = strchr(q, quote);
+            if (!e || e > tag_end) return 0;
+            size_t k = (size_t)(e - q);
+            if (k >= cap) k = cap - 1;
+            memcpy(out, q, k);
+            out[k] = 0;
+            return 1;
+        }
+    }
+    return 0;
+}
+
+typedef struct { char name[128]; double rgb[3]; } light_def;
+
+static int load_xml(orc_scene* s, const char* path, light_def** lights, int* nlights) {
+    char* buf = read_file(path, NULL);
+    if (!buf) { set_err("cannot open %s", path); return 0; }
+    int depth = 0, n = 0, cap = 16, cam_open = 0;
+    light_def* L = (light_def*)malloc(sizeof(light_def) * cap);
+    for (const char* p = buf; (p = strchr(p, '<')) != NULL;) {
+        if (!strncmp(p, "<!--", 4)) { const char* e = strstr(p, "-->"); if (!e) break; p = e + 3; continue; }
+        if (p[1] == '?' || p[1] == '!') { const char* e = strchr(p, '>'); if (!e) break; p = e + 1; continue; }
+        const char* e = strchr(p, '>');
+        if (!e) break;
+        if (p[1] == '/') { depth--; if (depth == 0) cam_open = 0; p = e + 1; continue; }
+        int selfclose = e[-1] == '/';
+        const char* nm = p + 1;
+        size_t nk = strcspn(nm, " \t\r\n/>");
+        if (depth == 0 && nk == 5 && !strncmp(nm, "light", 5)) {
+            char mn[128] = "", rad[256] = "";
+            xml_attr(nm + nk, e, "mtlname", mn, sizeof mn);
+            if (!xml_attr(nm + nk, e, "radiance", rad, sizeof rad)) { set_err("light without radiance"); free(buf); free(L); return 0; }
+            double rgb[3];
+            char* q = rad;
+            for (int c = 0; c < 3; c++) {  /* RadianceRGB(std::string): getline(',') + stod */
+                char* endp;
+                rgb[c] = strtod(q, &endp);
+                if (endp == q) { set_err("bad radiance '%s'", rad); free(buf); free(L); return 0; }
+                q = strchr(endp, ',');
+                q = q ? q + 1 : endp;
+            }
+            int k;
+            for (k = 0; k < n; k++) if (!strcmp(L[k].name, mn)) break;  /* map: later wins */
+            if (k == n) {
+                if (n == cap) { cap *= 2; L = (light_def*)realloc(L, sizeof(light_def) * cap); }
+                snprintf(L[n].name, sizeof L[n].name, "%s", mn);
+                n++;
+            }
+            memcpy(L[k].rgb, rgb, sizeof rgb);
+        } else if (depth == 0 && nk == 6 && !strncmp(nm, "camera", 6)) {
+            char a[64];
+            s->has_cam = 1;
+            s->cam.dist_scale = 1.0;
+            s->cam.up[1] = 1.0;
+            if (xml_attr(nm + nk, e, "width", a, sizeof a)) s->cam.width = atoi(a);
+            if (xml_attr(nm + nk, e, "height", a, sizeof a)) s->cam.height = atoi(a);
+            if (xml_attr(nm + nk, e, "fovy", a, sizeof a)) s->cam.fovy = strtod(a, NULL);
+            cam_open = !selfclose;
+        } else if (depth == 1 && cam_open) {
+            double* dst = NULL;
+            if (nk == 3 && !strncmp(nm, "eye", 3)) dst = s->cam.eye;
+            if (nk == 6 && !strncmp(nm, "lookat", 6)) dst = s->cam.lookat;
+            if (nk == 2 && !strncmp(nm, "up", 2)) dst = s->cam.up;
+            if (dst) {
+                char a[64];
+                if (xml_attr(nm + nk, e, "x", a, sizeof a)) dst[0] = strtod(a, NULL);
+                if (xml_attr(nm + nk, e, "y", a, sizeof a)) dst[1] = strtod(a, NULL);
+                if (xml_attr(nm + nk, e, "z", a, sizeof a)) dst[2] = strtod(a, NULL);
+            }
+        }
+        if (!selfclose) depth++;
+        p = e + 1;
+    }
+    free(buf);
+    *lights = L;
+    *nlights = n;
+    return 1;
+}
+
+static int cmp_light_def(const void* a, const void* b) {
+    return strcmp(((const light_def*)a)->name, ((const light_def*)b)->name);
+}
+
+orc_scene* orc_scene_load(const char* obj_path, const char* xml_path) {
+    orc_scene* s = (orc_scene*)calloc(1, sizeof(orc_scene));
+    light_def* L = NULL;
+    int nl = 0;
+    if (!load_obj(s, obj_path) || !load_xml(s, xml_path, &L, &nl)) { orc_scene_free(s); free(L); return NULL; }
+    for (int f = 0; f < s->F; f++)
+        if (s->mat[f] < 0 || s->mat[f] >= s->M) { set_err("facet %d has no material", f); orc_scene_free(s); free(L); return NULL; }
+    /* gather_light_triangles (Mylight.cpp:32-100): lightsRadiance is a std::map -> name order */
+    qsort(L, (size_t)nl, sizeof(light_def), cmp_light_def);
+    s->light_of = (int*)malloc(sizeof(int) * (s->F + 1));
+    int* lmat = (int*)malloc(sizeof(int) * (s->F + 1));
+    int NL = 0;
+    for (int f = 0; f < s->F; f++) {
+        s->light_of[f] = -1;
+        lmat[f] = -1;
+        for (int k = 0; k < nl; k++)
+            if (!strcmp(s->mtl[s->mat[f]].name, L[k].name)) { lmat[f] = k; NL++; break; }
+    }
+    s->NL = NL;
+    s->lfacet = (int*)malloc(sizeof(int) * (NL + 1));
+    s->larea = (double*)malloc(sizeof(double) * (NL + 1));
+    s->lrad = (double*)malloc(sizeof(double) * 3 * (NL + 1));
+    s->lsum = (double*)malloc(sizeof(double) * (NL + 1));
+    int li = 0;
+    for (int k = 0; k < nl; k++)          /* lightsTriangles map: name order, then facet order */
+        for (int f = 0; f < s->F; f++) {
+            if (lmat[f] != k) continue;
+            v3 a = fvert(s, f, 0), b = fvert(s, f, 1), c = fvert(s, f, 2);
+            v3 n = vcross(vsub(b, a), vsub(c, a));          /* Mylight.cpp:66-69 */
+            n = vmul(n, 1.0 / vnorm(n));
+            s->larea[li] = 0.5 * vdet(vsub(b, a), vsub(c, a), n);
+            memcpy(s->lrad + 3 * li, L[k].rgb, sizeof(double) * 3);
+            s->lsum[li] = L[k].rgb[0] + L[k].rgb[1] + L[k].rgb[2];  /* RadianceRGB::sum */
+            s->lfacet[li] = f;
+            s->light_of[f] = li;
+            li++;
+        }
+    free(lmat);
+    free(L);
+    /* unique normals (Myobj.cpp:680-709) */
+    s->un = (double*)malloc(sizeof(double) * 3 * (s->F + 1));
+    for (int f = 0; f < s->F; f++) {
+        v3 a = fvert(s, f, 0), b = fvert(s, f, 1), c = fvert(s, f, 2);
+        v3 na = vnormalized(fnorm(s, f, 0)), nb = vnormalized(fnorm(s, f, 1)), nc = vnormalized(fnorm(s, f, 2));
+        v3 n = vnormalized(vcross(vsub(b, a), vsub(c, a)));
+        v3 nr = vmul(n, -1);
+        double w = vdot(n, na) + vdot(n, nb) + vdot(n, nc);
+        double wr = vdot(nr, na) + vdot(nr, nb) + vdot(nr, nc);
+        st3(s->un + 3 * f, w > wr ? n : nr);
+    }
+    return s;
+}
+
+void orc_scene_free(orc_scene* s) {
+    if (!s) return;
+    free(s->v); free(s->vn); free(s->mat); free(s->light_of); free(s->un); free(s->mtl);
+    free(s->lfacet); free(s->larea); free(s->lrad); free(s->lsum);
+    free(s->cell_start); free(s->cell_tri);
+    free(s);
+}
+
+void orc_scene_counts(const orc_scene* s, int* nf, int* nm, int* nl) {
+    if (nf) *nf = s->F;
+    if (nm) *nm = s->M;
+    if (nl) *nl = s->NL;
+}
+void orc_scene_facets(const orc_scene* s, float* v18, int* mat, int* light_of, double* un3) {
+    for (int f = 0; f < s->F; f++) {
+        if (v18) { memcpy(v18 + 18 * f, s->v + 9 * f, 36); memcpy(v18 + 18 * f + 9, s->vn + 9 * f, 36); }
+        if (mat) mat[f] = s->mat[f];
+        if (light_of) light_of[f] = s->light_of[f];
+        if (un3) memcpy(un3 + 3 * f, s->un + 3 * f, 24);
+    }
+}
+void orc_scene_materials(const orc_scene* s, float* m7) {
+    for (int m = 0; m < s->M; m++) {
+        memcpy(m7 + 7 * m, s->mtl[m].kd, 12);
+        memcpy(m7 + 7 * m + 3, s->mtl[m].ks, 12);
+        m7[7 * m + 6] = s->mtl[m].ns;
+    }
+}
+void orc_scene_lights(const orc_scene* s, int* facet, double* a4) {
+    for (int l = 0; l < s->NL; l++) {
+        if (facet) facet[l] = s->lfacet[l];
+        if (a4) { a4[4 * l] = s->larea[l]; memcpy(a4 + 4 * l + 1, s->lrad + 3 * l, 24); }
+    }
+}
+int orc_scene_camera(const orc_scene* s, orc_camera* cam) {
+    if (!s->has_cam) return -1;
+    *cam = s->cam;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * uniform grid (Myobj.cpp:78-162)                                                           */
+void orc_grid_build(orc_scene* s, const double cam[3], int n0) {
+    for (int i = 0; i < 3; i++) s->mm[i][0] = s->mm[i][1] = cam[i];
+    for (int f = 0; f < s->F; f++)
+        for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 3; i++) {
+                s->mm[i][0] = fmin(s->mm[i][0], (double)s->v[9 * f + 3 * k + i]);
+                s->mm[i][1] = fmax(s->mm[i][1], (double)s->v[9 * f + 3 * k + i]);
+            }
+    double len[3];
+    for (int i = 0; i < 3; i++) len[i] = s->mm[i][1] - s->mm[i][0];
+    double d = fmax(fmax(len[0], len[1]), len[2]) / pow(n0, 1.0 / 3);
+    s->d = d;
+    s->inv_d = 1.0 / d;
+    for (int i = 0; i < 3; i++) {
+        s->lim[i] = (int)floor(len[i] / d) + 2;  /* Myobj.cpp:405 */
+        s->gd[i] = s->lim[i] + 1;
+    }
+    size_t ncell = (size_t)s->gd[0] * s->gd[1] * s->gd[2];
+    free(s->cell_start);
+    free(s->cell_tri);
+    s->cell_start = (int*)calloc(ncell + 1, sizeof(int));
+    int (*rng)[3][2] = malloc(sizeof(int[3][2]) * (s->F + 1));
+    for (int pass = 0; pass < 2; pass++) {
+        int* fillp = NULL;
+        if (pass == 1) {
+            for (size_t c = 0; c < ncell; c++) s->cell_start[c + 1] += s->cell_start[c];
+            s->cell_tri = (int*)malloc(sizeof(int) * (s->cell_start[ncell] + 1));
+            fillp = (int*)malloc(sizeof(int) * (ncell + 1));
+            memcpy(fillp, s->cell_start, sizeof(int) * ncell);
+        }
+        for (int f = 0; f < s->F; f++) {
+            if (pass == 0) {
+                double xyz[3][2];
+                for (int k = 0; k < 3; k++) { xyz[k][0] = DBL_MAX; xyz[k][1] = -DBL_MAX; }
+                for (int v = 0; v < 3; v++)
+                    for (int i = 0; i < 3; i++) {
+                        xyz[i][0] = fmin(xyz[i][0], (double)s->v[9 * f + 3 * v + i]);
+                        xyz[i][1] = fmax(xyz[i][1], (double)s->v[9 * f + 3 * v + i]);
+                    }
+                for (int k = 0; k < 3; k++) {
+                    rng[f][k][0] = (int)floor((xyz[k][0] - s->mm[k][0]) / d);
+                    rng[f][k][1] = (int)floor((xyz[k][1] - s->mm[k][0]) / d);
+                }
+            }
+            for (int i = rng[f][0][0]; i <= rng[f][0][1]; i++)
+                for (int j = rng[f][1][0]; j <= rng[f][1][1]; j++)
+                    for (int k = rng[f][2][0]; k <= rng[f][2][1]; k++) {
+                        size_t c = ((size_t)i * s->gd[1] + j) * s->gd[2] + k;
+                        if (pass == 0) s->cell_start[c + 1]++;
+                        else s->cell_tri[fillp[c]++] = f;
+                    }
+        }
+        free(fillp);
+    }
+    free(rng);
+    s->grid_ok = 1;
+}
+void orc_grid_info(const orc_scene* s, double* o) {
+    for (int i = 0; i < 3; i++) { o[2 * i] = s->mm[i][0]; o[2 * i + 1] = s->mm[i][1]; }
+    o[6] = s->d;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * ray/triangle (Myobj.cpp:165-192) and the 3D-DDA closest hit (Myobj.cpp:334-474, 476-622)   */
+typedef struct { int hit; double beta, gamma, t; } hitrec;
+
+static inline hitrec tri_hit(const orc_scene* s, v3 ro, v3 rd, int f) {
+    hitrec h = {0, 0, 0, 0};
+    v3 a = fvert(s, f, 0), b = fvert(s, f, 1), c = fvert(s, f, 2);
+    double detA = vdet(vsub(a, b), vsub(a, c), rd);
+    if (fabs(detA) < EPS) return h;
+    double beta = vdet(vsub(a, ro), vsub(a, c), rd) / detA;
+    double gamma = vdet(vsub(a, b), vsub(a, ro), rd) / detA;
+    double t = vdet(vsub(a, b), vsub(a, c), vsub(a, ro)) / detA;
+    if (beta < 0 || gamma < 0 || beta + gamma > 1 || t < 0 || fabs(t) < EPS) return h;
+    h.hit = 1; h.beta = beta; h.gamma = gamma; h.t = t;
+    return h;
+}
+
+/* light_only: Myobj.cpp:476-622 (skip non-light triangles; step every tied axis) */
+static int grid_trace(const orc_scene* s, v3 ro, v3 rd, int exclude, int light_only, hitrec* out) {
+    out->hit = 0;
+    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return -1;  /* reference: UB (Myobj.cpp:463-468) */
+    const double mn[3] = {s->mm[0][0], s->mm[1][0], s->mm[2][0]};
+    v3 x0v = vmul(vsub(ro, mk(mn[0], mn[1], mn[2])), s->inv_d);
+    double xyz0[3] = {x0v.x, x0v.y, x0v.z}, dir[3] = {rd.x, rd.y, rd.z};
+    int xyz[3], sign[3], nxyz[3];
+    double ts[3];
+    for (int i = 0; i < 3; i++) {
+        xyz[i] = (int)floor(xyz0[i]);
+        sign[i] = dir[i] < 0 ? -1 : 1;
+        if (fabs(dir[i]) < EPS) sign[i] = 0;
+    }
+    for (int i = 0; i < 3; i++) {
+        if (sign[i]) {
+            if (fabs(floor(xyz0[i]) - xyz0[i]) < EPS) nxyz[i] = xyz[i] + sign[i];
+            else nxyz[i] = sign[i] > 0 ? (int)ceil(xyz0[i]) : (int)floor(xyz0[i]);
+            ts[i] = (nxyz[i] - xyz0[i]) / dir[i];
+        } else {
+            nxyz[i] = -1;
+            ts[i] = DBL_MAX;
+        }
+    }
+    hitrec best = {0, 0, 0, DBL_MAX};
+    int bestf = -1;
+    for (;;) {
+        for (int i = 0; i < 3; i++)
+            if (xyz[i] < 0 || xyz[i] > s->lim[i]) return -1;
+        size_t c = ((size_t)xyz[0] * s->gd[1] + xyz[1]) * s->gd[2] + xyz[2];
+        for (int q = s->cell_start[c]; q < s->cell_start[c + 1]; q++) {
+            int f = s->cell_tri[q];
+            if (light_only && s->light_of[f] < 0) continue;
+            if (f == exclude) continue;
+            hitrec h = tri_hit(s, ro, rd, f);
+            if (!h.hit) continue;
+            v3 cp = vmul(vsub(vadd(ro, vmul(rd, h.t)), mk(mn[0], mn[1], mn[2])), s->inv_d);
+            if ((int)floor(cp.x) != xyz[0] || (int)floor(cp.y) != xyz[1] || (int)floor(cp.z) != xyz[2]) continue;
+            if (h.t < best.t) { best = h; bestf = f; }
+        }
+        if (best.hit) { *out = best; return bestf; }
+        if (!light_only) {
+            double t = DBL_MAX;
+            int ind = -1;
+            for (int i = 0; i < 3; i++) {
+                if (sign[i] == 0) continue;
+                if (ts[i] < t) { ind = i; t = ts[i]; }
+            }
+            if (ind < 0) return -1;
+            xyz[ind] += sign[ind];
+            nxyz[ind] += sign[ind];
+            ts[ind] = (nxyz[ind] - xyz0[ind]) / dir[ind];
+        } else {
+            double t = DBL_MAX;
+            for (int i = 0; i < 3; i++)
+                if (ts[i] < t) t = ts[i];
+            if (t == DBL_MAX) return -1;
+            for (int i = 0; i < 3; i++)
+                if (fabs(t - ts[i]) < EPS) {
+                    xyz[i] += sign[i];
+                    nxyz[i] += sign[i];
+                    ts[i] = (nxyz[i] - xyz0[i]) / dir[i];
+                }
+        }
+    }
+}
+
+int orc_closest_hit(const orc_scene* s, const double ro[3], const double rd[3], int ex, double* tbg) {
+    hitrec h;
+    int f = grid_trace(s, ld3(ro), ld3(rd), ex, 0, &h);
+    if (tbg) { tbg[0] = h.t; tbg[1] = h.beta; tbg[2] = h.gamma; }
+    return f;
+}
+int orc_closest_light_hit(const orc_scene* s, const double ro[3], const double rd[3], int ex, double* tbg) {
+    hitrec h;
+    int f = grid_trace(s, ld3(ro), ld3(rd), ex, 1, &h);
+    if (tbg) { tbg[0] = h.t; tbg[1] = h.beta; tbg[2] = h.gamma; }
+    return f;
+}
+int orc_intersect_triangle(const orc_scene* s, const double ro[3], const double rd[3], int f, double* tbg) {
+    hitrec h = tri_hit(s, ld3(ro), ld3(rd), f);
+    if (tbg) { tbg[0] = h.t; tbg[1] = h.beta; tbg[2] = h.gamma; }
+    return h.hit ? f : -1;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * RNG.  RefRng: the reference's clock-seeded std::default_random_engine (libstdc++ minstd_rand0)
+ * per RNG site, replayed from oracle/fakeclock.h's counter; generate_canonical<double,53> = two
+ * draws (random.tcc:3348-3380); discrete_distribution = normalised partial sums with the last
+ * forced to 1, lower_bound (random.tcc:2656-2712).  CounterRng: stateless hash keyed by
+ * (seed, pixel, sample, node, dim), identical on the GPU (monte_carlo_path_tracing_amd/csrc).  */
+typedef struct { uint64_t x; } minstd;
+
+static minstd ref_engine(uint64_t* ctr) {
+    uint64_t z = (++*ctr) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    unsigned seed = (unsigned)(long long)(z >> 1);  /* unsigned seed1 = ...count() */
+    minstd e;
+    e.x = (uint64_t)seed % 2147483647ull;
+    if (e.x == 0) e.x = 1;
+    return e;
+}
+static inline uint64_t minstd_next(minstd* e) {
+    e->x = (e->x * 16807ull) % 2147483647ull;
+    return e->x;
+}
+static double canon(minstd* e) {
+    const long double r = 2147483646.0L;
+    double sum = 0, tmp = 1;
+    for (int k = 0; k < 2; k++) {
+        sum += (double)(minstd_next(e) - 1) * tmp;
+        tmp = (double)((long double)tmp * r);
+    }
+    double ret = sum / tmp;
+    if (ret >= 1.0) ret = nextafter(1.0, 0.0);
+    return ret;
+}
+
+static inline uint64_t mix64(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+static inline uint64_t counter_key(uint64_t seed, uint64_t pixel, uint64_t sample, uint64_t node) {
+    uint64_t k = mix64(seed + 0x9E3779B97F4A7C15ull * (pixel + 1));
+    k = mix64(k ^ (0xD1B54A32D192ED03ull * (sample + 1)));
+    return mix64(k ^ (0xA24BAED4963EE407ull * node));
+}
+static inline double counter_u(uint64_t key, uint32_t dim) {
+    return (double)(mix64(key + 0x9FB21C651E98DF25ull * (dim + 1)) >> 11) * 0x1.0p-53;
+}
+double orc_counter_uniform(uint64_t seed, uint64_t pixel, uint64_t sample, uint64_t node, uint32_t dim) {
+    return counter_u(counter_key(seed, pixel, sample, node), dim);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Phong BRDF (BRDF.cpp)                                                                      */
+static v3 brdf_phong(v3 n, v3 wi, v3 wr, v3 kd, v3 ks, double sh) { /* BRDF.cpp:17-25 */
+    v3 R = vadd(vmul(wi, -1), vmul(n, 2 * vdot(wi, n)));
+    v3 ans = vmul(kd, 1.0 / PI);
+    if (vdot(wr, R) > 0) ans = vadd(ans, vmul(ks, (sh + 1) * pow(vdot(wr, R), sh) / (2 * PI)));
+    return ans;
+}
+static double phong_pdf(v3 n, v3 wi, v3 wr, v3 kd, v3 ks, double sh) { /* BRDF.cpp:107-133 */
+    double d = vdot(kd, mk(1, 1, 1)) / 3;
+    double s = vdot(ks, mk(1, 1, 1)) / 3;
+    double sum = d + s;
+    double prob_d = d / sum, prob_s = s / sum;
+    double cosT = vdot(wi, n);
+    if (cosT < 0) prob_d *= 0;
+    else prob_d *= cosT / PI;
+    v3 R = vnormalized(vadd(vmul(wr, -1), vmul(n, 2 * vdot(wr, n))));
+    double cosS = vdot(wi, R);
+    if (cosS < 0) prob_s *= 0;
+    else prob_s *= (sh + 1) / (2 * PI) * pow(cosS, sh);
+    return prob_d + prob_s;
+}
+/* sample_from_phong (BRDF.cpp:28-104) given the lobe-pick uniform and xi1, xi2 */
+static v3 sample_phong(v3 n, v3 wr, v3 kd, v3 ks, double sh, double u0, double k1, double k2, double* pdf_out) {
+    double d = vdot(kd, mk(1, 1, 1)) / 3;
+    double s = vdot(ks, mk(1, 1, 1)) / 3;
+    double sum = 0.0;
+    sum += d;
+    sum += s;
+    double p0 = d / sum, p1 = s / sum;
+    int ind = (p0 >= u0) ? 0 : 1;  /* lower_bound over {p0, 1.0} */
+    double pdf = 1;
+    pdf *= ind == 0 ? p0 : p1;
+    /* the compiled reference evaluates sin/cos of theta and of phi with glibc sincos()
+     * (BRDF.o has 4 sincos and no cos/sin calls); the pdf's cos(theta) is that value */
+    v3 axis = n;
+    double theta, st, ct, sp, cp;
+    double phi = 2 * PI * k2;
+    if (ind == 0) {
+        theta = 0.5 * acos(fmax(-1, fmin(1, 1 - 2 * k1)));
+        sincos(theta, &st, &ct);
+        pdf *= ct / PI;
+    } else {
+        theta = acos(fmax(-1, fmin(1, pow(k1, 1 / (sh + 1)))));
+        sincos(theta, &st, &ct);
+        pdf *= (sh + 1) / (2 * PI) * pow(k1, sh / (sh + 1));
+        axis = vnormalized(vadd(vmul(wr, -1), vmul(n, 2 * vdot(wr, n))));
+    }
+    sincos(phi, &sp, &cp);
+    v3 nx;
+    if (fabs(vdot(axis, mk(1, 0, 0)) - 1) > EPS) nx = vnormalized(vcross(axis, mk(1, 0, 0)));
+    else nx = vnormalized(vcross(axis, mk(0, 1, 0)));
+    v3 ny = vnormalized(vcross(axis, nx));
+    v3 dir = vnormalized(mat_cols_mul(nx, ny, axis, mk(st * cp, st * sp, ct)));
+    *pdf_out = pdf;
+    return dir;
+}
+
+void orc_brdf_phong(const double n[3], const double wi[3], const double wr[3], const double kd[3],
+                    const double ks[3], double ns, double rgb[3]) {
+    st3(rgb, brdf_phong(ld3(n), ld3(wi), ld3(wr), ld3(kd), ld3(ks), ns));
+}
+double orc_phong_pdf(const double n[3], const double wi[3], const double wr[3], const double kd[3],
+                     const double ks[3], double ns) {
+    return phong_pdf(ld3(n), ld3(wi), ld3(wr), ld3(kd), ld3(ks), ns);
+}
+void orc_sample_phong_ref(uint64_t ctr, const double n[3], const double wr[3], const double kd[3],
+                          const double ks[3], double ns, double o[4]) {
+    minstd e = ref_engine(&ctr);
+    double u0 = canon(&e), u1 = canon(&e), u2 = canon(&e);
+    double pdf;
+    v3 d = sample_phong(ld3(n), ld3(wr), ld3(kd), ld3(ks), ns, u0, u1, u2, &pdf);
+    st3(o, d);
+    o[3] = pdf;
+}
+void orc_sample_phong_u(const double n[3], const double wr[3], const double kd[3], const double ks[3],
+                        double ns, double u0, double u1, double u2, double o[4]) {
+    double pdf;
+    v3 d = sample_phong(ld3(n), ld3(wr), ld3(kd), ld3(ks), ns, u0, u1, u2, &pdf);
+    st3(o, d);
+    o[3] = pdf;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * staged spherical-triangle light sampling (Mylight.cpp:322-493)                            */
+typedef struct { v3 A, B, C; double alpha, c, sA, w; } sphtri;
+
+/* one light triangle at (x1, n): the cull chain and weight of Mylight.cpp:335-413 */
+static int light_tri_eval(const orc_scene* s, int li, v3 x1, v3 n, sphtri* o) {
+    int f = s->lfacet[li];
+    v3 p0 = fvert(s, f, 0), p1 = fvert(s, f, 1), p2 = fvert(s, f, 2);
+    v3 nl = ld3(s->un + 3 * f);
+    double tmp = vdot(nl, vsub(x1, p0));
+    if (tmp < 0 || fabs(tmp) < EPS) return 0;
+    double t0 = vdot(n, vsub(p0, x1)), t1 = vdot(n, vsub(p1, x1)), t2 = vdot(n, vsub(p2, x1));
+    if ((t0 < 0 || fabs(t0) < EPS) && (t1 < 0 || fabs(t1) < EPS) && (t2 < 0 || fabs(t2) < EPS)) return 0;
+    v3 A = vnormalized(vsub(p0, x1)), B = vnormalized(vsub(p1, x1)), C = vnormalized(vsub(p2, x1));
+    if (vdot(vcross(vnormalized(vsub(C, A)), vnormalized(vsub(B, A))), n) < 0) { v3 t = B; B = C; C = t; }
+    double a = acos(fmax(-1, fmin(1, vdot(B, C))));
+    double b = acos(fmax(-1, fmin(1, vdot(A, C))));
+    double c = acos(fmax(-1, fmin(1, vdot(A, B))));
+    if (a < EPS || b < EPS || c < EPS) return 0;
+    double alpha = acos(fmax(-1, fmin(1, -vdot(vnormalized(vcross(B, A)), vnormalized(vcross(A, C))))));
+    double beta = acos(fmax(-1, fmin(1, -vdot(vnormalized(vcross(C, B)), vnormalized(vcross(B, A))))));
+    double gamma = acos(fmax(-1, fmin(1, -vdot(vnormalized(vcross(A, C)), vnormalized(vcross(C, B))))));
+    if (alpha < EPS || beta < EPS || gamma < EPS) return 0;
+    double sA = alpha + beta + gamma - PI;
+    if (sA < 0) return 0;
+    double w = sA * s->lsum[li];
+    if (w < 0) return 0;
+    if (isinf(w) || isnan(w)) return 0;
+    if (o) { o->A = A; o->B = B; o->C = C; o->alpha = alpha; o->c = c; o->sA = sA; o->w = w; }
+    return 1;
+}
+
+typedef struct {
+    int count;
+    double wsum;
+    int* idx;          /* survivors' light indices, in order */
+    sphtri* st;        /* survivors' spherical triangles */
+    unsigned* member;  /* per light index: == gen if survived the last prep */
+    unsigned gen;
+} light_state;
+
+static void ls_init(light_state* L, int NL) {
+    L->count = 0;
+    L->wsum = 0;
+    L->idx = (int*)malloc(sizeof(int) * (NL + 1));
+    L->st = (sphtri*)malloc(sizeof(sphtri) * (NL + 1));
+    L->member = (unsigned*)calloc((size_t)NL + 1, sizeof(unsigned));
+    L->gen = 0;
+}
+static void ls_free(light_state* L) { free(L->idx); free(L->st); free(L->member); }
+
+static void light_prep(const orc_scene* s, v3 x1, v3 n, light_state* L) { /* Mylight.cpp:322-422 */
+    L->count = 0;
+    L->wsum = 0;
+    L->gen++;
+    for (int li = 0; li < s->NL; li++) {
+        sphtri t;
+        if (!light_tri_eval(s, li, x1, n, &t)) continue;
+        L->idx[L->count] = li;
+        L->st[L->count] = t;
+        L->count++;
+        L->member[li] = L->gen;
+        L->wsum += t.w;
+    }
+}
+
+/* lights_spherical_triangle_sampling (Mylight.cpp:424-482) after the pick.  out: light index
+ * (-1 dummy), coord, prob */
+static int light_sample_after_pick(const orc_scene* s, const light_state* L, int rind, v3 x1,
+                                   double ksi1, double ksi2, v3* coord, double* prob) {
+    const sphtri* st = &L->st[rind];
+    double sA1 = ksi1 * st->sA;
+    double ss, tt, sa, ca;  /* glibc sincos, as in the compiled reference (Mylight.o) */
+    sincos(sA1 - st->alpha, &ss, &tt);
+    sincos(st->alpha, &sa, &ca);
+    double u = tt - ca;
+    double v = ss + sa * cos(st->c);
+    double q = ((v * tt - u * ss) * ca - v) / ((v * ss + u * tt) * sa);
+    v3 C1 = vnormalized(vadd(vmul(st->A, q), vmul(vnormalized(vsub(st->C, vmul(st->A, vdot(st->C, st->A)))), sqrt(1 - q * q))));
+    double z = 1 - ksi2 * (1 - vdot(C1, st->B));
+    v3 P = vnormalized(vadd(vmul(st->B, z), vmul(vnormalized(vsub(C1, vmul(st->B, vdot(C1, st->B)))), sqrt(1 - z * z))));
+    int li = L->idx[rind];
+    hitrec h = tri_hit(s, x1, P, s->lfacet[li]);
+    *coord = vadd(x1, vmul(P, h.t));  /* h.t = 0 on a miss: coord = x1 (reference quirk) */
+    *prob = s->lsum[li] / L->wsum;
+    return li;
+}
+
+/* reference discrete pick: normalised partial sums, last forced to 1, lower_bound */
+static int ref_pick(const light_state* L, double u) {
+    if (L->count < 2) return 0;
+    double sum = 0.0;
+    for (int i = 0; i < L->count; i++) sum += L->st[i].w;
+    double cp = 0;
+    for (int i = 0; i < L->count; i++) {
+        double p = L->st[i].w / sum;
+        cp = (i == 0) ? p : cp + p;
+        if (i == L->count - 1) cp = 1.0;
+        if (!(cp < u)) return i;
+    }
+    return L->count - 1;
+}
+/* counter-RNG pick: first survivor with cumulative weight >= u * wsum (GPU rule) */
+static int counter_pick(const light_state* L, double u) {
+    double target = u * L->wsum, cum = 0;
+    for (int i = 0; i < L->count; i++) {
+        cum += L->st[i].w;
+        if (cum >= target) return i;
+    }
+    return L->count - 1;
+}
+
+double orc_light_prep(const orc_scene* s, const double x1[3], const double n[3], int* count, int* idx, double* w) {
+    light_state L;
+    ls_init(&L, s->NL);
+    light_prep(s, ld3(x1), ld3(n), &L);
+    if (count) *count = L.count;
+    for (int i = 0; i < L.count; i++) {
+        if (idx) idx[i] = L.idx[i];
+        if (w) w[i] = L.st[i].w;
+    }
+    double ws = L.wsum;
+    ls_free(&L);
+    return ws;
+}
+void orc_light_sample_ref(const orc_scene* s, uint64_t ctr, const double x1p[3], const double np[3], double out[6]) {
+    light_state L;
+    ls_init(&L, s->NL);
+    v3 x1 = ld3(x1p), n = ld3(np);
+    light_prep(s, x1, n, &L);
+    uint64_t c0 = ctr;
+    if (L.count == 0 || fabs(L.wsum) < EPS) {
+        v3 co = vadd(vmul(n, -1), x1);
+        out[0] = -1; out[1] = co.x; out[2] = co.y; out[3] = co.z; out[4] = 1; out[5] = 0;
+    } else {
+        minstd e = ref_engine(&ctr);
+        int rind = 0;
+        if (L.count >= 2) rind = ref_pick(&L, canon(&e));
+        double k1 = canon(&e), k2 = canon(&e);
+        v3 co;
+        double prob;
+        int li = light_sample_after_pick(s, &L, rind, x1, k1, k2, &co, &prob);
+        out[0] = s->lfacet[li]; out[1] = co.x; out[2] = co.y; out[3] = co.z; out[4] = prob;
+        out[5] = (double)(ctr - c0);
+    }
+    ls_free(&L);
+}
+void orc_light_sample_u(const orc_scene* s, const double x1p[3], const double np[3], double u, double k1,
+                        double k2, double out[6]) {
+    light_state L;
+    ls_init(&L, s->NL);
+    v3 x1 = ld3(x1p), n = ld3(np);
+    light_prep(s, x1, n, &L);
+    if (L.count == 0 || fabs(L.wsum) < EPS) {
+        v3 co = vadd(vmul(n, -1), x1);
+        out[0] = -1; out[1] = co.x; out[2] = co.y; out[3] = co.z; out[4] = 1;
+    } else {
+        v3 co;
+        double prob;
+        int li = light_sample_after_pick(s, &L, counter_pick(&L, u), x1, k1, k2, &co, &prob);
+        out[0] = s->lfacet[li]; out[1] = co.x; out[2] = co.y; out[3] = co.z; out[4] = prob;
+    }
+    out[5] = L.wsum;
+    ls_free(&L);
+}
+double orc_light_pdf(const orc_scene* s, const double x1[3], const double n[3], int facet) {
+    int li = s->light_of[facet];
+    if (li < 0) return 0;
+    light_state L;
+    ls_init(&L, s->NL);
+    light_prep(s, ld3(x1), ld3(n), &L);
+    double r = 0;
+    if (L.member[li] == L.gen && !(fabs(L.wsum) < EPS)) r = s->lsum[li] / L.wsum;  /* Mylight.cpp:484-493 */
+    ls_free(&L);
+    return r;
+}
+
+void orc_tone_map(const double rgb[3], double maxr, double gamma, int out[3]) { /* RadianceRGB.cpp:51-67 */
+    double A = pow(maxr, -gamma);
+    for (int i = 0; i < 3; i++) {
+        double r = A * pow(rgb[i], gamma);
+        double x = floor(r * 255 + 0.5);
+        int v = (x >= -2147483648.0 && x < 2147483648.0) ? (int)x : (int)0x80000000u; /* x86 cvttsd2si */
+        out[i] = v > 255 ? 255 : (v < 0 ? 0 : v);
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * camera (main.cpp:507-510, 547-564 generalised to W x H: pixellen = tan(fovy/360)|w|/(H/2))  */
+typedef struct { v3 eye, U, V, N; double wlen, pixellen; int W, H; } cam_frame;
+static cam_frame cam_setup(const orc_camera* c) {
+    cam_frame f;
+    v3 start = ld3(c->eye);
+    v3 w = vsub(ld3(c->lookat), start);
+    start = vsub(start, vmul(w, c->dist_scale - 1));
+    w = vmul(w, c->dist_scale);
+    f.eye = start;
+    f.wlen = vnorm(w);
+    f.pixellen = tan(c->fovy / 360) * vnorm(w) / (c->height / 2.0);
+    f.N = vnormalized(w);
+    f.V = vnormalized(vcross(f.N, ld3(c->up)));
+    f.U = vnormalized(vcross(f.V, f.N));
+    f.W = c->width;
+    f.H = c->height;
+    return f;
+}
+static v3 cam_dir(const cam_frame* f, int i, int j) {
+    v3 delta = mk(-f->pixellen * (i - (f->H - 1) / 2.0), f->pixellen * (j - (f->W - 1) / 2.0), 0);
+    return vnormalized(mat_cols_mul(f->U, f->V, f->N, vadd(delta, mk(0, 0, f->wlen))));
+}
+void orc_camera_ray(const orc_camera* cam, int i, int j, double eye[3], double dir[3]) {
+    cam_frame f = cam_setup(cam);
+    st3(eye, f.eye);
+    st3(dir, cam_dir(&f, i, j));
+}
+
+/* ------------------------------------------------------------------------------------------
+ * integrators (main.cpp:348-399, 402-494)                                                    */
+typedef struct {
+    const orc_scene* s;
+    int rng;          /* ORC_RNG_REF / ORC_RNG_COUNTER */
+    uint64_t ctr;     /* RefRng clock counter */
+    uint64_t seed, pixel, sample;
+    light_state L;    /* RefRng: the global Mylight member state (stale-pdf quirk) */
+    uint64_t stats[4]; /* shading nodes, light preps, extension rays, light-only rays */
+} ctx;
+
+static v3 rgb_mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+
+static v3 shade_brdf(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t node) {
+    const orc_scene* s = C->s;
+    if (C->rng == ORC_RNG_COUNTER && node > COUNTER_MAX_DEPTH + 1) return mk(0, 0, 0); /* path: node = depth+1 */
+    C->stats[0]++;
+    double a0 = 1.0 - beta - gamma;
+    v3 p = vadd(vadd(vmul(fvert(s, f, 0), a0), vmul(fvert(s, f, 1), beta)), vmul(fvert(s, f, 2), gamma));
+    v3 N = vnormalized(vadd(vadd(vmul(fnorm(s, f, 0), a0), vmul(fnorm(s, f, 1), beta)), vmul(fnorm(s, f, 2), gamma)));
+    if (vdot(N, wo) < 0) return mk(0, 0, 0);
+    int li = s->light_of[f];
+    if (li >= 0) return ld3(s->lrad + 3 * li);
+    const material* m = &s->mtl[s->mat[f]];
+    v3 kd = mk(m->kd[0], m->kd[1], m->kd[2]), ks = mk(m->ks[0], m->ks[1], m->ks[2]);
+    double sh = m->ns;
+    uint64_t key = 0;
+    double ksi;
+    if (C->rng == ORC_RNG_REF) {
+        minstd e = ref_engine(&C->ctr);
+        ksi = canon(&e);
+    } else {
+        key = counter_key(C->seed, C->pixel, C->sample, node);
+        ksi = counter_u(key, 0);
+    }
+    if (ksi > P_RR) return mk(0, 0, 0);
+    double u0, u1, u2, pdf;
+    if (C->rng == ORC_RNG_REF) {
+        minstd e = ref_engine(&C->ctr);
+        u0 = canon(&e); u1 = canon(&e); u2 = canon(&e);
+    } else {
+        u0 = counter_u(key, 4); u1 = counter_u(key, 5); u2 = counter_u(key, 6);
+    }
+    v3 wi = sample_phong(N, wo, kd, ks, sh, u0, u1, u2, &pdf);
+    if (vdot(wi, N) < 0) return mk(0, 0, 0);
+    hitrec h;
+    C->stats[2]++;
+    int g = grid_trace(s, p, wi, f, 0, &h);
+    if (g < 0) return mk(0, 0, 0);
+    v3 brdf = brdf_phong(N, wi, wo, kd, ks, sh);
+    v3 Li = shade_brdf(C, g, h.beta, h.gamma, vmul(wi, -1), node + 1);
+    return vmul(rgb_mul(Li, brdf), vdot(wi, N) / pdf / P_RR);
+}
+
+static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t node) {
+    const orc_scene* s = C->s;
+    if (C->rng == ORC_RNG_COUNTER && node >= ((uint64_t)2 << COUNTER_MAX_DEPTH)) return mk(0, 0, 0); /* heap id */
+    C->stats[0]++;
+    double a0 = 1.0 - beta - gamma;
+    v3 p = vadd(vadd(vmul(fvert(s, f, 0), a0), vmul(fvert(s, f, 1), beta)), vmul(fvert(s, f, 2), gamma));
+    v3 N = vnormalized(vadd(vadd(vmul(fnorm(s, f, 0), a0), vmul(fnorm(s, f, 1), beta)), vmul(fnorm(s, f, 2), gamma)));
+    if (vdot(N, wo) < 0) return mk(0, 0, 0);
+    int lf = s->light_of[f];
+    if (lf >= 0) return ld3(s->lrad + 3 * lf);
+    const material* m = &s->mtl[s->mat[f]];
+    v3 kd = mk(m->kd[0], m->kd[1], m->kd[2]), ks = mk(m->ks[0], m->ks[1], m->ks[2]);
+    double sh = m->ns;
+    uint64_t key = 0;
+    double ksi;
+    if (C->rng == ORC_RNG_REF) {
+        minstd e = ref_engine(&C->ctr);
+        ksi = canon(&e);
+    } else {
+        key = counter_key(C->seed, C->pixel, C->sample, node);
+        ksi = counter_u(key, 0);
+    }
+    if (ksi > P_RR) return mk(0, 0, 0);
+
+    /* light branch (main.cpp:443-466) */
+    v3 L_light = mk(0, 0, 0);
+    C->stats[1]++;
+    light_prep(s, p, N, &C->L);
+    double wsum_here = C->L.wsum;
+    v3 coord;
+    double lprob = 1;
+    if (C->L.count == 0 || fabs(C->L.wsum) < EPS) {
+        coord = vadd(vmul(N, -1), p);
+    } else {
+        double u, k1, k2;
+        int rind;
+        if (C->rng == ORC_RNG_REF) {
+            minstd e = ref_engine(&C->ctr);
+            rind = C->L.count >= 2 ? ref_pick(&C->L, canon(&e)) : 0;
+            k1 = canon(&e);
+            k2 = canon(&e);
+        } else {
+            u = counter_u(key, 1);
+            rind = counter_pick(&C->L, u);
+            k1 = counter_u(key, 2);
+            k2 = counter_u(key, 3);
+        }
+        light_sample_after_pick(s, &C->L, rind, p, k1, k2, &coord, &lprob);
+    }
+    v3 wl = vnormalized(vsub(coord, p));
+    if (vdot(wl, N) > 0) {
+        hitrec h;
+        C->stats[2]++;
+        int g = grid_trace(s, p, wl, f, 0, &h);
+        if (g >= 0) {
+            v3 brdf = brdf_phong(N, wl, wo, kd, ks, sh);
+            double ppdf = phong_pdf(N, wl, wo, kd, ks, sh);
+            v3 Li = shade_mis(C, g, h.beta, h.gamma, vmul(wl, -1), 2 * node);
+            L_light = vmul(rgb_mul(Li, brdf), vdot(wl, N) / (lprob + ppdf) / P_RR);
+        }
+    }
+    /* BRDF branch (main.cpp:469-493) */
+    v3 L_brdf = mk(0, 0, 0);
+    double u0, u1, u2, pdf;
+    if (C->rng == ORC_RNG_REF) {
+        minstd e = ref_engine(&C->ctr);
+        u0 = canon(&e); u1 = canon(&e); u2 = canon(&e);
+    } else {
+        u0 = counter_u(key, 4); u1 = counter_u(key, 5); u2 = counter_u(key, 6);
+    }
+    v3 wi = sample_phong(N, wo, kd, ks, sh, u0, u1, u2, &pdf);
+    if (vdot(wi, N) < 0) return vadd(L_light, L_brdf);
+    hitrec h;
+    C->stats[2]++;
+    int g = grid_trace(s, p, wi, f, 0, &h);
+    if (g >= 0) {
+        v3 brdf = brdf_phong(N, wi, wo, kd, ks, sh);
+        double light_pdf = 0;
+        hitrec hl;
+        C->stats[3]++;
+        int lg = grid_trace(s, p, wi, f, 1, &hl);
+        if (lg >= 0) {
+            int li = s->light_of[lg];
+            if (C->rng == ORC_RNG_REF) {  /* stale state, as the reference (Mylight.cpp:484-493) */
+                if (C->L.member[li] == C->L.gen && !(fabs(C->L.wsum) < EPS)) light_pdf = s->lsum[li] / C->L.wsum;
+            } else {                       /* fresh: this node's own prep */
+                if (!(fabs(wsum_here) < EPS) && light_tri_eval(s, li, p, N, NULL)) light_pdf = s->lsum[li] / wsum_here;
+            }
+        }
+        v3 Li = shade_mis(C, g, h.beta, h.gamma, vmul(wi, -1), 2 * node + 1);
+        L_brdf = vmul(rgb_mul(Li, brdf), vdot(wi, N) / (pdf + light_pdf) / P_RR);
+    }
+    return vadd(L_light, L_brdf);
+}
+
+static void ctx_init(ctx* C, const orc_scene* s, int rng) {
+    memset(C, 0, sizeof *C);
+    C->s = s;
+    C->rng = rng;
+    ls_init(&C->L, s->NL);
+}
+
+void orc_shade_sample(const orc_scene* s, const orc_camera* cam, int mode, int rng, uint64_t ctr_or_seed,
+                      int i, int j, int sample, double rgb[3], uint64_t* draws) {
+    ctx C;
+    ctx_init(&C, s, rng);
+    if (rng == ORC_RNG_REF) C.ctr = ctr_or_seed;
+    else C.seed = ctr_or_seed;
+    C.pixel = (uint64_t)i * cam->width + j;
+    C.sample = (uint64_t)sample;
+    cam_frame fr = cam_setup(cam);
+    v3 dir = cam_dir(&fr, i, j);
+    hitrec h;
+    int f = grid_trace(s, fr.eye, dir, -1, 0, &h);
+    v3 L = mk(0, 0, 0);
+    if (f >= 0) {
+        if (mode == ORC_MODE_MIS) L = shade_mis(&C, f, h.beta, h.gamma, vmul(dir, -1), 1);
+        else L = shade_brdf(&C, f, h.beta, h.gamma, vmul(dir, -1), 1);
+    }
+    st3(rgb, L);
+    if (draws) *draws = C.ctr - ctr_or_seed;
+    ls_free(&C.L);
+}
+
+int orc_render(const orc_scene* s, const orc_camera* cam, int mode, uint64_t seed, int spp, int s0, int s1,
+               int stride, int offset, int nthreads, double* out, uint64_t* stats4) {
+    if (!s->grid_ok) { set_err("grid not built"); return -1; }
+    cam_frame fr = cam_setup(cam);
+    const int W = cam->width, H = cam->height;
+    if (stride < 1) stride = 1;
+    int nx = (W - offset + stride - 1) / stride, ny = (H - offset + stride - 1) / stride;
+    if (nx < 0) nx = 0;
+    if (ny < 0) ny = 0;
+    long npx = (long)nx * ny;
+    uint64_t tot[4] = {0, 0, 0, 0};
+    const double inv = 1.0 / spp;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+    {
+        ctx C;
+        ctx_init(&C, s, ORC_RNG_COUNTER);
+        C.seed = seed;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+        for (long q = 0; q < npx; q++) {
+            int i = offset + (int)(q / nx) * stride, j = offset + (int)(q % nx) * stride;
+            v3 dir = cam_dir(&fr, i, j);
+            hitrec h;
+            int f = grid_trace(s, fr.eye, dir, -1, 0, &h);
+            double* px = out + 3 * ((size_t)i * W + j);
+            v3 sum = mk(px[0], px[1], px[2]);
+            if (f >= 0) {
+                C.pixel = (uint64_t)i * W + j;
+                for (int k = s0; k < s1; k++) {
+                    C.sample = (uint64_t)k;
+                    v3 L = mode == ORC_MODE_MIS ? shade_mis(&C, f, h.beta, h.gamma, vmul(dir, -1), 1)
+                                                : shade_brdf(&C, f, h.beta, h.gamma, vmul(dir, -1), 1);
+                    sum = vadd(sum, vmul(L, inv));  /* main.cpp:575-576 */
+                }
+            }
+            st3(px, sum);
+        }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        for (int k = 0; k < 4; k++) tot[k] += C.stats[k];
+        ls_free(&C.L);
+    }
+    if (stats4) for (int k = 0; k < 4; k++) stats4[k] = tot[k];
+    return 0;
+}
