@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the MI355X path tracer on the Veach-MIS stand-in (BASELINE.json).
+
+Workload (BASELINE.json configs[2]): MIS (light + BRDF sampling), 800x600, frame of
+steps x gpus x spp_per_step samples per pixel (default 128 x 1 x 8 = 1024 spp).  A "step" is one
+pass of the hot path over one batch: spp_per_step samples of every pixel of the 800x600 frame,
+rendered by the wavefront kernels into an fp64 framebuffer resident in HBM.
+
+Multi-GPU (torchrun, one process per GPU): weak scaling by sample-range sharding -- rank r renders
+global samples [(k*G + r)*S, (k*G + r + 1)*S) in step k -- and ONE RCCL reduce of the framebuffer
+inside the timed region (monte_carlo_path_tracing_amd/shard.py).
+
+Also reported: the roofline of the dominant kernel (k_prep: fp64 VALU-bound light prep), the
+CPU baseline (the C oracle on a bounded stratified pixel subset, rank 0, N=1 only) and the
+relative L2 of the GPU frame against that CPU render on the same pixels and samples.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/sec (whole node) + per-pixel L2 vs CPU, Veach-MIS 800×600@1024spp"
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (spec); see DESIGN.md §roofline
+HBM_PEAK_GBS = 8000.0
+# algorithmic fp64 operations of one light-triangle evaluation of Mylight.cpp:335-413 by the
+# stage at which it ends (+,-,*,/,sqrt,acos,fmin/fmax each 1)
+FLOPS_CULL_BACKFACE = 8
+FLOPS_CULL_PLANE = 32
+FLOPS_FULL = 269
+SCENE = os.path.join(ROOT, "scenes", "veach-mis")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(W, H, mode, seed, target_s):
+    """The C oracle (oracle/liboracle.so), 1 thread, every 20th pixel in x and y, at an spp chosen
+    so that the run takes about target_s seconds.  Returns (dict, subset image, spp)."""
+    from oracle import pyoracle as po
+
+    osc = po.Scene(SCENE + "/veach-mis.obj", SCENE + "/veach-mis.xml")
+    ocam = po.reference_camera(W, H)
+    e, _ = po.camera_ray(ocam, 0, 0)
+    osc.build_grid(e)
+    m = po.MODE_MIS if mode == "mis" else po.MODE_BRDF
+    t = time.perf_counter()
+    osc.render(ocam, m, seed, 1, stride=20, offset=7, nthreads=1)
+    t1 = time.perf_counter() - t
+    spp = int(max(1, min(256, target_s / max(t1, 1e-3))))
+    t = time.perf_counter()
+    img, _ = osc.render(ocam, m, seed, spp, stride=20, offset=7, nthreads=1)
+    dt = time.perf_counter() - t
+    npx = len(range(7, H, 20)) * len(range(7, W, 20))
+    return ({"value": npx * spp / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+             "sample": "oracle/mcpt_oracle.c (fp64 C restatement incl. the reference's uniform grid), "
+                       "1 thread, every 20th pixel in x and y of %dx%d (%d px) x %d spp %s = %d camera samples "
+                       "in %.1f s" % (W, H, npx, spp, mode.upper(), npx * spp, dt)}, img, spp)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--spp-per-step", type=int, default=8)
+    ap.add_argument("--width", type=int, default=800)
+    ap.add_argument("--height", type=int, default=600)
+    ap.add_argument("--mode", default="mis", choices=["mis", "brdf"])
+    ap.add_argument("--seed", type=int, default=20240430)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and L2 check")
+    ap.add_argument("--out", default="", help="optional .bmp of the rendered frame (rank 0)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+
+    import monte_carlo_path_tracing_amd as mcpt
+    from monte_carlo_path_tracing_amd.shard import reduce_framebuffers
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    W, H, S = args.width, args.height, args.spp_per_step
+    frame_spp = args.steps * world * S
+    scene = mcpt.Scene.load(SCENE + "/veach-mis.obj", SCENE + "/veach-mis.xml")
+    cam = mcpt.Camera.reference(W, H)
+    fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    scratch = torch.zeros_like(fb)
+
+    for k in range(args.warmup):  # warmup renders go to a scratch buffer
+        mcpt.render_device(scene, cam, S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
+                           sample_range=(0, S), device=local)
+    totals = {}
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tlog = t0
+    for k in range(args.steps):
+        s0 = (k * world + rank) * S
+        st = mcpt.render_device(scene, cam, frame_spp, fb.data_ptr(), mode=args.mode, seed=args.seed,
+                                sample_range=(s0, s0 + S), device=local)
+        for key, v in st.as_dict().items():
+            totals[key] = totals.get(key, 0) + v
+        if rank == 0 and time.perf_counter() - tlog > 30:
+            tlog = time.perf_counter()
+            log("step %d/%d, %.1f s" % (k + 1, args.steps, tlog - t0))
+    if world > 1:
+        reduce_framebuffers(fb, dist, dst=0)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    samples = float(W * H) * frame_spp
+    value = samples / elapsed / 1e6
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    # ---- roofline of the dominant kernel (rank 0's launches; HIP events on its stream) ----
+    ev_tot, c1, c2, surv = (totals.get(k, 0) for k in ("light_evals_total", "light_evals_culled_backface",
+                                                         "light_evals_culled_plane", "light_evals_survived"))
+    launches = max(totals.get("prep_launches", 0), 1)
+    prep_s = totals.get("prep_seconds", 0.0)
+    flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + (ev_tot - c1 - c2) * FLOPS_FULL
+    if args.mode == "mis" and prep_s > 0:
+        achieved = flops / launches / (prep_s / launches) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "k_prep_hbm_bytes_per_node.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                per_node = json.load(f).get("hbm_bytes_per_node")
+            nodes = totals.get("shading_nodes", 0)
+            traffic = per_node * nodes / launches if per_node is not None else None
+        roofline = {"bound": "valu_fp64", "kernel": "k_prep", "achieved": round(achieved, 3),
+                    "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
+                    "traffic": traffic, "avg_launch_ms": round(prep_s / launches * 1e3, 3), "launches": launches,
+                    "flop_per_launch": flops / launches, "share_of_device_time": round(prep_s / max(totals["seconds"], 1e-12), 3),
+                    "hbm_algorithmic_GBs": round(totals.get("shading_nodes", 0) * 60 / prep_s / 1e9, 3),
+                    "hbm_peak_GBs": HBM_PEAK_GBS}
+    else:
+        roofline = {"bound": "valu_fp64", "kernel": "k_extend_brdf", "achieved": None, "peak": FP64_VECTOR_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": None, "traffic": None}
+
+    cpu = None
+    l2 = None
+    if world == 1 and not args.no_cpu:
+        log("cpu baseline (~%.0f s) ..." % args.cpu_seconds)
+        cpu, cimg, cspp = cpu_baseline(W, H, args.mode, args.seed, args.cpu_seconds)
+        g, _ = mcpt.render(scene, cam, cspp, mode=args.mode, seed=args.seed, device=local)
+        sub = (slice(7, None, 20), slice(7, None, 20))
+        l2 = float(np.linalg.norm(g[sub] - cimg[sub]) / max(np.linalg.norm(cimg[sub]), 1e-300))
+    if args.out:
+        mcpt.write_bmp(args.out, mcpt.tone_map(fb.cpu().numpy()))
+    line = {
+        "metric": METRIC, "value": round(value, 4), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: Veach-MIS stand-in scene (scenes/gen_veach_mis.py; the reference's scene files are missing)",
+        "config": {"workload": "veach-mis %s %dx%d" % (args.mode.upper(), W, H), "width": W, "height": H,
+                   "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
+                   "parallelism": "sample-shard x%d + 1 RCCL reduce" % world},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "l2_vs_cpu": l2,
+        "device_seconds": round(totals.get("seconds", 0.0), 4),
+        "samples": samples,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

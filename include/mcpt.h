@@ -1,0 +1,141 @@
+/* mcpt.h -- C ABI of libmcpt_hip.so, the MI355X (gfx950) path tracer.
+ *
+ * Drop-in boundary for the reference's per-pixel radiance loop (luotong96/Monte_Carlo_Path_Tracing).
+ * The reference has no plugin/FFI seam: its loop is inlined in main() (main.cpp:547-588) and
+ * calls `veach.closet_ray_intersect(eye, dir, triangle(-1,-1))` then
+ * `shade_with_mis` / `shade_with_brdf` on the globals `Myobj veach` / `Mylight lights`
+ * (main.cpp:23-24).  Each entry point below names the reference interface it replaces.
+ *
+ * Conventions: every function returns 0 (MCPT_OK) or a negative MCPT_E_* code; no exception
+ * crosses the ABI (the reference instead exit(1)s on load errors, Myobj.cpp:15-20,
+ * Mylight.cpp:16-20, and throws std::out_of_range on a bad material, main.cpp:425);
+ * mcpt_last_error() returns a thread-local message.  Callers own host buffers; the library owns
+ * device memory.  One render at a time per scene handle.  Results are deterministic for a fixed
+ * (seed, spp, width, height) independent of how the sample range is split across calls / GPUs,
+ * up to fp64 summation order.
+ */
+#ifndef MCPT_H
+#define MCPT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCPT_VERSION 10000 /* 1.0.0 */
+
+enum {
+    MCPT_OK = 0,
+    MCPT_E_INVALID = -1,  /* bad argument */
+    MCPT_E_IO = -2,       /* file not found / parse error */
+    MCPT_E_SCENE = -3,    /* scene violates the reference's assumptions (e.g. facet without material) */
+    MCPT_E_DEVICE = -4,   /* HIP error */
+    MCPT_E_OVERFLOW = -5, /* wavefront queue overflow (raise mcpt_render_opts.queue_factor) */
+};
+
+enum { MCPT_MODE_MIS = 0, MCPT_MODE_BRDF = 1 }; /* shade_with_mis main.cpp:402 / shade_with_brdf :348 */
+
+typedef struct mcpt_scene mcpt_scene;
+
+/* Flattened scene (host pointers, copied by mcpt_scene_create).  Facets in the reference's
+ * (shape, face) order; light table in Mylight::lightsTriangles order (material name, then facet,
+ * Mylight.cpp:88). */
+typedef struct {
+    int32_t nfacets, nmaterials, nlights;
+    const float* positions;      /* nfacets*9: v0 v1 v2 (tinyobj real_t = float) */
+    const float* normals;        /* nfacets*9: vertex normals */
+    const int32_t* material_id;  /* nfacets */
+    const float* materials;      /* nmaterials*7: Kd[3] Ks[3] Ns */
+    const int32_t* light_facet;  /* nlights: facet of each light triangle */
+    const double* light_radiance; /* nlights*3: radiance of its <light> material */
+} mcpt_scene_desc;
+
+/* Camera of main.cpp:507-510,547-564 generalised to width x height:
+ * pixellen = tan(fovy/360)*|w|/(height/2) (the reference's /360 quirk kept), eye pulled back by
+ * dist_scale (2 in the reference). */
+typedef struct {
+    double eye[3], lookat[3], up[3];
+    double fovy;
+    double dist_scale;
+    int32_t width, height;
+} mcpt_camera;
+
+typedef struct {
+    int32_t spp;            /* samples per pixel of the whole frame (the 1/spp weight) */
+    int32_t sample_begin;   /* render global sample indices [sample_begin, sample_end) */
+    int32_t sample_end;     /*   (sharding across GPUs/calls; 0,0 = all) */
+    int32_t mode;           /* MCPT_MODE_MIS / MCPT_MODE_BRDF */
+    uint64_t seed;          /* counter-RNG seed (reference default 20240430 in bench/tests) */
+    int32_t samples_per_launch; /* wavefront batch: spp slices per launch (0 = auto) */
+    int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2) */
+    int32_t device;         /* HIP device ordinal (-1 = current) */
+    int32_t reserved;
+} mcpt_render_opts;
+
+typedef struct {
+    double seconds;         /* device time of the render (HIP events) */
+    uint64_t camera_samples;
+    uint64_t shading_nodes; /* nodes that passed entry + RR (prep nodes in MIS) */
+    uint64_t light_evals_survived; /* light triangles surviving the cull chain (MIS prep) */
+    uint64_t rays;          /* extension rays traced */
+    uint64_t light_rays;    /* light-only rays traced (MIS light pdf) */
+    uint64_t generations;   /* wavefront generations launched */
+    double prep_seconds;    /* device time inside the light-prep kernel (HIP events, its stream) */
+    uint64_t prep_launches;
+    uint64_t light_evals_total;           /* shading nodes x light triangles (MIS) */
+    uint64_t light_evals_culled_backface; /* culled by the light-side test (Mylight.cpp:340-345) */
+    uint64_t light_evals_culled_plane;    /* culled by the tangent-plane test (Mylight.cpp:347-357) */
+} mcpt_stats;
+
+int mcpt_version(void);
+const char* mcpt_last_error(void);
+
+/* Myobj::read + Mylight::read + gather_light_triangles (Myobj.cpp:10-28, Mylight.cpp:11-100):
+ * OBJ/MTL via the tinyobjloader-compatible reader, <light mtlname radiance> via the XML reader. */
+int mcpt_scene_load(const char* obj_path, const char* xml_path, mcpt_scene** out);
+/* flattened-array form of the same (the reference's data after loading) */
+int mcpt_scene_create(const mcpt_scene_desc* desc, mcpt_scene** out);
+void mcpt_scene_destroy(mcpt_scene* scene);
+int mcpt_scene_counts(const mcpt_scene* scene, int32_t* nfacets, int32_t* nmaterials, int32_t* nlights);
+/* host copies of the loaded, flattened scene (any pointer may be NULL): the reference's data
+ * after Myobj::read / gather_light_triangles, plus Myobj::get_unique_normal_of_facet (Myobj.cpp:680) */
+int mcpt_scene_arrays(const mcpt_scene* scene, float* positions, float* normals, int32_t* material_id,
+                      float* materials, int32_t* light_facet, double* light_radiance, double* unique_normals);
+/* the XML's <camera> block (README.md:339-343; ignored by the reference main.cpp:507-510) */
+int mcpt_scene_camera(const mcpt_scene* scene, mcpt_camera* cam);
+
+/* main.cpp:547-588: render samples [sample_begin, sample_end) of an spp-sample frame and ADD
+ * sum_k L_k * (1/spp) into out_rgb (caller-owned host buffer, height*width*3 doubles, row 0 =
+ * top image row).  Devices: opts->device. */
+int mcpt_render(mcpt_scene* scene, const mcpt_camera* cam, const mcpt_render_opts* opts, double* out_rgb,
+                mcpt_stats* stats);
+/* same, accumulating into a DEVICE buffer (height*width*3 doubles on opts->device), without any
+ * host round trip -- the form used with torch.distributed / RCCL reduce. */
+int mcpt_render_device(mcpt_scene* scene, const mcpt_camera* cam, const mcpt_render_opts* opts,
+                       double* dev_out_rgb, mcpt_stats* stats);
+
+/* Myobj::closet_ray_intersect (Myobj.cpp:334) / closet_ray_intersect_light_triangle (:476) for a
+ * batch of n rays (host arrays): ro/rd n*3, exclude n (origin facet, -1 none) ->
+ * facet (or -1) and t, beta, gamma (n*3). */
+int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const double* rd, const int32_t* exclude,
+                     int32_t light_only, int32_t* facet, double* tbg);
+/* Mylight::prepared_for_lights_spherical_triangle_sampling (Mylight.cpp:322) at n shading points
+ * (x1, normal) -> weights_sum, survivor count, and the FACET of the light triangle picked by the
+ * counter-RNG rule for uniform u[k] (first survivor with cumulative weight >= u*weights_sum;
+ * -1 if empty or weights_sum < 1e-8). */
+int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
+                    double* weights_sum, int32_t* count, int32_t* pick);
+/* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */
+int mcpt_primary_hits(mcpt_scene* scene, const mcpt_camera* cam, int32_t* facet, double* tbg);
+
+/* RadianceRGB::tone_mapping (RadianceRGB.cpp:51-67) of an HDR frame + the EasyX saveimage BMP
+ * layout (32-bpp BI_RGB, bottom-up) of main.cpp:583-596 */
+int mcpt_tone_map(const double* rgb, int32_t width, int32_t height, double max_radiance, double gamma,
+                  uint8_t* out_rgb8);
+int mcpt_write_bmp(const char* path, const uint8_t* rgb8, int32_t width, int32_t height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

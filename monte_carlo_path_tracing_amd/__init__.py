@@ -1,0 +1,231 @@
+"""MI355X-native Monte Carlo path tracer -- host-side mirror of the reference's render interface.
+
+The reference (luotong96/Monte_Carlo_Path_Tracing) renders in `main()` (main.cpp:497-600):
+load `Myobj veach` / `Mylight lights` (main.cpp:23-24, 500-504), set the camera (main.cpp:507-510),
+trace one pixel-centre ray per pixel and average `spp` calls of `shade_with_mis` /
+`shade_with_brdf` (main.cpp:557-588), tone-map (main.cpp:583) and save `test.bmp` (main.cpp:596).
+
+Here the same steps are `Scene.load`, `Camera.reference`, `render(scene, camera, spp, mode)`,
+`tone_map` and `write_bmp`, all backed by the C ABI of `libmcpt_hip.so` (include/mcpt.h), whose
+hot path is hand-written HIP for gfx950.  There is no CPU fallback: every call fails loudly when
+the native library (or, for rendering, a GPU) is missing.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = ["Scene", "Camera", "render", "render_device", "closest_hit", "light_prep", "primary_hits",
+           "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "Stats", "MCPTError", "LIB_PATH", "lib"]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmcpt_hip.so")
+MODE_MIS, MODE_BRDF = 0, 1
+DEFAULT_SEED = 20240430
+
+
+class MCPTError(RuntimeError):
+    pass
+
+
+class Camera(C.Structure):
+    """mcpt_camera: main.cpp:507-510,547-564 generalised to width x height."""
+    _fields_ = [("eye", C.c_double * 3), ("lookat", C.c_double * 3), ("up", C.c_double * 3),
+                ("fovy", C.c_double), ("dist_scale", C.c_double), ("width", C.c_int32), ("height", C.c_int32)]
+
+    @classmethod
+    def reference(cls, width=1280, height=720, dist_scale=2.0):
+        """The hard-coded Veach camera of main.cpp:507-510 (eye pulled back 2x)."""
+        c = cls()
+        c.eye[:] = (28.2792, 5.2, 1.23612e-06)
+        c.lookat[:] = (0.0, 2.8, 0.0)
+        c.up[:] = (0.0, 1.0, 0.0)
+        c.fovy = 20.1143
+        c.dist_scale = dist_scale
+        c.width, c.height = int(width), int(height)
+        return c
+
+
+class RenderOpts(C.Structure):
+    _fields_ = [("spp", C.c_int32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32), ("mode", C.c_int32),
+                ("seed", C.c_uint64), ("samples_per_launch", C.c_int32), ("queue_factor", C.c_int32),
+                ("device", C.c_int32), ("reserved", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("seconds", C.c_double), ("camera_samples", C.c_uint64), ("shading_nodes", C.c_uint64),
+                ("light_evals_survived", C.c_uint64), ("rays", C.c_uint64), ("light_rays", C.c_uint64),
+                ("generations", C.c_uint64), ("prep_seconds", C.c_double), ("prep_launches", C.c_uint64),
+                ("light_evals_total", C.c_uint64), ("light_evals_culled_backface", C.c_uint64),
+                ("light_evals_culled_plane", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+# every symbol include/mcpt.h declares (tests check the .so exports them all)
+EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_create", "mcpt_scene_destroy",
+           "mcpt_scene_counts", "mcpt_scene_arrays", "mcpt_scene_camera", "mcpt_render", "mcpt_render_device",
+           "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map", "mcpt_write_bmp"]
+
+
+def lib():
+    """The native library; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MCPTError("libmcpt_hip.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                            "or `make -C monte_carlo_path_tracing_amd/csrc`")
+        L = C.CDLL(LIB_PATH)
+        P, I, D = C.c_void_p, C.c_int32, C.c_double
+        dp = np.ctypeslib.ndpointer(np.float64, flags="C")
+        fp = np.ctypeslib.ndpointer(np.float32, flags="C")
+        ip = np.ctypeslib.ndpointer(np.int32, flags="C")
+        u8 = np.ctypeslib.ndpointer(np.uint8, flags="C")
+        L.mcpt_version.restype = C.c_int
+        L.mcpt_last_error.restype = C.c_char_p
+        L.mcpt_scene_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(P)]
+        L.mcpt_scene_create.argtypes = [P, C.POINTER(P)]
+        L.mcpt_scene_destroy.argtypes = [P]
+        L.mcpt_scene_destroy.restype = None
+        L.mcpt_scene_counts.argtypes = [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]
+        L.mcpt_scene_arrays.argtypes = [P, fp, fp, ip, fp, ip, dp, dp]
+        L.mcpt_scene_camera.argtypes = [P, C.POINTER(Camera)]
+        L.mcpt_render.argtypes = [P, C.POINTER(Camera), C.POINTER(RenderOpts), dp, C.POINTER(Stats)]
+        L.mcpt_render_device.argtypes = [P, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p, C.POINTER(Stats)]
+        L.mcpt_closest_hit.argtypes = [P, I, dp, dp, ip, I, ip, dp]
+        L.mcpt_light_prep.argtypes = [P, I, dp, dp, dp, dp, ip, ip]
+        L.mcpt_primary_hits.argtypes = [P, C.POINTER(Camera), ip, dp]
+        L.mcpt_tone_map.argtypes = [dp, I, I, D, D, u8]
+        L.mcpt_write_bmp.argtypes = [C.c_char_p, u8, I, I]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise MCPTError("mcpt error %d: %s" % (rc, lib().mcpt_last_error().decode()))
+
+
+def _d(x, shape=None):
+    a = np.ascontiguousarray(x, dtype=np.float64)
+    return a if shape is None else a.reshape(shape)
+
+
+class Scene:
+    """Myobj + Mylight: an OBJ/MTL scene and its <light mtlname radiance> XML (main.cpp:500-504)."""
+
+    def __init__(self, handle):
+        self.h = handle
+        f, m, n = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(lib().mcpt_scene_counts(self.h, C.byref(f), C.byref(m), C.byref(n)))
+        self.nfacets, self.nmaterials, self.nlights = f.value, m.value, n.value
+
+    @classmethod
+    def load(cls, obj_path, xml_path):
+        h = C.c_void_p()
+        _check(lib().mcpt_scene_load(os.fsencode(obj_path), os.fsencode(xml_path), C.byref(h)))
+        return cls(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mcpt_scene_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def arrays(self):
+        F, M, NL = self.nfacets, self.nmaterials, self.nlights
+        pos, nrm = np.zeros((F, 9), np.float32), np.zeros((F, 9), np.float32)
+        mat, mtl = np.zeros(F, np.int32), np.zeros((M, 7), np.float32)
+        lf, lr, un = np.zeros(max(NL, 1), np.int32), np.zeros((max(NL, 1), 3)), np.zeros((F, 3))
+        _check(lib().mcpt_scene_arrays(self.h, pos, nrm, mat, mtl, lf, lr, un))
+        return dict(positions=pos, normals=nrm, material_id=mat, materials=mtl, light_facet=lf[:NL],
+                    light_radiance=lr[:NL], unique_normal=un)
+
+    def camera(self):
+        c = Camera()
+        _check(lib().mcpt_scene_camera(self.h, C.byref(c)))
+        return c
+
+
+def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor):
+    o = RenderOpts()
+    o.spp = int(spp)
+    o.mode = MODE_MIS if mode in ("mis", MODE_MIS) else MODE_BRDF if mode in ("brdf", MODE_BRDF) else -1
+    if o.mode < 0:
+        raise ValueError("mode must be 'mis' or 'brdf'")
+    o.seed = int(seed)
+    if sample_range is not None:
+        o.sample_begin, o.sample_end = int(sample_range[0]), int(sample_range[1])
+    o.device = -1 if device is None else int(device)
+    o.samples_per_launch = int(samples_per_launch or 0)
+    o.queue_factor = int(queue_factor or 0)
+    return o
+
+
+def render(scene, camera, spp, mode="mis", seed=DEFAULT_SEED, sample_range=None, out=None, device=None,
+           samples_per_launch=0, queue_factor=0):
+    """render(scene, camera, spp, mode) -- main.cpp:547-588.  Returns (H x W x 3 fp64 radiance, Stats).
+
+    Adds sum_k L_k / spp over samples k in `sample_range` (default all) into `out` (zeros if None)."""
+    if out is None:
+        out = np.zeros((camera.height, camera.width, 3))
+    assert out.dtype == np.float64 and out.flags.c_contiguous and out.shape == (camera.height, camera.width, 3)
+    st = Stats()
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor)
+    _check(lib().mcpt_render(scene.h, C.byref(camera), C.byref(o), out.reshape(-1), C.byref(st)))
+    return out, st
+
+
+def render_device(scene, camera, spp, dev_ptr, mode="mis", seed=DEFAULT_SEED, sample_range=None, device=None,
+                  samples_per_launch=0, queue_factor=0):
+    """Accumulate into a device buffer of H*W*3 doubles (e.g. a torch.float64 CUDA tensor's data_ptr())."""
+    st = Stats()
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor)
+    _check(lib().mcpt_render_device(scene.h, C.byref(camera), C.byref(o), C.c_void_p(int(dev_ptr)), C.byref(st)))
+    return st
+
+
+def closest_hit(scene, ro, rd, exclude=None, light_only=False):
+    """Myobj::closet_ray_intersect (Myobj.cpp:334) / ..._light_triangle (:476) for a batch of rays."""
+    ro, rd = _d(ro, (-1, 3)), _d(rd, (-1, 3))
+    n = ro.shape[0]
+    ex = np.full(n, -1, np.int32) if exclude is None else np.ascontiguousarray(exclude, np.int32)
+    f, tbg = np.zeros(n, np.int32), np.zeros((n, 3))
+    _check(lib().mcpt_closest_hit(scene.h, n, ro, rd, ex, int(bool(light_only)), f, tbg))
+    return f, tbg
+
+
+def light_prep(scene, x1, normal, u):
+    """Mylight::prepared_for_lights_spherical_triangle_sampling at n points + the inverse-CDF pick."""
+    x1, normal, u = _d(x1, (-1, 3)), _d(normal, (-1, 3)), _d(u, (-1,))
+    n = x1.shape[0]
+    ws, cnt, pick = np.zeros(n), np.zeros(n, np.int32), np.zeros(n, np.int32)
+    _check(lib().mcpt_light_prep(scene.h, n, x1, normal, u, ws, cnt, pick))
+    return ws, cnt, pick
+
+
+def primary_hits(scene, camera):
+    n = camera.width * camera.height
+    f, tbg = np.zeros(n, np.int32), np.zeros((n, 3))
+    _check(lib().mcpt_primary_hits(scene.h, C.byref(camera), f, tbg))
+    return f, tbg
+
+
+def tone_map(hdr, max_radiance=380.0, gamma=0.25):
+    """RadianceRGB::tone_mapping(380, 0.25) of main.cpp:583 over a whole H x W x 3 frame."""
+    hdr = np.ascontiguousarray(hdr, np.float64)
+    H, W = hdr.shape[:2]
+    out = np.zeros((H, W, 3), np.uint8)
+    _check(lib().mcpt_tone_map(hdr.reshape(-1), W, H, max_radiance, gamma, out.reshape(-1)))
+    return out
+
+
+def write_bmp(path, rgb8):
+    """The 32-bpp bottom-up BMP layout of the reference's test.bmp (main.cpp:596)."""
+    rgb8 = np.ascontiguousarray(rgb8, np.uint8)
+    H, W = rgb8.shape[:2]
+    _check(lib().mcpt_write_bmp(os.fsencode(path), rgb8.reshape(-1), W, H))

@@ -1,0 +1,212 @@
+// Device-side fp64 vector math with the reference's evaluation order (vec.cpp, matrix3d.cpp,
+// BRDF.cpp, Mylight.cpp), plus the counter RNG shared bit-for-bit with the CPU oracle.
+// Compiled with -ffp-contract=off: +, -, *, / and sqrt round exactly like the x86 reference.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mcpt {
+
+#define MCPT_EPS 1e-8
+#define MCPT_PI 3.141592653589793
+#define MCPT_P_RR 0.6
+#define MCPT_MAX_DEPTH 48  // counter-RNG trees: deeper nodes contribute 0 (oracle COUNTER_MAX_DEPTH)
+
+struct d3 {
+    double x, y, z;
+};
+__device__ __host__ inline d3 mk3(double a, double b, double c) { return d3{a, b, c}; }
+__device__ inline d3 add(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ inline d3 sub(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ inline d3 mul(d3 a, double c) { return d3{a.x * c, a.y * c, a.z * c}; }
+__device__ inline d3 hmul(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ inline double dot(d3 a, d3 b) {  // vec.cpp:73-81 (ans = 0; ans += ...)
+    double s = 0;
+    s += a.x * b.x;
+    s += a.y * b.y;
+    s += a.z * b.z;
+    return s;
+}
+__device__ inline d3 cross(d3 a, d3 b) {
+    return d3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ inline double norm2(d3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ inline d3 normalized(d3 a) {  // vec.cpp:99-103
+    double l = norm2(a);
+    return d3{a.x / l, a.y / l, a.z / l};
+}
+__device__ inline double det3(d3 a, d3 b, d3 c) { return dot(cross(a, b), c); }
+__device__ inline d3 cols_mul(d3 c0, d3 c1, d3 c2, d3 x) {  // matrix3d(c0,c1,c2) * x
+    double b0 = 0, b1 = 0, b2 = 0;
+    b0 += c0.x * x.x;
+    b0 += c1.x * x.y;
+    b0 += c2.x * x.z;
+    b1 += c0.y * x.x;
+    b1 += c1.y * x.y;
+    b1 += c2.y * x.z;
+    b2 += c0.z * x.x;
+    b2 += c1.z * x.y;
+    b2 += c2.z * x.z;
+    return d3{b0, b1, b2};
+}
+__device__ inline d3 f3(float4 v) { return d3{(double)v.x, (double)v.y, (double)v.z}; }
+
+// ---- counter RNG (identical to oracle/mcpt_oracle.c counter_key / counter_u) -------------
+__device__ __host__ inline uint64_t mix64(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+__device__ __host__ inline uint64_t counter_key(uint64_t seed, uint64_t pixel, uint64_t sample, uint64_t node) {
+    uint64_t k = mix64(seed + 0x9E3779B97F4A7C15ull * (pixel + 1));
+    k = mix64(k ^ (0xD1B54A32D192ED03ull * (sample + 1)));
+    return mix64(k ^ (0xA24BAED4963EE407ull * node));
+}
+__device__ __host__ inline double counter_u(uint64_t key, uint32_t dim) {
+    return (double)(mix64(key + 0x9FB21C651E98DF25ull * (dim + 1)) >> 11) * 0x1.0p-53;
+}
+
+// ---- Phong BRDF (BRDF.cpp) --------------------------------------------------------------
+__device__ inline d3 brdf_phong(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:17-25
+    d3 R = add(mul(wi, -1), mul(n, 2 * dot(wi, n)));
+    d3 ans = mul(kd, 1.0 / MCPT_PI);
+    double c = dot(wr, R);
+    if (c > 0) ans = add(ans, mul(ks, (sh + 1) * pow(c, sh) / (2 * MCPT_PI)));
+    return ans;
+}
+__device__ inline double phong_pdf(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:107-133
+    double d = dot(kd, mk3(1, 1, 1)) / 3;
+    double s = dot(ks, mk3(1, 1, 1)) / 3;
+    double sum = d + s;
+    double pd = d / sum, ps = s / sum;
+    double ct = dot(wi, n);
+    if (ct < 0) pd *= 0;
+    else pd *= ct / MCPT_PI;
+    d3 R = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
+    double cs = dot(wi, R);
+    if (cs < 0) ps *= 0;
+    else ps *= (sh + 1) / (2 * MCPT_PI) * pow(cs, sh);
+    return pd + ps;
+}
+// sample_from_phong (BRDF.cpp:28-104) with explicit uniforms: lobe pick u0 (lower_bound on the
+// normalised {p0, 1}), xi1, xi2.  May return directions below the surface (reference).
+__device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u0, double k1, double k2,
+                                  double* pdf_out) {
+    double d = dot(kd, mk3(1, 1, 1)) / 3;
+    double s = dot(ks, mk3(1, 1, 1)) / 3;
+    double sum = 0.0;
+    sum += d;
+    sum += s;
+    double p0 = d / sum, p1 = s / sum;
+    int ind = (p0 >= u0) ? 0 : 1;
+    double pdf = 1;
+    pdf *= ind == 0 ? p0 : p1;
+    d3 axis = n;
+    double theta, st, ct, sp, cp;
+    double phi = 2 * MCPT_PI * k2;
+    if (ind == 0) {
+        theta = 0.5 * acos(fmax(-1.0, fmin(1.0, 1 - 2 * k1)));
+        sincos(theta, &st, &ct);
+        pdf *= ct / MCPT_PI;
+    } else {
+        theta = acos(fmax(-1.0, fmin(1.0, pow(k1, 1 / (sh + 1)))));
+        sincos(theta, &st, &ct);
+        pdf *= (sh + 1) / (2 * MCPT_PI) * pow(k1, sh / (sh + 1));
+        axis = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
+    }
+    sincos(phi, &sp, &cp);
+    d3 nx;
+    if (fabs(dot(axis, mk3(1, 0, 0)) - 1) > MCPT_EPS) nx = normalized(cross(axis, mk3(1, 0, 0)));
+    else nx = normalized(cross(axis, mk3(0, 1, 0)));
+    d3 ny = normalized(cross(axis, nx));
+    *pdf_out = pdf;
+    return normalized(cols_mul(nx, ny, axis, mk3(st * cp, st * sp, ct)));
+}
+
+// ---- ray / triangle: the reference's Cramer rule in fp64 (Myobj.cpp:165-192) -------------
+struct TriHit {
+    bool hit;
+    double beta, gamma, t;
+};
+__device__ inline TriHit tri_hit(d3 a, d3 b, d3 c, d3 ro, d3 rd) {
+    TriHit h{false, 0, 0, 0};
+    d3 ab = sub(a, b), ac = sub(a, c), ar = sub(a, ro);
+    double detA = det3(ab, ac, rd);
+    if (fabs(detA) < MCPT_EPS) return h;
+    double beta = det3(ar, ac, rd) / detA;
+    double gamma = det3(ab, ar, rd) / detA;
+    double t = det3(ab, ac, ar) / detA;
+    if (beta < 0 || gamma < 0 || beta + gamma > 1 || t < 0 || fabs(t) < MCPT_EPS) return h;
+    h.hit = true;
+    h.beta = beta;
+    h.gamma = gamma;
+    h.t = t;
+    return h;
+}
+
+// ---- spherical triangle of one light triangle at (x1, n): Mylight.cpp:335-413 -------------
+struct SphTri {
+    d3 A, B, C;
+    double alpha, c, sA, w;
+};
+// cull stage reached: 0 = survives the reference's cull chain, 1 = culled by the light-side test
+// (Mylight.cpp:340-345), 2 = by the tangent-plane test (:347-357), 3 = by a later degeneracy test
+__device__ inline int light_tri_stage(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d3 x1, d3 n, SphTri* o) {
+    double tmp = dot(nl, sub(x1, p0));
+    if (tmp < 0 || fabs(tmp) < MCPT_EPS) return 1;
+    double t0 = dot(n, sub(p0, x1)), t1 = dot(n, sub(p1, x1)), t2 = dot(n, sub(p2, x1));
+    if ((t0 < 0 || fabs(t0) < MCPT_EPS) && (t1 < 0 || fabs(t1) < MCPT_EPS) && (t2 < 0 || fabs(t2) < MCPT_EPS))
+        return 2;
+    d3 A = normalized(sub(p0, x1)), B = normalized(sub(p1, x1)), C = normalized(sub(p2, x1));
+    if (dot(cross(normalized(sub(C, A)), normalized(sub(B, A))), n) < 0) {
+        d3 t = B;
+        B = C;
+        C = t;
+    }
+    double a = acos(fmax(-1.0, fmin(1.0, dot(B, C))));
+    double b = acos(fmax(-1.0, fmin(1.0, dot(A, C))));
+    double c = acos(fmax(-1.0, fmin(1.0, dot(A, B))));
+    if (a < MCPT_EPS || b < MCPT_EPS || c < MCPT_EPS) return 3;
+    double alpha = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(B, A)), normalized(cross(A, C))))));
+    double beta = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(C, B)), normalized(cross(B, A))))));
+    double gamma = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(A, C)), normalized(cross(C, B))))));
+    if (alpha < MCPT_EPS || beta < MCPT_EPS || gamma < MCPT_EPS) return 3;
+    double sA = alpha + beta + gamma - MCPT_PI;
+    if (sA < 0) return 3;
+    double w = sA * lsum;
+    if (w < 0) return 3;
+    if (isinf(w) || isnan(w)) return 3;
+    if (o) {
+        o->A = A;
+        o->B = B;
+        o->C = C;
+        o->alpha = alpha;
+        o->c = c;
+        o->sA = sA;
+        o->w = w;
+    }
+    return 0;
+}
+__device__ inline bool light_tri_eval(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d3 x1, d3 n, SphTri* o) {
+    return light_tri_stage(p0, p1, p2, nl, lsum, x1, n, o) == 0;
+}
+
+// Arvo SampleTriangle (Mylight.cpp:453-461)
+__device__ inline d3 arvo_sample(const SphTri& st, double ksi1, double ksi2) {
+    double sA1 = ksi1 * st.sA;
+    double ss, tt, sa, ca;
+    sincos(sA1 - st.alpha, &ss, &tt);
+    sincos(st.alpha, &sa, &ca);
+    double u = tt - ca;
+    double v = ss + sa * cos(st.c);
+    double q = ((v * tt - u * ss) * ca - v) / ((v * ss + u * tt) * sa);
+    d3 C1 = normalized(add(mul(st.A, q), mul(normalized(sub(st.C, mul(st.A, dot(st.C, st.A)))), sqrt(1 - q * q))));
+    double z = 1 - ksi2 * (1 - dot(C1, st.B));
+    return normalized(add(mul(st.B, z), mul(normalized(sub(C1, mul(st.B, dot(C1, st.B)))), sqrt(1 - z * z))));
+}
+
+}  // namespace mcpt

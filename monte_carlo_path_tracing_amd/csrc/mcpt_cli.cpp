@@ -1,0 +1,117 @@
+// mcpt_render -- the reference's render driver (main.cpp:497-600) as a host C++ program over the
+// C ABI: load the scene (Myobj::read / Mylight::read, main.cpp:500-504), set the camera
+// (main.cpp:507-510, eye pulled back 2x by default), render(scene, camera, spp, mode), tone-map
+// (380, 0.25; main.cpp:583) and save the BMP (main.cpp:596).  Unlike the reference, size, spp,
+// integrator and output path are flags instead of edits to main.cpp.
+//
+//   mcpt_render --scene scenes/veach-mis/veach-mis [--width 1280 --height 720] [--spp 10]
+//               [--mode mis|brdf] [--seed 20240430] [--out test.bmp] [--hdr out.pfm]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mcpt.h"
+
+namespace {
+
+// render(scene, camera, spp, mode): main.cpp:547-588 lifted into a function.
+int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, std::vector<double>& hdr,
+           mcpt_stats* st) {
+    hdr.assign(3ull * cam.width * cam.height, 0.0);
+    mcpt_render_opts o{};
+    o.spp = spp;
+    o.mode = mode;
+    o.seed = seed;
+    o.device = -1;
+    return mcpt_render(scene, &cam, &o, hdr.data(), st);
+}
+
+bool write_pfm(const char* path, const std::vector<double>& hdr, int W, int H) {
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return false;
+    std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H);
+    std::vector<float> row(3ull * W);
+    for (int i = H - 1; i >= 0; i--) {  // PFM is bottom-up
+        for (int k = 0; k < 3 * W; k++) row[k] = static_cast<float>(hdr[3ull * i * W + k]);
+        std::fwrite(row.data(), sizeof(float), row.size(), f);
+    }
+    std::fclose(f);
+    return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::string scene_base = "scenes/veach-mis/veach-mis", out = "test.bmp", hdr_out;
+    int W = 1280, H = 720, spp = 10, mode = MCPT_MODE_MIS;
+    double dist_scale = 2.0;
+    uint64_t seed = 20240430;
+    bool xml_cam = false;
+    for (int a = 1; a < argc; a++) {
+        auto next = [&]() -> const char* {
+            if (a + 1 >= argc) {
+                std::fprintf(stderr, "missing value for %s\n", argv[a]);
+                std::exit(2);
+            }
+            return argv[++a];
+        };
+        if (!std::strcmp(argv[a], "--scene")) scene_base = next();
+        else if (!std::strcmp(argv[a], "--width")) W = std::atoi(next());
+        else if (!std::strcmp(argv[a], "--height")) H = std::atoi(next());
+        else if (!std::strcmp(argv[a], "--spp")) spp = std::atoi(next());
+        else if (!std::strcmp(argv[a], "--mode")) mode = std::strcmp(next(), "brdf") ? MCPT_MODE_MIS : MCPT_MODE_BRDF;
+        else if (!std::strcmp(argv[a], "--seed")) seed = std::strtoull(next(), nullptr, 10);
+        else if (!std::strcmp(argv[a], "--out")) out = next();
+        else if (!std::strcmp(argv[a], "--hdr")) hdr_out = next();
+        else if (!std::strcmp(argv[a], "--dist-scale")) dist_scale = std::atof(next());
+        else if (!std::strcmp(argv[a], "--xml-camera")) xml_cam = true;
+        else {
+            std::fprintf(stderr, "unknown option %s\n", argv[a]);
+            return 2;
+        }
+    }
+    mcpt_scene* scene = nullptr;
+    if (mcpt_scene_load((scene_base + ".obj").c_str(), (scene_base + ".xml").c_str(), &scene) != MCPT_OK) {
+        std::fprintf(stderr, "scene load failed: %s\n", mcpt_last_error());
+        return 1;
+    }
+    int32_t nf, nm, nl;
+    mcpt_scene_counts(scene, &nf, &nm, &nl);
+    std::printf("facets %d, materials %d, light triangles %d\n", nf, nm, nl);
+    mcpt_camera cam{};
+    if (!xml_cam || mcpt_scene_camera(scene, &cam) != MCPT_OK) {  // main.cpp:507-510
+        const double eye[3] = {28.2792, 5.2, 1.23612e-06}, look[3] = {0.0, 2.8, 0.0}, up[3] = {0, 1, 0};
+        std::memcpy(cam.eye, eye, sizeof eye);
+        std::memcpy(cam.lookat, look, sizeof look);
+        std::memcpy(cam.up, up, sizeof up);
+        cam.fovy = 20.1143;
+    }
+    cam.dist_scale = dist_scale;
+    cam.width = W;
+    cam.height = H;
+    std::vector<double> hdr;
+    mcpt_stats st{};
+    const auto t0 = std::chrono::steady_clock::now();
+    if (render(scene, cam, spp, mode, seed, hdr, &st) != MCPT_OK) {
+        std::fprintf(stderr, "render failed: %s\n", mcpt_last_error());
+        return 1;
+    }
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("%dx%d @ %d spp (%s): %.3f s wall, %.3f s device, %.2f Msamples/s\n", W, H, spp,
+                mode == MCPT_MODE_MIS ? "MIS" : "BRDF", sec, st.seconds, st.camera_samples / st.seconds * 1e-6);
+    std::vector<uint8_t> rgb8(hdr.size());
+    mcpt_tone_map(hdr.data(), W, H, 380.0, 0.25, rgb8.data());  // main.cpp:583
+    if (mcpt_write_bmp(out.c_str(), rgb8.data(), W, H) != MCPT_OK) {
+        std::fprintf(stderr, "%s\n", mcpt_last_error());
+        return 1;
+    }
+    if (!hdr_out.empty() && !write_pfm(hdr_out.c_str(), hdr, W, H)) {
+        std::fprintf(stderr, "cannot write %s\n", hdr_out.c_str());
+        return 1;
+    }
+    mcpt_scene_destroy(scene);
+    return 0;
+}

@@ -1,0 +1,54 @@
+// Host-side scene representation shared by the loaders, the BVH builder and the HIP renderer.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mcpt.h"
+
+namespace mcpt {
+
+// Flattened scene: facets in the reference's (shape, face) order, the light table in
+// Mylight::lightsTriangles order (Mylight.cpp:88: material name, then facet).
+struct HostScene {
+    int F = 0, M = 0, NL = 0;
+    std::vector<float> pos;         // F*9  v0 v1 v2
+    std::vector<float> nrm;         // F*9  vertex normals
+    std::vector<int32_t> mat;       // F
+    std::vector<float> mtl;         // M*7  Kd Ks Ns
+    std::vector<std::string> mtl_names;
+    std::vector<int32_t> light_facet;   // NL
+    std::vector<double> light_rad;      // NL*3
+    std::vector<double> light_sum;      // NL  RadianceRGB::sum()
+    std::vector<int32_t> light_of;      // F -> light index or -1
+    std::vector<double> unique_n;       // F*3  Myobj::get_unique_normal_of_facet
+    bool has_cam = false;
+    mcpt_camera cam{};
+};
+
+// scene_io.cpp
+bool load_obj_mtl(const std::string& obj_path, HostScene& s, std::string& err);
+struct LightDef {
+    std::string name;
+    double rgb[3];
+};
+bool load_light_xml(const std::string& xml_path, HostScene& s, std::vector<LightDef>& lights, std::string& err);
+// gather_light_triangles + unique normals (Mylight.cpp:32-100, Myobj.cpp:680-709)
+bool finalize_scene(HostScene& s, std::vector<LightDef> lights, std::string& err);
+
+// bvh.cpp -- binary BVH over a facet subset, flattened for the GPU.
+struct BvhNode {       // 64 B: both children's boxes in one node (one fetch per visit)
+    float lo[2][3];    // child 0/1 AABB min
+    float hi[2][3];    // child 0/1 AABB max
+    int32_t child[2];  // >= 0: inner node index; < 0: leaf, ~child = first leaf slot
+    int32_t count[2];  // leaf triangle count (0 for inner children)
+};
+struct Bvh {
+    std::vector<BvhNode> nodes;
+    std::vector<int32_t> leaf_facets;  // facet ids in leaf order
+};
+Bvh build_bvh(const HostScene& s, const std::vector<int32_t>& facets, int max_leaf);
+
+void set_error(const char* fmt, ...);
+
+}  // namespace mcpt

@@ -1,0 +1,1105 @@
+// MI355X (gfx950) wavefront path tracer for the reference's per-pixel radiance loop
+// (main.cpp:547-588 -> shade_with_mis main.cpp:402-494 / shade_with_brdf :348-399).
+//
+// The recursion is flattened into generations of a persistent SoA node queue in HBM:
+//
+//   k_primary   lane per pixel : camera ray (main.cpp:547-564) + BVH closest hit, once per frame
+//   k_roots     lane per root  : node-entry checks of the root (back-face, emitter, RR) -> queue
+//   k_prep      WAVE per node  : Mylight::prepared_for_lights_spherical_triangle_sampling over all
+//                                light triangles (64 lanes = 64 light triangles, fp64), wave
+//                                prefix sums -> weights_sum and the inverse-CDF pick (MIS only)
+//   k_extend_*  lane per node  : Arvo light sample, Phong BRDF sample, up to 3 BVH traversals,
+//                                MIS weights, and the entry checks of the <= 2 children, which are
+//                                appended to the next generation's queue (wave-aggregated atomics)
+//
+// A node's value is the sum over its subtree's emitter hits of (throughput x emit); contributions
+// are accumulated straight into an fp64 framebuffer with hardware fp64 atomics.
+// RNG: counter hash of (seed, pixel, sample, heap node id, dim) -- identical to the CPU oracle.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "device_math.h"
+#include "mcpt.h"
+#include "mcpt_internal.h"
+
+using namespace mcpt;
+
+// ============================================================================================
+// device scene
+// ============================================================================================
+struct DScene {
+    int F, NL;
+    const float4* tri_v;      // F*3, original facet order
+    const float* tri_n;       // F*9 vertex normals
+    const int* tri_mat;       // F
+    const int* tri_light;     // F -> light index or -1
+    const float* mtl;         // M*7
+    const double* light_rad;  // NL*3
+    const double* light_sum;  // NL
+    const int* light_facet;   // NL
+    const float4* lt_v;       // NL*3 light vertices (reference order)
+    const double4* lt_n;      // NL: unique normal xyz, w = RadianceRGB::sum()
+    const BvhNode* bvh;       // all facets
+    const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
+    const BvhNode* lbvh;      // light facets only
+    const float4* lleaf_v;
+};
+
+struct CamFrame {
+    d3 eye, U, V, N;
+    double wlen, pixellen;
+    int W, H;
+};
+
+// camera of main.cpp:507-510,547-553 (host, fp64, same operation order as the oracle)
+static CamFrame cam_setup(const mcpt_camera& c) {
+    auto sub3 = [](d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; };
+    auto mul3 = [](d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; };
+    auto nrm = [](d3 a) { return std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); };
+    auto unit = [&](d3 a) {
+        double l = nrm(a);
+        return d3{a.x / l, a.y / l, a.z / l};
+    };
+    auto cr = [](d3 a, d3 b) { return d3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; };
+    CamFrame f;
+    d3 start{c.eye[0], c.eye[1], c.eye[2]};
+    d3 w = sub3(d3{c.lookat[0], c.lookat[1], c.lookat[2]}, start);
+    start = sub3(start, mul3(w, c.dist_scale - 1));
+    w = mul3(w, c.dist_scale);
+    f.eye = start;
+    f.wlen = nrm(w);
+    f.pixellen = std::tan(c.fovy / 360) * nrm(w) / (c.height / 2.0);
+    f.N = unit(w);
+    f.V = unit(cr(f.N, d3{c.up[0], c.up[1], c.up[2]}));
+    f.U = unit(cr(f.V, f.N));
+    f.W = c.width;
+    f.H = c.height;
+    return f;
+}
+
+__device__ inline d3 cam_dir(const CamFrame& f, int i, int j) {  // main.cpp:563-564
+    d3 delta = mk3(-f.pixellen * (i - (f.H - 1) / 2.0), f.pixellen * (j - (f.W - 1) / 2.0), 0);
+    return normalized(cols_mul(f.U, f.V, f.N, add(delta, mk3(0, 0, f.wlen))));
+}
+
+// ============================================================================================
+// BVH traversal: fp32 slab tests on conservatively enlarged boxes (prune only), fp64 reference
+// triangle test on every candidate.  Stack in LDS, [depth][thread] layout (conflict-free).
+// ============================================================================================
+constexpr int kStack = 48;
+constexpr int kTraceBlock = 128;
+
+struct Hit {
+    int f;
+    double t, beta, gamma;
+};
+
+__device__ inline Hit trace(const BvhNode* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
+                            int exclude, int* __restrict__ stack, int stride) {
+    Hit best{-1, DBL_MAX, 0, 0};
+    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
+    const float ox = (float)ro.x, oy = (float)ro.y, oz = (float)ro.z;
+    auto inv = [](double d) {
+        float f = (float)d;
+        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
+        return 1.0f / f;
+    };
+    const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
+    float tlimit = FLT_MAX;
+    int sp = 0;
+    int node = 0;
+    while (true) {
+        const BvhNode nd = nodes[node];
+        float tn[2];
+        bool hitc[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            float tx0 = (nd.lo[k][0] - ox) * ix, tx1 = (nd.hi[k][0] - ox) * ix;
+            float ty0 = (nd.lo[k][1] - oy) * iy, ty1 = (nd.hi[k][1] - oy) * iy;
+            float tz0 = (nd.lo[k][2] - oz) * iz, tz1 = (nd.hi[k][2] - oz) * iz;
+            float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+            float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+            hitc[k] = t0 <= t1 * 1.00001f + 1e-6f;
+            tn[k] = t0;
+        }
+        int next[2];
+        int nn = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (!hitc[k]) continue;
+            const int c = nd.child[k];
+            if (c >= 0) {
+                next[nn++] = c;
+                continue;
+            }
+            const int first = ~c, cnt = nd.count[k];
+            for (int q = first; q < first + cnt; q++) {
+                const float4 a = leafv[3 * q], b = leafv[3 * q + 1], cc = leafv[3 * q + 2];
+                const int fac = __float_as_int(a.w);
+                if (fac == exclude) continue;
+                TriHit h = tri_hit(f3(a), f3(b), f3(cc), ro, rd);
+                if (h.hit && (h.t < best.t || (h.t == best.t && fac < best.f))) {
+                    best.f = fac;
+                    best.t = h.t;
+                    best.beta = h.beta;
+                    best.gamma = h.gamma;
+                    tlimit = (float)h.t * 1.0001f + 1e-5f;
+                }
+            }
+        }
+        if (nn == 2) {
+            int nearc = next[0], farc = next[1];
+            if (tn[1] < tn[0]) {
+                nearc = next[1];
+                farc = next[0];
+            }
+            if (sp < kStack) stack[(sp++) * stride] = farc;
+            node = nearc;
+        } else if (nn == 1) {
+            node = next[0];
+        } else {
+            if (sp == 0) break;
+            node = stack[(--sp) * stride];
+        }
+    }
+    return best;
+}
+
+// ============================================================================================
+// wavefront queue (SoA)
+// ============================================================================================
+struct Queue {
+    double* p;      // 3*cap  shading point
+    double* n;      // 3*cap  interpolated normal
+    double* wo;     // 3*cap
+    double* tp;     // 3*cap  path throughput
+    int* f;         // cap
+    int* pixel;     // cap
+    int* sample;    // cap
+    uint64_t* node; // cap   heap id (MIS) / depth+1 (BRDF)
+    double* wsum;   // cap   (MIS prep output)
+    int* pick;      // cap   (MIS prep output)
+    unsigned* count;
+    int cap;
+};
+
+struct Params {
+    DScene S;
+    uint64_t seed;
+    double inv_spp;
+    double* fb;                  // W*H*3 fp64
+    unsigned long long* stats;   // [0] nodes pushed [1] light survivors [2] rays [3] light rays [4] overflow
+    int mode;
+};
+
+__device__ inline int lane_id() { return __lane_id(); }
+
+// wave-aggregated append: returns this lane's slot (or -1 if !want)
+__device__ inline int wave_append(unsigned* counter, bool want) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return -1;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int lane = lane_id();
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(m));
+    base = __shfl(base, leader);
+    const uint64_t below = lane == 0 ? 0ull : (m & ((~0ull) >> (64 - lane)));
+    return want ? (int)(base + __popcll(below)) : -1;
+}
+
+// node entry of shade_with_* (main.cpp:406-437 / :351-383): interpolate, back-face -> 0,
+// emitter -> emit, Russian roulette; survivors are appended to the queue.
+// Must be called by ALL lanes of the wave (wave_append); `active` masks the lane.
+__device__ inline void node_entry(const Params& P, bool active, int f, double beta, double gamma, d3 wo, d3 tp,
+                                  int pixel, int sample, uint64_t node, Queue& q) {
+    const DScene& S = P.S;
+    d3 p, N;
+    bool push = false;
+    if (active) {
+        const bool too_deep = P.mode == MCPT_MODE_MIS ? node >= (2ull << MCPT_MAX_DEPTH) : node > MCPT_MAX_DEPTH + 1;
+        if (!too_deep) {
+            const float4* v = S.tri_v + 3 * f;
+            const float* nv = S.tri_n + 9 * f;
+            const double a0 = 1.0 - beta - gamma;
+            p = add(add(mul(f3(v[0]), a0), mul(f3(v[1]), beta)), mul(f3(v[2]), gamma));
+            N = normalized(add(add(mul(mk3(nv[0], nv[1], nv[2]), a0), mul(mk3(nv[3], nv[4], nv[5]), beta)),
+                               mul(mk3(nv[6], nv[7], nv[8]), gamma)));
+            if (!(dot(N, wo) < 0)) {
+                const int li = S.tri_light[f];
+                if (li >= 0) {
+                    double* px = P.fb + 3 * (size_t)pixel;
+                    unsafeAtomicAdd(px + 0, tp.x * S.light_rad[3 * li + 0] * P.inv_spp);
+                    unsafeAtomicAdd(px + 1, tp.y * S.light_rad[3 * li + 1] * P.inv_spp);
+                    unsafeAtomicAdd(px + 2, tp.z * S.light_rad[3 * li + 2] * P.inv_spp);
+                } else {
+                    const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
+                    push = !(counter_u(key, 0) > MCPT_P_RR);
+                }
+            }
+        }
+    }
+    const int slot = wave_append(q.count, push);
+    if (push) {
+        if (slot >= q.cap) {
+            atomicOr((unsigned long long*)(P.stats + 4), 1ull);
+            return;
+        }
+        const size_t s = (size_t)slot;
+        q.p[3 * s] = p.x;
+        q.p[3 * s + 1] = p.y;
+        q.p[3 * s + 2] = p.z;
+        q.n[3 * s] = N.x;
+        q.n[3 * s + 1] = N.y;
+        q.n[3 * s + 2] = N.z;
+        q.wo[3 * s] = wo.x;
+        q.wo[3 * s + 1] = wo.y;
+        q.wo[3 * s + 2] = wo.z;
+        q.tp[3 * s] = tp.x;
+        q.tp[3 * s + 1] = tp.y;
+        q.tp[3 * s + 2] = tp.z;
+        q.f[s] = f;
+        q.pixel[s] = pixel;
+        q.sample[s] = sample;
+        q.node[s] = node;
+    }
+}
+
+// ============================================================================================
+// kernels
+// ============================================================================================
+__global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam, int* hit_f, double* hit_tbg) {
+    __shared__ int stack[kStack * kTraceBlock];
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int npx = cam.W * cam.H;
+    if (idx >= npx) return;
+    const int i = idx / cam.W, j = idx % cam.W;
+    const d3 dir = cam_dir(cam, i, j);
+    Hit h = trace(S.bvh, S.leaf_v, cam.eye, dir, -1, stack + threadIdx.x, kTraceBlock);
+    hit_f[idx] = h.f;
+    hit_tbg[3 * idx] = h.f >= 0 ? h.t : 0.0;
+    hit_tbg[3 * idx + 1] = h.f >= 0 ? h.beta : 0.0;
+    hit_tbg[3 * idx + 2] = h.f >= 0 ? h.gamma : 0.0;
+}
+
+// roots: r in [0, nroots): pixel = r % npx, sample = s0 + r / npx
+__global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
+                                               int s0, int nroots, Queue q) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int npx = cam.W * cam.H;
+    bool active = r < nroots;
+    int pixel = 0, sample = 0, f = -1;
+    double beta = 0, gamma = 0;
+    d3 wo = mk3(0, 0, 0);
+    if (active) {
+        pixel = r % npx;
+        sample = s0 + r / npx;
+        f = hit_f[pixel];
+        active = f >= 0;
+        if (active) {
+            beta = hit_tbg[3 * pixel + 1];
+            gamma = hit_tbg[3 * pixel + 2];
+            wo = mul(cam_dir(cam, pixel / cam.W, pixel % cam.W), -1);
+        }
+    }
+    node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
+}
+
+// Light prep, one wave per node (Mylight.cpp:322-422): lane l evaluates light triangle 64c+l
+// of chunk c.  Chunk totals are the last lane of an inclusive wave scan, stored in LDS; the total
+// weight is their sequential sum; the inverse-CDF pick (first survivor whose cumulative weight
+// >= u * weights_sum, u = dim 1) re-evaluates only the chunk that contains the target.
+// u_override / count_out: test entry (mcpt_light_prep).
+__device__ inline double wave_incl_scan(double v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        double t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
+                                              const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                              const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                              const double* __restrict__ u_override, double* __restrict__ wsum_out,
+                                              int* __restrict__ pick_out, int* __restrict__ count_out,
+                                              unsigned long long* stats, int nchunks) {
+    extern __shared__ double chunk_lds[];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    double* ctot = chunk_lds + (size_t)wib * nchunks;
+    const int nwaves = gridDim.x * (blockDim.x >> 6);
+    unsigned long long surv_acc = 0, c1_acc = 0, c2_acc = 0;
+    for (int node = blockIdx.x * (blockDim.x >> 6) + wib; node < n; node += nwaves) {
+        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        int survivors = 0, cull1 = 0, cull2 = 0;
+        int last_chunk = -1;
+        for (int c = 0; c < nchunks; c++) {
+            const int li = c * 64 + lane;
+            double w = 0;
+            int stage = 4;
+            if (li < S.NL) {
+                const double4 ln = S.lt_n[li];
+                SphTri st;
+                stage = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                        mk3(ln.x, ln.y, ln.z), ln.w, x1, nn, &st);
+                if (stage == 0) w = st.w;
+            }
+            const double sc = wave_incl_scan(w, lane);
+            const uint64_t m = __ballot(stage == 0);
+            survivors += __popcll(m);
+            cull1 += __popcll(__ballot(stage == 1));
+            cull2 += __popcll(__ballot(stage == 2));
+            if (m) last_chunk = c;
+            if (lane == 63) ctot[c] = sc;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double wsum = 0;
+        for (int c = 0; c < nchunks; c++) wsum += ctot[c];
+        int pick = -1;
+        if (!(fabs(wsum) < MCPT_EPS)) {
+            double u;
+            if (u_override) u = u_override[node];
+            else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+            const double target = u * wsum;
+            double cum = 0;
+            int cc = -1;
+            double base = 0;
+            for (int c = 0; c < nchunks; c++) {
+                const double nxt = cum + ctot[c];
+                if (nxt >= target && ctot[c] > 0) {
+                    cc = c;
+                    base = cum;
+                    break;
+                }
+                cum = nxt;
+            }
+            if (cc < 0) {  // rounding: fall back to the last chunk with a survivor
+                cc = last_chunk;
+                base = 0;
+                for (int c = 0; c < cc; c++) base += ctot[c];
+            }
+            const int li = cc * 64 + lane;
+            double w = 0;
+            bool ok = false;
+            if (li < S.NL) {
+                const double4 ln = S.lt_n[li];
+                SphTri st;
+                ok = light_tri_eval(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                    mk3(ln.x, ln.y, ln.z), ln.w, x1, nn, &st);
+                if (ok) w = st.w;
+            }
+            const double sc = wave_incl_scan(w, lane);
+            const uint64_t cand = __ballot(ok && (base + sc >= target));
+            const uint64_t okm = __ballot(ok);
+            int pl;
+            if (cand) pl = __ffsll((unsigned long long)cand) - 1;
+            else pl = 63 - __clzll((long long)okm);
+            pick = cc * 64 + pl;
+        }
+        if (lane == 0) {
+            wsum_out[node] = wsum;
+            pick_out[node] = pick;
+            if (count_out) count_out[node] = survivors;
+        }
+        surv_acc += survivors;
+        c1_acc += cull1;
+        c2_acc += cull2;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0 && stats) {
+        if (surv_acc) atomicAdd(stats + 1, surv_acc);
+        if (c1_acc) atomicAdd(stats + 5, c1_acc);
+        if (c2_acc) atomicAdd(stats + 6, c2_acc);
+    }
+}
+
+// one MIS node (main.cpp:440-493), lane per node; children go through node_entry.
+__global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur, int n, Queue nxt) {
+    __shared__ int stack[kStack * kTraceBlock];
+    int* st = stack + threadIdx.x;
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    const int ii = active ? i : 0;
+    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
+    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
+    const d3 wo = mk3(cur.wo[3 * ii], cur.wo[3 * ii + 1], cur.wo[3 * ii + 2]);
+    const d3 tp = mk3(cur.tp[3 * ii], cur.tp[3 * ii + 1], cur.tp[3 * ii + 2]);
+    const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
+    const uint64_t node = cur.node[ii];
+    const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
+    const float* m = S.mtl + 7 * S.tri_mat[f];
+    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
+    const double sh = m[6];
+    const double wsum = cur.wsum[ii];
+    const int pick = cur.pick[ii];
+
+    // ---- light branch (main.cpp:443-466) ----
+    bool c1 = false;
+    Hit h1{-1, 0, 0, 0};
+    d3 wl = mk3(0, 0, 0), tp1 = mk3(0, 0, 0);
+    if (active) {
+        d3 coord;
+        double lprob = 1;
+        if (pick >= 0) {
+            const double4 ln = S.lt_n[pick];
+            SphTri sph;
+            light_tri_eval(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]),
+                           mk3(ln.x, ln.y, ln.z), ln.w, p, N, &sph);
+            const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
+            TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
+            coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:475-481)
+            lprob = S.light_sum[pick] / wsum;
+        } else {
+            coord = add(mul(N, -1), p);  // Mylight.cpp:427-430
+        }
+        wl = normalized(sub(coord, p));
+        if (dot(wl, N) > 0) {
+            h1 = trace(S.bvh, S.leaf_v, p, wl, f, st, kTraceBlock);
+            if (h1.f >= 0) {
+                const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
+                const double pp = phong_pdf(N, wl, wo, kd, ks, sh);
+                tp1 = mul(hmul(tp, b), dot(wl, N) / (lprob + pp) / MCPT_P_RR);
+                c1 = true;
+            }
+        }
+    }
+    // ---- BRDF branch (main.cpp:469-493) ----
+    bool c2 = false;
+    Hit h2{-1, 0, 0, 0};
+    d3 wi = mk3(0, 0, 0), tp2 = mk3(0, 0, 0);
+    unsigned nrays = 0, nlrays = 0;
+    if (active) {
+        nrays += (dot(wl, N) > 0);
+        double pdf;
+        wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+        if (!(dot(wi, N) < 0)) {
+            nrays++;
+            h2 = trace(S.bvh, S.leaf_v, p, wi, f, st, kTraceBlock);
+            if (h2.f >= 0) {
+                const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
+                double lpdf = 0;
+                nlrays++;
+                Hit hl = trace(S.lbvh, S.lleaf_v, p, wi, f, st, kTraceBlock);
+                if (hl.f >= 0 && !(fabs(wsum) < MCPT_EPS)) {
+                    const int li = S.tri_light[hl.f];
+                    const double4 ln = S.lt_n[li];
+                    if (light_tri_eval(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                       mk3(ln.x, ln.y, ln.z), ln.w, p, N, nullptr))
+                        lpdf = S.light_sum[li] / wsum;  // fresh-state eval (Mylight.cpp:484-493)
+                }
+                tp2 = mul(hmul(tp, b), dot(wi, N) / (pdf + lpdf) / MCPT_P_RR);
+                c2 = true;
+            }
+        }
+    }
+    node_entry(P, c1, h1.f, h1.beta, h1.gamma, mul(wl, -1), tp1, pixel, sample, 2 * node, nxt);
+    node_entry(P, c2, h2.f, h2.beta, h2.gamma, mul(wi, -1), tp2, pixel, sample, 2 * node + 1, nxt);
+    if (active) {
+        atomicAdd(P.stats + 2, (unsigned long long)nrays);
+        atomicAdd(P.stats + 3, (unsigned long long)nlrays);
+    }
+}
+
+// one BRDF-only path vertex (main.cpp:385-396)
+__global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
+    __shared__ int stack[kStack * kTraceBlock];
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    const int ii = active ? i : 0;
+    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
+    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
+    const d3 wo = mk3(cur.wo[3 * ii], cur.wo[3 * ii + 1], cur.wo[3 * ii + 2]);
+    const d3 tp = mk3(cur.tp[3 * ii], cur.tp[3 * ii + 1], cur.tp[3 * ii + 2]);
+    const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
+    const uint64_t node = cur.node[ii];
+    bool c = false;
+    Hit h{-1, 0, 0, 0};
+    d3 wi = mk3(0, 0, 0), tpc = mk3(0, 0, 0);
+    if (active) {
+        const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
+        const float* m = S.mtl + 7 * S.tri_mat[f];
+        const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
+        const double sh = m[6];
+        double pdf;
+        wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+        if (!(dot(wi, N) < 0)) {
+            atomicAdd(P.stats + 2, 1ull);
+            h = trace(S.bvh, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock);
+            if (h.f >= 0) {
+                const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
+                tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
+                c = true;
+            }
+        }
+    }
+    node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
+}
+
+// batch closest hit (test / FFI entry mcpt_closest_hit)
+__global__ __launch_bounds__(kTraceBlock) void k_trace_batch(DScene S, int n, const double* ro, const double* rd,
+                                                             const int* ex, int light_only, int* f_out,
+                                                             double* tbg) {
+    __shared__ int stack[kStack * kTraceBlock];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Hit h = trace(light_only ? S.lbvh : S.bvh, light_only ? S.lleaf_v : S.leaf_v, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]),
+                  mk3(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]), ex[i], stack + threadIdx.x, kTraceBlock);
+    f_out[i] = h.f;
+    tbg[3 * i] = h.f >= 0 ? h.t : 0.0;
+    tbg[3 * i + 1] = h.f >= 0 ? h.beta : 0.0;
+    tbg[3 * i + 2] = h.f >= 0 ? h.gamma : 0.0;
+}
+
+// ============================================================================================
+// host side
+// ============================================================================================
+#define HIP_OK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            set_error("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return MCPT_E_DEVICE;                                                              \
+        }                                                                                      \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct DeviceState {
+    int device = -1;
+    DScene d{};
+    std::vector<void*> allocs;
+    hipStream_t stream = nullptr;
+    // reusable work buffers
+    DevBuf hit_f, hit_tbg, fb, stats, qa[14], qb[14];
+    unsigned* pinned_count = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr;
+};
+
+}  // namespace
+
+struct mcpt_scene {
+    HostScene host;
+    Bvh bvh, lbvh;
+    std::vector<std::unique_ptr<DeviceState>> devs;
+    std::mutex mu;
+};
+
+namespace {
+
+int ensure(DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return MCPT_OK;
+    if (b.p) HIP_OK(hipFree(b.p));
+    b.p = nullptr;
+    HIP_OK(hipMalloc(&b.p, std::max<size_t>(bytes, 256)));
+    b.bytes = std::max<size_t>(bytes, 256);
+    return MCPT_OK;
+}
+
+template <class T>
+int upload(DeviceState& D, const std::vector<T>& v, const T** out) {
+    void* p = nullptr;
+    HIP_OK(hipMalloc(&p, std::max<size_t>(v.size() * sizeof(T), 64)));
+    if (!v.empty()) HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    D.allocs.push_back(p);
+    *out = static_cast<const T*>(p);
+    return MCPT_OK;
+}
+
+std::vector<float4> leaf_vertices(const HostScene& s, const Bvh& b) {
+    std::vector<float4> v(3 * std::max<size_t>(b.leaf_facets.size(), 1));
+    for (size_t q = 0; q < b.leaf_facets.size(); q++) {
+        const int f = b.leaf_facets[q];
+        for (int k = 0; k < 3; k++) {
+            float4 x;
+            x.x = s.pos[9 * f + 3 * k];
+            x.y = s.pos[9 * f + 3 * k + 1];
+            x.z = s.pos[9 * f + 3 * k + 2];
+            int fb = f;
+            float w;
+            std::memcpy(&w, &fb, 4);
+            x.w = k == 0 ? w : 0.0f;
+            v[3 * q + k] = x;
+        }
+    }
+    return v;
+}
+
+int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
+    if (device < 0) HIP_OK(hipGetDevice(&device));
+    for (auto& d : sc->devs)
+        if (d->device == device) {
+            HIP_OK(hipSetDevice(device));
+            *out = d.get();
+            return MCPT_OK;
+        }
+    HIP_OK(hipSetDevice(device));
+    auto D = std::make_unique<DeviceState>();
+    D->device = device;
+    const HostScene& s = sc->host;
+    DScene& d = D->d;
+    d.F = s.F;
+    d.NL = s.NL;
+    std::vector<float4> tv(3 * std::max(s.F, 1));
+    for (int f = 0; f < s.F; f++)
+        for (int k = 0; k < 3; k++) tv[3 * f + k] = make_float4(s.pos[9 * f + 3 * k], s.pos[9 * f + 3 * k + 1], s.pos[9 * f + 3 * k + 2], 0.f);
+    int rc;
+    if ((rc = upload(*D, tv, &d.tri_v))) return rc;
+    if ((rc = upload(*D, s.nrm, &d.tri_n))) return rc;
+    if ((rc = upload(*D, s.mat, &d.tri_mat))) return rc;
+    if ((rc = upload(*D, s.light_of, &d.tri_light))) return rc;
+    if ((rc = upload(*D, s.mtl, &d.mtl))) return rc;
+    if ((rc = upload(*D, s.light_rad, &d.light_rad))) return rc;
+    if ((rc = upload(*D, s.light_sum, &d.light_sum))) return rc;
+    if ((rc = upload(*D, s.light_facet, &d.light_facet))) return rc;
+    std::vector<float4> lv(3 * std::max(s.NL, 1));
+    std::vector<double4> ln(std::max(s.NL, 1));
+    for (int l = 0; l < s.NL; l++) {
+        const int f = s.light_facet[l];
+        for (int k = 0; k < 3; k++) lv[3 * l + k] = tv[3 * f + k];
+        ln[l] = make_double4(s.unique_n[3 * f], s.unique_n[3 * f + 1], s.unique_n[3 * f + 2], s.light_sum[l]);
+    }
+    if ((rc = upload(*D, lv, &d.lt_v))) return rc;
+    if ((rc = upload(*D, ln, &d.lt_n))) return rc;
+    if ((rc = upload(*D, sc->bvh.nodes, &d.bvh))) return rc;
+    if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
+    if ((rc = upload(*D, sc->lbvh.nodes, &d.lbvh))) return rc;
+    if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
+    HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+    HIP_OK(hipHostMalloc(&D->pinned_count, 64));
+    HIP_OK(hipEventCreate(&D->ev0));
+    HIP_OK(hipEventCreate(&D->ev1));
+    HIP_OK(hipEventCreate(&D->evp0));
+    HIP_OK(hipEventCreate(&D->evp1));
+    *out = D.get();
+    sc->devs.push_back(std::move(D));
+    return MCPT_OK;
+}
+
+int alloc_queue(DevBuf* b, int cap, Queue& q) {
+    const size_t c = (size_t)cap;
+    const size_t sz[14] = {24 * c, 24 * c, 24 * c, 24 * c, 4 * c, 4 * c, 4 * c, 8 * c, 8 * c, 4 * c, 64, 0, 0, 0};
+    for (int k = 0; k < 11; k++) {
+        int rc = ensure(b[k], sz[k]);
+        if (rc) return rc;
+    }
+    q.p = (double*)b[0].p;
+    q.n = (double*)b[1].p;
+    q.wo = (double*)b[2].p;
+    q.tp = (double*)b[3].p;
+    q.f = (int*)b[4].p;
+    q.pixel = (int*)b[5].p;
+    q.sample = (int*)b[6].p;
+    q.node = (uint64_t*)b[7].p;
+    q.wsum = (double*)b[8].p;
+    q.pick = (int*)b[9].p;
+    q.count = (unsigned*)b[10].p;
+    q.cap = cap;
+    return MCPT_OK;
+}
+
+int validate_camera(const mcpt_camera* cam) {
+    if (!cam || cam->width <= 0 || cam->height <= 0 || cam->dist_scale <= 0) {
+        set_error("invalid camera");
+        return MCPT_E_INVALID;
+    }
+    return MCPT_OK;
+}
+
+int prep_chunks(int NL) { return std::max(1, (NL + 63) / 64); }
+
+// the wavefront render into a device framebuffer already resident on D's device
+int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o,
+                     double* dfb, mcpt_stats* stats) {
+    const CamFrame cf = cam_setup(*cam);
+    const int W = cam->width, H = cam->height, npx = W * H;
+    const int s0 = (o->sample_begin == 0 && o->sample_end == 0) ? 0 : o->sample_begin;
+    const int s1 = (o->sample_begin == 0 && o->sample_end == 0) ? o->spp : o->sample_end;
+    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF)) {
+        set_error("invalid render options (spp %d, range [%d,%d), mode %d)", o->spp, s0, s1, o->mode);
+        return MCPT_E_INVALID;
+    }
+    int spb = o->samples_per_launch > 0 ? o->samples_per_launch : std::max(1, (2 << 20) / std::max(npx, 1));
+    spb = std::min(spb, std::max(1, s1 - s0));
+    const long long roots_ll = (long long)spb * npx;
+    if (roots_ll > (1ll << 30)) {
+        set_error("batch too large");
+        return MCPT_E_INVALID;
+    }
+    const int roots = (int)roots_ll;
+    const int qf = o->queue_factor > 0 ? o->queue_factor : 2;
+    const int cap = (int)std::min<long long>((long long)qf * roots + 1024, (1ll << 30));
+    int rc;
+    if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) || (rc = ensure(D.stats, 64)))
+        return rc;
+    Queue qa, qb;
+    if ((rc = alloc_queue(D.qa, cap, qa)) || (rc = alloc_queue(D.qb, cap, qb))) return rc;
+    hipStream_t st = D.stream;
+    Params P;
+    P.S = D.d;
+    P.seed = o->seed;
+    P.inv_spp = 1.0 / o->spp;
+    P.fb = dfb;
+    P.stats = (unsigned long long*)D.stats.p;
+    P.mode = o->mode;
+    HIP_OK(hipMemsetAsync(D.stats.p, 0, 64, st));
+    HIP_OK(hipEventRecord(D.ev0, st));
+    hipLaunchKernelGGL(k_primary, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, D.d, cf,
+                       (int*)D.hit_f.p, (double*)D.hit_tbg.p);
+    HIP_OK(hipGetLastError());
+    const int nchunks = prep_chunks(D.d.NL);
+    const size_t prep_lds = 4 * (size_t)nchunks * sizeof(double);
+    if (prep_lds > 160 * 1024) {
+        set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
+        return MCPT_E_SCENE;
+    }
+    double prep_ms = 0;
+    uint64_t gens = 0, prep_launches = 0, nodes_total = 0;
+    for (int sb = s0; sb < s1; sb += spb) {
+        const int nb = std::min(spb, s1 - sb);
+        const int nroots = nb * npx;
+        HIP_OK(hipMemsetAsync(qa.count, 0, 4, st));
+        hipLaunchKernelGGL(k_roots, dim3((nroots + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
+                           (const double*)D.hit_tbg.p, sb, nroots, qa);
+        HIP_OK(hipGetLastError());
+        Queue* cur = &qa;
+        Queue* nxt = &qb;
+        while (true) {
+            HIP_OK(hipMemcpyAsync(D.pinned_count, cur->count, 4, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipMemcpyAsync(D.pinned_count + 2, (char*)D.stats.p + 32, 8, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            if (*(unsigned long long*)(D.pinned_count + 2)) {
+                set_error("wavefront queue overflow (capacity %d); raise queue_factor", cap);
+                return MCPT_E_OVERFLOW;
+            }
+            const int n = (int)std::min<unsigned>(D.pinned_count[0], (unsigned)cap);
+            if (n == 0) break;
+            gens++;
+            nodes_total += (uint64_t)n;
+            if (o->mode == MCPT_MODE_MIS) {
+                const int blocks = std::min((n + 3) / 4, 1 << 20);
+                HIP_OK(hipEventRecord(D.evp0, st));
+                hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds, st, D.d, o->seed, n, cur->p, cur->n,
+                                   cur->pixel, cur->sample, cur->node, (const double*)nullptr, cur->wsum, cur->pick,
+                                   (int*)nullptr, P.stats, nchunks);
+                HIP_OK(hipGetLastError());
+                HIP_OK(hipEventRecord(D.evp1, st));
+                prep_launches++;
+            }
+            HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
+            if (o->mode == MCPT_MODE_MIS)
+                hipLaunchKernelGGL(k_extend_mis, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, P,
+                                   *cur, n, *nxt);
+            else
+                hipLaunchKernelGGL(k_extend_brdf, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
+                                   P, *cur, n, *nxt);
+            HIP_OK(hipGetLastError());
+            if (o->mode == MCPT_MODE_MIS) {
+                float ms = 0;
+                HIP_OK(hipEventSynchronize(D.evp1));
+                HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
+                prep_ms += ms;
+            }
+            std::swap(cur, nxt);
+        }
+    }
+    HIP_OK(hipEventRecord(D.ev1, st));
+    HIP_OK(hipEventSynchronize(D.ev1));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, D.ev0, D.ev1));
+    if (stats) {
+        unsigned long long hs[8] = {0};
+        HIP_OK(hipMemcpy(hs, D.stats.p, 64, hipMemcpyDeviceToHost));
+        stats->seconds = ms * 1e-3;
+        stats->camera_samples = (uint64_t)(s1 - s0) * npx;
+        stats->light_evals_survived = hs[1];
+        stats->rays = hs[2];
+        stats->light_rays = hs[3];
+        stats->generations = gens;
+        stats->shading_nodes = nodes_total;
+        stats->light_evals_culled_backface = hs[5];
+        stats->light_evals_culled_plane = hs[6];
+        stats->light_evals_total = (uint64_t)nodes_total * (o->mode == MCPT_MODE_MIS ? (uint64_t)D.d.NL : 0ull);
+        stats->prep_seconds = prep_ms * 1e-3;
+        stats->prep_launches = prep_launches;
+    }
+    return MCPT_OK;
+}
+
+}  // namespace
+
+// ============================================================================================
+// C ABI
+// ============================================================================================
+extern "C" {
+
+int mcpt_version(void) { return MCPT_VERSION; }
+
+static int finish_scene(HostScene&& hs, mcpt_scene** out) {
+    auto* sc = new mcpt_scene();
+    sc->host = std::move(hs);
+    std::vector<int32_t> all(sc->host.F), lights(sc->host.light_facet);
+    for (int f = 0; f < sc->host.F; f++) all[f] = f;
+    sc->bvh = build_bvh(sc->host, all, 4);
+    sc->lbvh = build_bvh(sc->host, lights, 4);
+    *out = sc;
+    return MCPT_OK;
+}
+
+int mcpt_scene_load(const char* obj_path, const char* xml_path, mcpt_scene** out) {
+    if (!obj_path || !xml_path || !out) {
+        set_error("null argument");
+        return MCPT_E_INVALID;
+    }
+    HostScene hs;
+    std::vector<LightDef> lights;
+    std::string err;
+    if (!load_obj_mtl(obj_path, hs, err) || !load_light_xml(xml_path, hs, lights, err)) {
+        set_error("%s", err.c_str());
+        return MCPT_E_IO;
+    }
+    if (!finalize_scene(hs, lights, err)) {
+        set_error("%s", err.c_str());
+        return MCPT_E_SCENE;
+    }
+    return finish_scene(std::move(hs), out);
+}
+
+int mcpt_scene_create(const mcpt_scene_desc* d, mcpt_scene** out) {
+    if (!d || !out || d->nfacets < 0 || d->nmaterials < 0 || d->nlights < 0 || !d->positions || !d->normals ||
+        !d->material_id || !d->materials || (d->nlights && (!d->light_facet || !d->light_radiance))) {
+        set_error("invalid scene descriptor");
+        return MCPT_E_INVALID;
+    }
+    HostScene hs;
+    hs.F = d->nfacets;
+    hs.M = d->nmaterials;
+    hs.pos.assign(d->positions, d->positions + 9 * (size_t)hs.F);
+    hs.nrm.assign(d->normals, d->normals + 9 * (size_t)hs.F);
+    hs.mat.assign(d->material_id, d->material_id + hs.F);
+    hs.mtl.assign(d->materials, d->materials + 7 * (size_t)hs.M);
+    for (int m = 0; m < hs.M; m++) hs.mtl_names.push_back("m" + std::to_string(m));
+    // lights are given directly: synthesise one light "material" per light triangle in order
+    std::vector<LightDef> none;
+    std::string err;
+    if (!finalize_scene(hs, none, err)) {
+        set_error("%s", err.c_str());
+        return MCPT_E_SCENE;
+    }
+    hs.NL = d->nlights;
+    hs.light_facet.assign(d->light_facet, d->light_facet + hs.NL);
+    hs.light_rad.assign(d->light_radiance, d->light_radiance + 3 * (size_t)hs.NL);
+    hs.light_sum.resize(hs.NL);
+    hs.light_of.assign(hs.F, -1);
+    for (int l = 0; l < hs.NL; l++) {
+        if (hs.light_facet[l] < 0 || hs.light_facet[l] >= hs.F) {
+            set_error("light %d: facet out of range", l);
+            return MCPT_E_INVALID;
+        }
+        hs.light_sum[l] = hs.light_rad[3 * l] + hs.light_rad[3 * l + 1] + hs.light_rad[3 * l + 2];
+        hs.light_of[hs.light_facet[l]] = l;
+    }
+    return finish_scene(std::move(hs), out);
+}
+
+void mcpt_scene_destroy(mcpt_scene* sc) {
+    if (!sc) return;
+    for (auto& D : sc->devs) {
+        (void)hipSetDevice(D->device);
+        for (void* p : D->allocs) (void)hipFree(p);
+        DevBuf* bufs[] = {&D->hit_f, &D->hit_tbg, &D->fb, &D->stats};
+        for (DevBuf* b : bufs)
+            if (b->p) (void)hipFree(b->p);
+        for (int k = 0; k < 14; k++) {
+            if (D->qa[k].p) (void)hipFree(D->qa[k].p);
+            if (D->qb[k].p) (void)hipFree(D->qb[k].p);
+        }
+        if (D->pinned_count) (void)hipHostFree(D->pinned_count);
+        if (D->stream) (void)hipStreamDestroy(D->stream);
+        hipEvent_t evs[] = {D->ev0, D->ev1, D->evp0, D->evp1};
+        for (hipEvent_t e : evs)
+            if (e) (void)hipEventDestroy(e);
+    }
+    delete sc;
+}
+
+int mcpt_scene_counts(const mcpt_scene* sc, int32_t* nf, int32_t* nm, int32_t* nl) {
+    if (!sc) return MCPT_E_INVALID;
+    if (nf) *nf = sc->host.F;
+    if (nm) *nm = sc->host.M;
+    if (nl) *nl = sc->host.NL;
+    return MCPT_OK;
+}
+
+int mcpt_scene_arrays(const mcpt_scene* sc, float* pos, float* nrm, int32_t* mat, float* mtl, int32_t* lf,
+                      double* lrad, double* un) {
+    if (!sc) return MCPT_E_INVALID;
+    const HostScene& h = sc->host;
+    if (pos) std::copy(h.pos.begin(), h.pos.end(), pos);
+    if (nrm) std::copy(h.nrm.begin(), h.nrm.end(), nrm);
+    if (mat) std::copy(h.mat.begin(), h.mat.end(), mat);
+    if (mtl) std::copy(h.mtl.begin(), h.mtl.end(), mtl);
+    if (lf) std::copy(h.light_facet.begin(), h.light_facet.end(), lf);
+    if (lrad) std::copy(h.light_rad.begin(), h.light_rad.end(), lrad);
+    if (un) std::copy(h.unique_n.begin(), h.unique_n.end(), un);
+    return MCPT_OK;
+}
+
+int mcpt_scene_camera(const mcpt_scene* sc, mcpt_camera* cam) {
+    if (!sc || !cam) return MCPT_E_INVALID;
+    if (!sc->host.has_cam) {
+        set_error("scene XML has no <camera>");
+        return MCPT_E_SCENE;
+    }
+    *cam = sc->host.cam;
+    return MCPT_OK;
+}
+
+int mcpt_render_device(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* dev_out,
+                       mcpt_stats* stats) {
+    if (!sc || !o || !dev_out) {
+        set_error("null argument");
+        return MCPT_E_INVALID;
+    }
+    int rc = validate_camera(cam);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    DeviceState* D;
+    if ((rc = get_device_state(sc, o->device, &D))) return rc;
+    // the caller's buffer may still be written by work on other streams (e.g. torch's)
+    HIP_OK(hipDeviceSynchronize());
+    return render_on_device(sc, *D, cam, o, dev_out, stats);
+}
+
+int mcpt_render(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* out_rgb,
+                mcpt_stats* stats) {
+    if (!sc || !o || !out_rgb) {
+        set_error("null argument");
+        return MCPT_E_INVALID;
+    }
+    int rc = validate_camera(cam);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    DeviceState* D;
+    if ((rc = get_device_state(sc, o->device, &D))) return rc;
+    const size_t n = 3ull * cam->width * cam->height;
+    if ((rc = ensure(D->fb, n * sizeof(double)))) return rc;
+    HIP_OK(hipMemcpyAsync(D->fb.p, out_rgb, n * sizeof(double), hipMemcpyHostToDevice, D->stream));
+    if ((rc = render_on_device(sc, *D, cam, o, (double*)D->fb.p, stats))) return rc;
+    HIP_OK(hipMemcpyAsync(out_rgb, D->fb.p, n * sizeof(double), hipMemcpyDeviceToHost, D->stream));
+    HIP_OK(hipStreamSynchronize(D->stream));
+    return MCPT_OK;
+}
+
+int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* rd, const int32_t* ex,
+                     int32_t light_only, int32_t* facet, double* tbg) {
+    if (!sc || n < 0 || (n && (!ro || !rd || !ex || !facet || !tbg))) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    if (n == 0) return MCPT_OK;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    DeviceState* D;
+    int rc;
+    if ((rc = get_device_state(sc, -1, &D))) return rc;
+    void *dro, *drd, *dex, *df, *dt;
+    HIP_OK(hipMalloc(&dro, 24ull * n));
+    HIP_OK(hipMalloc(&drd, 24ull * n));
+    HIP_OK(hipMalloc(&dex, 4ull * n));
+    HIP_OK(hipMalloc(&df, 4ull * n));
+    HIP_OK(hipMalloc(&dt, 24ull * n));
+    HIP_OK(hipMemcpy(dro, ro, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(drd, rd, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(dex, ex, 4ull * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_trace_batch, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d, n,
+                       (const double*)dro, (const double*)drd, (const int*)dex, light_only, (int*)df, (double*)dt);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(D->stream));
+    HIP_OK(hipMemcpy(facet, df, 4ull * n, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(tbg, dt, 24ull * n, hipMemcpyDeviceToHost));
+    (void)hipFree(dro);
+    (void)hipFree(drd);
+    (void)hipFree(dex);
+    (void)hipFree(df);
+    (void)hipFree(dt);
+    return MCPT_OK;
+}
+
+int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* nrm, const double* u, double* wsum,
+                    int32_t* count, int32_t* pick) {
+    if (!sc || n < 0 || (n && (!x1 || !nrm || !u || !wsum || !count || !pick))) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    if (n == 0) return MCPT_OK;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    DeviceState* D;
+    int rc;
+    if ((rc = get_device_state(sc, -1, &D))) return rc;
+    void *dp, *dn, *du, *dw, *dc, *dk;
+    HIP_OK(hipMalloc(&dp, 24ull * n));
+    HIP_OK(hipMalloc(&dn, 24ull * n));
+    HIP_OK(hipMalloc(&du, 8ull * n));
+    HIP_OK(hipMalloc(&dw, 8ull * n));
+    HIP_OK(hipMalloc(&dc, 4ull * n));
+    HIP_OK(hipMalloc(&dk, 4ull * n));
+    HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
+    const int nchunks = prep_chunks(D->d.NL);
+    hipLaunchKernelGGL(k_prep, dim3((n + 3) / 4), dim3(256), 4 * (size_t)nchunks * sizeof(double), D->stream, D->d,
+                       (uint64_t)0, n, (const double*)dp, (const double*)dn, (const int*)nullptr, (const int*)nullptr,
+                       (const uint64_t*)nullptr, (const double*)du, (double*)dw, (int*)dk, (int*)dc,
+                       (unsigned long long*)nullptr, nchunks);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(D->stream));
+    HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(count, dc, 4ull * n, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
+    for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
+    void* bufs[] = {dp, dn, du, dw, dc, dk};
+    for (void* b : bufs) (void)hipFree(b);
+    return MCPT_OK;
+}
+
+int mcpt_primary_hits(mcpt_scene* sc, const mcpt_camera* cam, int32_t* facet, double* tbg) {
+    if (!sc || !facet || !tbg) {
+        set_error("null argument");
+        return MCPT_E_INVALID;
+    }
+    int rc = validate_camera(cam);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    DeviceState* D;
+    if ((rc = get_device_state(sc, -1, &D))) return rc;
+    const int npx = cam->width * cam->height;
+    if ((rc = ensure(D->hit_f, 4ull * npx)) || (rc = ensure(D->hit_tbg, 24ull * npx))) return rc;
+    hipLaunchKernelGGL(k_primary, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d,
+                       cam_setup(*cam), (int*)D->hit_f.p, (double*)D->hit_tbg.p);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(D->stream));
+    HIP_OK(hipMemcpy(facet, D->hit_f.p, 4ull * npx, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(tbg, D->hit_tbg.p, 24ull * npx, hipMemcpyDeviceToHost));
+    return MCPT_OK;
+}
+
+}  // extern "C"
