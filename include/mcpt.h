@@ -86,6 +86,7 @@ typedef struct {
     uint64_t light_evals_total;           /* shading nodes x light triangles (MIS) */
     uint64_t light_evals_culled_backface; /* culled by the light-side test (Mylight.cpp:340-345) */
     uint64_t light_evals_culled_plane;    /* culled by the tangent-plane test (Mylight.cpp:347-357) */
+    uint64_t light_evals_candidates;      /* passed both; evaluated in full (Mylight.cpp:360-413) */
 } mcpt_stats;
 
 int mcpt_version(void);

@@ -195,6 +195,78 @@ __device__ inline bool light_tri_eval(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d
     return light_tri_stage(p0, p1, p2, nl, lsum, x1, n, o) == 0;
 }
 
+// ---- light prep, GPU formulation ---------------------------------------------------------
+// Stage 1+2 (cheap, exact reference arithmetic): the light-side test (Mylight.cpp:340-345) and
+// the tangent-plane test (:347-357).  Returns true if the triangle is a candidate.
+// 0 = candidate, 1 = culled by the light-side test, 2 = culled by the tangent-plane test
+__device__ inline int light_cheap_stage(d3 p0, d3 p1, d3 p2, d3 nl, d3 x1, d3 n) {
+    double tmp = dot(nl, sub(x1, p0));
+    if (tmp < 0 || fabs(tmp) < MCPT_EPS) return 1;
+    double t0 = dot(n, sub(p0, x1)), t1 = dot(n, sub(p1, x1)), t2 = dot(n, sub(p2, x1));
+    return ((t0 < 0 || fabs(t0) < MCPT_EPS) && (t1 < 0 || fabs(t1) < MCPT_EPS) && (t2 < 0 || fabs(t2) < MCPT_EPS)) ? 2 : 0;
+}
+__device__ inline bool light_cheap(d3 p0, d3 p1, d3 p2, d3 nl, d3 x1, d3 n) {
+    return light_cheap_stage(p0, p1, p2, nl, x1, n) == 0;
+}
+
+__device__ inline double fdot(d3 a, d3 b) { return fma(a.x, b.x, fma(a.y, b.y, a.z * b.z)); }
+__device__ inline d3 fcross(d3 a, d3 b) {
+    return d3{fma(a.y, b.z, -a.z * b.y), fma(a.z, b.x, -a.x * b.z), fma(a.x, b.y, -a.y * b.x)};
+}
+__device__ inline d3 funit(d3 a) {
+    const double r = rsqrt(fdot(a, a));
+    return d3{a.x * r, a.y * r, a.z * r};
+}
+__device__ inline double clamp1(double x) { return fmax(-1.0, fmin(1.0, x)); }
+
+// Stage 3 (Mylight.cpp:360-413) in fp64 with fewer instructions than the reference's literal
+// formulation; identical up to rounding (DESIGN.md "light prep numerics"):
+//  * unit vectors by rsqrt instead of sqrt + 3 divisions; the B/C orientation test on the
+//    un-normalised edge vectors (normalising by positive lengths cannot change the sign);
+//  * the edge-length culls a,b,c < 1e-8 rad as clamp(cos) >= 1: in fp64, acos(x) < 1e-8 iff x
+//    rounds to 1 (acos of the largest double below 1 is 1.49e-8), so no acos is needed for them;
+//  * the vertex-angle culls alpha, beta, gamma < 1e-8 likewise as clamp(-cos) >= 1, with the
+//    cosines from the un-normalised cross products scaled by rsqrt;
+//  * the spherical excess sA = alpha + beta + gamma - pi by the Van Oosterom-Strackee identity
+//    sA = 2 atan2(|A.(BxC)|, 1 + A.B + B.C + C.A) (one atan2 instead of three acos, and free of the
+//    cancellation of alpha+beta+gamma-pi for small triangles);
+//  * alpha (needed only by Arvo's sampling of the picked triangle) and c only when want_alpha_c.
+// Returns true if the triangle survives; fills o.
+__device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, d3 n, SphTri* o, bool want_c) {
+    // want_c: also compute alpha and c = acos(A.B) (Arvo sampling of the picked triangle)
+    const d3 A = funit(sub(p0, x1));
+    d3 B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
+    if (fdot(fcross(sub(C, A), sub(B, A)), n) < 0) {
+        const d3 t = B;
+        B = C;
+        C = t;
+    }
+    const double cab = clamp1(fdot(A, B));
+    if (clamp1(fdot(B, C)) >= 1.0 || clamp1(fdot(A, C)) >= 1.0 || cab >= 1.0) return false;
+    const d3 u1 = fcross(B, A), u2 = fcross(A, C), u3 = fcross(C, B);
+    const double r1 = rsqrt(fdot(u1, u1)), r2 = rsqrt(fdot(u2, u2)), r3 = rsqrt(fdot(u3, u3));
+    const double ca = clamp1(-(fdot(u1, u2) * r1 * r2));
+    const double cb = clamp1(-(fdot(u3, u1) * r3 * r1));
+    const double cg = clamp1(-(fdot(u2, u3) * r2 * r3));
+    if (ca >= 1.0 || cb >= 1.0 || cg >= 1.0) return false;
+    const double num = fabs(fdot(A, fcross(B, C)));
+    const double den = 1.0 + fdot(A, B) + fdot(B, C) + fdot(C, A);
+    const double sA = 2.0 * atan2(num, den);
+    if (sA < 0) return false;
+    const double w = sA * lsum;
+    if (w < 0 || isinf(w) || isnan(w)) return false;
+    if (o) {
+        o->A = A;
+        o->B = B;
+        o->C = C;
+        o->alpha = want_c ? acos(ca) : 0.0;
+        o->c = want_c ? acos(cab) : 0.0;
+        o->sA = sA;
+        o->w = w;
+    }
+    return true;
+}
+
 // Arvo SampleTriangle (Mylight.cpp:453-461)
 __device__ inline d3 arvo_sample(const SphTri& st, double ksi1, double ksi2) {
     double sA1 = ksi1 * st.sA;

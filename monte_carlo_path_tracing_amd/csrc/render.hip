@@ -313,10 +313,14 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
     node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
 }
 
-// Light prep, one wave per node (Mylight.cpp:322-422): lane l evaluates light triangle 64c+l
-// of chunk c.  Chunk totals are the last lane of an inclusive wave scan, stored in LDS; the total
-// weight is their sequential sum; the inverse-CDF pick (first survivor whose cumulative weight
-// >= u * weights_sum, u = dim 1) re-evaluates only the chunk that contains the target.
+// Light prep, one wave per node (Mylight.cpp:322-422).
+//  pass 1: chunks of 64 light triangles run the cheap cull stages (light side, tangent plane);
+//          candidates are compacted into a per-wave LDS queue, and every 64 queued candidates are
+//          evaluated densely (full stage, fp64) as one batch: wave inclusive scan -> batch total.
+//          weights_sum = sequential sum of the batch totals (index order is preserved).
+//  pass 2: the inverse-CDF pick (first survivor whose cumulative weight >= u*weights_sum, u = dim
+//          1) re-runs the cheap stages to rebuild only the batch that holds the target and
+//          re-evaluates those <= 64 candidates.
 // u_override / count_out: test entry (mcpt_light_prep).
 __device__ inline double wave_incl_scan(double v, int lane) {
 #pragma unroll
@@ -327,87 +331,147 @@ __device__ inline double wave_incl_scan(double v, int lane) {
     return v;
 }
 
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct PrepLight {
+    d3 p0, p1, p2, nl;
+    double lsum;
+};
+__device__ inline PrepLight load_light(const DScene& S, int li) {
+    const double4 ln = S.lt_n[li];
+    return PrepLight{f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]), mk3(ln.x, ln.y, ln.z), ln.w};
+}
+__device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n) {
+    if (li >= S.NL) return 3;
+    const double4 ln = S.lt_n[li];
+    return light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]), mk3(ln.x, ln.y, ln.z),
+                             x1, n);
+}
+
+constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
+
 __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                               const double* __restrict__ qn, const int* __restrict__ qpixel,
                                               const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                               const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                               int* __restrict__ pick_out, int* __restrict__ count_out,
                                               unsigned long long* stats, int nchunks) {
-    extern __shared__ double chunk_lds[];
+    extern __shared__ double prep_lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
-    double* ctot = chunk_lds + (size_t)wib * nchunks;
+    // per wave: [nchunks doubles batch totals][kPrepQueue ints]
+    double* bt = prep_lds + (size_t)wib * (nchunks + kPrepQueue / 2);
+    int* q = reinterpret_cast<int*>(bt + nchunks);
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int nwaves = gridDim.x * (blockDim.x >> 6);
-    unsigned long long surv_acc = 0, c1_acc = 0, c2_acc = 0;
+    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
     for (int node = blockIdx.x * (blockDim.x >> 6) + wib; node < n; node += nwaves) {
         const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
         const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
-        int survivors = 0, cull1 = 0, cull2 = 0;
-        int last_chunk = -1;
+        int qcnt = 0, nb = 0, survivors = 0, candidates = 0, culled1 = 0;
+        // ---- pass 1 ----
         for (int c = 0; c < nchunks; c++) {
             const int li = c * 64 + lane;
-            double w = 0;
-            int stage = 4;
-            if (li < S.NL) {
-                const double4 ln = S.lt_n[li];
-                SphTri st;
-                stage = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                        mk3(ln.x, ln.y, ln.z), ln.w, x1, nn, &st);
-                if (stage == 0) w = st.w;
+            const int stage = prep_stage(S, li, x1, nn);
+            const bool cand = stage == 0;
+            const uint64_t m = __ballot(cand);
+            if (cand) q[qcnt + __popcll(m & lt_mask)] = li;
+            qcnt += __popcll(m);
+            candidates += __popcll(m);
+            culled1 += __popcll(__ballot(stage == 1));
+            const bool last = (c == nchunks - 1);
+            while (qcnt >= 64 || (last && qcnt > 0)) {
+                wave_lds_sync();
+                const bool act = lane < qcnt;
+                const int lj = act ? q[lane] : 0;
+                double w = 0;
+                bool ok = false;
+                if (act) {
+                    const PrepLight L = load_light(S, lj);
+                    SphTri st;
+                    ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
+                    if (ok) w = st.w;
+                }
+                const double sc = wave_incl_scan(w, lane);
+                survivors += __popcll(__ballot(ok));
+                if (lane == 63) bt[nb] = sc;
+                nb++;
+                const int rem = qcnt > 64 ? qcnt - 64 : 0;
+                const int mv = lane < rem ? q[64 + lane] : 0;
+                wave_lds_sync();
+                if (lane < rem) q[lane] = mv;
+                qcnt = rem;
             }
-            const double sc = wave_incl_scan(w, lane);
-            const uint64_t m = __ballot(stage == 0);
-            survivors += __popcll(m);
-            cull1 += __popcll(__ballot(stage == 1));
-            cull2 += __popcll(__ballot(stage == 2));
-            if (m) last_chunk = c;
-            if (lane == 63) ctot[c] = sc;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_lds_sync();
         double wsum = 0;
-        for (int c = 0; c < nchunks; c++) wsum += ctot[c];
+        for (int b = 0; b < nb; b++) wsum += bt[b];
+        // ---- pass 2: inverse-CDF pick ----
         int pick = -1;
         if (!(fabs(wsum) < MCPT_EPS)) {
             double u;
             if (u_override) u = u_override[node];
             else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
             const double target = u * wsum;
-            double cum = 0;
-            int cc = -1;
-            double base = 0;
-            for (int c = 0; c < nchunks; c++) {
-                const double nxt = cum + ctot[c];
-                if (nxt >= target && ctot[c] > 0) {
-                    cc = c;
+            int kb = -1, lastpos = -1;
+            double cum = 0, base = 0;
+            for (int b = 0; b < nb; b++) {
+                const double nxt = cum + bt[b];
+                if (bt[b] > 0) lastpos = b;
+                if (kb < 0 && nxt >= target && bt[b] > 0) {
+                    kb = b;
                     base = cum;
-                    break;
                 }
                 cum = nxt;
             }
-            if (cc < 0) {  // rounding: fall back to the last chunk with a survivor
-                cc = last_chunk;
+            if (kb < 0) {  // rounding: fall back to the last batch with weight
+                kb = lastpos;
                 base = 0;
-                for (int c = 0; c < cc; c++) base += ctot[c];
+                for (int b = 0; b < kb; b++) base += bt[b];
             }
-            const int li = cc * 64 + lane;
+            // rebuild the candidate queue up to batch kb
+            qcnt = 0;
+            int formed = 0;
+            for (int c = 0; c < nchunks; c++) {
+                const int li = c * 64 + lane;
+                const bool cand = prep_stage(S, li, x1, nn) == 0;
+                const uint64_t m = __ballot(cand);
+                if (cand) q[qcnt + __popcll(m & lt_mask)] = li;
+                qcnt += __popcll(m);
+                if (qcnt >= 64 || (c == nchunks - 1 && qcnt > 0)) {
+                    if (formed == kb) break;
+                    const int rem = qcnt > 64 ? qcnt - 64 : 0;
+                    wave_lds_sync();
+                    const int mv = lane < rem ? q[64 + lane] : 0;
+                    wave_lds_sync();
+                    if (lane < rem) q[lane] = mv;
+                    qcnt = rem;
+                    formed++;
+                    if (c == nchunks - 1 && qcnt > 0 && formed == kb) break;
+                }
+            }
+            wave_lds_sync();
+            const bool act = lane < qcnt && lane < 64;
+            const int lj = act ? q[lane] : 0;
             double w = 0;
             bool ok = false;
-            if (li < S.NL) {
-                const double4 ln = S.lt_n[li];
+            if (act) {
+                const PrepLight L = load_light(S, lj);
                 SphTri st;
-                ok = light_tri_eval(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                    mk3(ln.x, ln.y, ln.z), ln.w, x1, nn, &st);
+                ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
                 if (ok) w = st.w;
             }
             const double sc = wave_incl_scan(w, lane);
-            const uint64_t cand = __ballot(ok && (base + sc >= target));
+            const uint64_t candm = __ballot(ok && (base + sc >= target));
             const uint64_t okm = __ballot(ok);
-            int pl;
-            if (cand) pl = __ffsll((unsigned long long)cand) - 1;
-            else pl = 63 - __clzll((long long)okm);
-            pick = cc * 64 + pl;
+            int pl = -1;
+            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+            else if (okm) pl = 63 - __clzll((long long)okm);
+            if (pl >= 0) pick = __shfl(lj, pl);
         }
         if (lane == 0) {
             wsum_out[node] = wsum;
@@ -415,14 +479,14 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
             if (count_out) count_out[node] = survivors;
         }
         surv_acc += survivors;
-        c1_acc += cull1;
-        c2_acc += cull2;
-        __builtin_amdgcn_wave_barrier();
+        cand_acc += candidates;
+        c1_acc += culled1;
+        wave_lds_sync();
     }
     if (lane == 0 && stats) {
         if (surv_acc) atomicAdd(stats + 1, surv_acc);
-        if (c1_acc) atomicAdd(stats + 5, c1_acc);
-        if (c2_acc) atomicAdd(stats + 6, c2_acc);
+        if (cand_acc) atomicAdd(stats + 5, cand_acc);
+        if (c1_acc) atomicAdd(stats + 6, c1_acc);
     }
 }
 
@@ -457,8 +521,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur,
         if (pick >= 0) {
             const double4 ln = S.lt_n[pick];
             SphTri sph;
-            light_tri_eval(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]),
-                           mk3(ln.x, ln.y, ln.z), ln.w, p, N, &sph);
+            light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph,
+                       true);
             const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
             TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
             coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:475-481)
@@ -496,9 +560,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur,
                 Hit hl = trace(S.lbvh, S.lleaf_v, p, wi, f, st, kTraceBlock);
                 if (hl.f >= 0 && !(fabs(wsum) < MCPT_EPS)) {
                     const int li = S.tri_light[hl.f];
-                    const double4 ln = S.lt_n[li];
-                    if (light_tri_eval(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                       mk3(ln.x, ln.y, ln.z), ln.w, p, N, nullptr))
+                    const PrepLight L = load_light(S, li);
+                    if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) &&
+                        light_full(L.p0, L.p1, L.p2, L.lsum, p, N, nullptr, false))
                         lpdf = S.light_sum[li] / wsum;  // fresh-state eval (Mylight.cpp:484-493)
                 }
                 tp2 = mul(hmul(tp, b), dot(wi, N) / (pdf + lpdf) / MCPT_P_RR);
@@ -726,6 +790,7 @@ int validate_camera(const mcpt_camera* cam) {
 }
 
 int prep_chunks(int NL) { return std::max(1, (NL + 63) / 64); }
+size_t prep_lds_bytes(int nchunks) { return 4 * ((size_t)nchunks * sizeof(double) + kPrepQueue * sizeof(int)); }
 
 // the wavefront render into a device framebuffer already resident on D's device
 int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o,
@@ -767,7 +832,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                        (int*)D.hit_f.p, (double*)D.hit_tbg.p);
     HIP_OK(hipGetLastError());
     const int nchunks = prep_chunks(D.d.NL);
-    const size_t prep_lds = 4 * (size_t)nchunks * sizeof(double);
+    const size_t prep_lds = prep_lds_bytes(nchunks);
     if (prep_lds > 160 * 1024) {
         set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
         return MCPT_E_SCENE;
@@ -836,8 +901,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->light_rays = hs[3];
         stats->generations = gens;
         stats->shading_nodes = nodes_total;
-        stats->light_evals_culled_backface = hs[5];
-        stats->light_evals_culled_plane = hs[6];
+        stats->light_evals_culled_backface = hs[6];
+        stats->light_evals_candidates = hs[5];
+        stats->light_evals_culled_plane = stats->light_evals_total - hs[5] - hs[6];
         stats->light_evals_total = (uint64_t)nodes_total * (o->mode == MCPT_MODE_MIS ? (uint64_t)D.d.NL : 0ull);
         stats->prep_seconds = prep_ms * 1e-3;
         stats->prep_launches = prep_launches;
@@ -1066,7 +1132,7 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
     const int nchunks = prep_chunks(D->d.NL);
-    hipLaunchKernelGGL(k_prep, dim3((n + 3) / 4), dim3(256), 4 * (size_t)nchunks * sizeof(double), D->stream, D->d,
+    hipLaunchKernelGGL(k_prep, dim3((n + 3) / 4), dim3(256), prep_lds_bytes(nchunks), D->stream, D->d,
                        (uint64_t)0, n, (const double*)dp, (const double*)dn, (const int*)nullptr, (const int*)nullptr,
                        (const uint64_t*)nullptr, (const double*)du, (double*)dw, (int*)dk, (int*)dc,
                        (unsigned long long*)nullptr, nchunks);
