@@ -132,6 +132,7 @@ def main():
     samples = float(W * H) * frame_spp
     value = samples / elapsed / 1e6
 
+    log("rank %d totals: %s" % (rank, json.dumps({k: v for k, v in totals.items()})))
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -140,7 +141,9 @@ def main():
                                                          "light_evals_culled_plane", "light_evals_survived"))
     launches = max(totals.get("prep_launches", 0), 1)
     prep_s = totals.get("prep_seconds", 0.0)
-    flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + (ev_tot - c1 - c2) * FLOPS_FULL
+    cand = totals.get("light_evals_candidates", 0)
+    c2 = ev_tot - c1 - cand
+    flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
     if args.mode == "mis" and prep_s > 0:
         achieved = flops / launches / (prep_s / launches) / 1e12
         traffic = None

@@ -78,6 +78,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise MCPTError("libmcpt_hip.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                             "or `make -C monte_carlo_path_tracing_amd/csrc`")
+        # One HIP runtime per process: torch wheels bundle their own libamdhip64.so.7 /
+        # libhsa-runtime64.so.1 (same sonames as /opt/rocm's).  Loading torch first makes this
+        # library bind to torch's runtime, so device pointers and streams are shared; loading
+        # /opt/rocm's runtime first would leave torch without a usable GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         P, I, D = C.c_void_p, C.c_int32, C.c_double
         dp = np.ctypeslib.ndpointer(np.float64, flags="C")

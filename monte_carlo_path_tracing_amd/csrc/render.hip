@@ -46,7 +46,8 @@ struct DScene {
     const double* light_rad;  // NL*3
     const double* light_sum;  // NL
     const int* light_facet;   // NL
-    const float4* lt_v;       // NL*3 light vertices (reference order)
+    const float4* lt_v;       // NL*3 light vertices (reference order); .w = float(unique normal)
+    float light_bound;        // max |coordinate| over light vertices
     const double4* lt_n;      // NL: unique normal xyz, w = RadianceRGB::sum()
     const BvhNode* bvh;       // all facets
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
@@ -345,11 +346,36 @@ __device__ inline PrepLight load_light(const DScene& S, int li) {
     const double4 ln = S.lt_n[li];
     return PrepLight{f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]), mk3(ln.x, ln.y, ln.z), ln.w};
 }
-__device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n) {
+// The cheap stages evaluated in fp32 with a rigorous rounding-error bound `err`, falling back to
+// the exact fp64 reference arithmetic only when a value lies within err of the 1e-8 threshold:
+// the decisions are exactly those of Mylight.cpp:340-357.  Light-side test: culled iff
+// nl.(x1-p0) < 1e-8; tangent-plane test: culled iff n.(pi-x1) < 1e-8 for all three vertices.
+// lt_v[3l+k].w holds float(nl[k]).
+struct NodeF {
+    float x, y, z, nx, ny, nz, err;
+};
+__device__ inline NodeF node_f(d3 x1, d3 n, float scene_bound) {
+    const float X = fmaxf(fmaxf(fabsf((float)x1.x), fabsf((float)x1.y)), fabsf((float)x1.z));
+    // |t_f32 - t| <= 15 u (X + P) for u = 2^-24 (DESIGN.md "light prep numerics"); 2^-19 (X+P) bounds it
+    return NodeF{(float)x1.x, (float)x1.y, (float)x1.z, (float)n.x, (float)n.y, (float)n.z,
+                 0x1.0p-19f * (X + scene_bound) + 1e-30f};
+}
+__device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n, const NodeF& nf) {
     if (li >= S.NL) return 3;
-    const double4 ln = S.lt_n[li];
-    return light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]), mk3(ln.x, ln.y, ln.z),
-                             x1, n);
+    const float4 a = S.lt_v[3 * li], b = S.lt_v[3 * li + 1], c = S.lt_v[3 * li + 2];
+    constexpr float kEps = 1e-8f;
+    const float s1 = fmaf(a.w, nf.x - a.x, fmaf(b.w, nf.y - a.y, c.w * (nf.z - a.z)));
+    if (s1 < kEps - nf.err) return 1;
+    const float t0 = fmaf(nf.nx, a.x - nf.x, fmaf(nf.ny, a.y - nf.y, nf.nz * (a.z - nf.z)));
+    const float t1 = fmaf(nf.nx, b.x - nf.x, fmaf(nf.ny, b.y - nf.y, nf.nz * (b.z - nf.z)));
+    const float t2 = fmaf(nf.nx, c.x - nf.x, fmaf(nf.ny, c.y - nf.y, nf.nz * (c.z - nf.z)));
+    const float tm = fmaxf(fmaxf(t0, t1), t2);
+    if (s1 > kEps + nf.err) {
+        if (tm < kEps - nf.err) return 2;
+        if (tm > kEps + nf.err) return 0;
+    }
+    const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
+    return light_cheap_stage(f3(a), f3(b), f3(c), mk3(ln.x, ln.y, ln.z), x1, n);
 }
 
 constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
@@ -372,11 +398,12 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
     for (int node = blockIdx.x * (blockDim.x >> 6) + wib; node < n; node += nwaves) {
         const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
         const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        const NodeF nf = node_f(x1, nn, S.light_bound);
         int qcnt = 0, nb = 0, survivors = 0, candidates = 0, culled1 = 0;
         // ---- pass 1 ----
         for (int c = 0; c < nchunks; c++) {
             const int li = c * 64 + lane;
-            const int stage = prep_stage(S, li, x1, nn);
+            const int stage = prep_stage(S, li, x1, nn, nf);
             const bool cand = stage == 0;
             const uint64_t m = __ballot(cand);
             if (cand) q[qcnt + __popcll(m & lt_mask)] = li;
@@ -438,7 +465,7 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
             int formed = 0;
             for (int c = 0; c < nchunks; c++) {
                 const int li = c * 64 + lane;
-                const bool cand = prep_stage(S, li, x1, nn) == 0;
+                const bool cand = prep_stage(S, li, x1, nn, nf) == 0;
                 const uint64_t m = __ballot(cand);
                 if (cand) q[qcnt + __popcll(m & lt_mask)] = li;
                 qcnt += __popcll(m);
@@ -723,6 +750,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     DScene& d = D->d;
     d.F = s.F;
     d.NL = s.NL;
+    d.light_bound = 0.0f;
     std::vector<float4> tv(3 * std::max(s.F, 1));
     for (int f = 0; f < s.F; f++)
         for (int k = 0; k < 3; k++) tv[3 * f + k] = make_float4(s.pos[9 * f + 3 * k], s.pos[9 * f + 3 * k + 1], s.pos[9 * f + 3 * k + 2], 0.f);
@@ -739,7 +767,12 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     std::vector<double4> ln(std::max(s.NL, 1));
     for (int l = 0; l < s.NL; l++) {
         const int f = s.light_facet[l];
-        for (int k = 0; k < 3; k++) lv[3 * l + k] = tv[3 * f + k];
+        for (int k = 0; k < 3; k++) {
+            lv[3 * l + k] = tv[3 * f + k];
+            lv[3 * l + k].w = (float)s.unique_n[3 * f + k];
+            d.light_bound = std::max({d.light_bound, std::fabs(lv[3 * l + k].x), std::fabs(lv[3 * l + k].y),
+                                      std::fabs(lv[3 * l + k].z)});
+        }
         ln[l] = make_double4(s.unique_n[3 * f], s.unique_n[3 * f + 1], s.unique_n[3 * f + 2], s.light_sum[l]);
     }
     if ((rc = upload(*D, lv, &d.lt_v))) return rc;
