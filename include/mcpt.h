@@ -127,6 +127,11 @@ int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const doubl
  * -1 if empty or weights_sum < 1e-8). */
 int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                     double* weights_sum, int32_t* count, int32_t* pick);
+/* diagnostics: run the light-prep kernel variant `variant` (-1 auto, 0 LDS queue, 1 stored LDS
+ * candidate list, 2 stored list + software prefetch) `iters` times on the n points and report the
+ * mean device time per launch; outputs as mcpt_light_prep (pick = facet). */
+int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
+                          int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 /* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */
 int mcpt_primary_hits(mcpt_scene* scene, const mcpt_camera* cam, int32_t* facet, double* tbg);
 

@@ -68,7 +68,8 @@ _lib = None
 # every symbol include/mcpt.h declares (tests check the .so exports them all)
 EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_create", "mcpt_scene_destroy",
            "mcpt_scene_counts", "mcpt_scene_arrays", "mcpt_scene_camera", "mcpt_render", "mcpt_render_device",
-           "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map", "mcpt_write_bmp"]
+           "mcpt_closest_hit", "mcpt_light_prep", "mcpt_debug_prep_bench", "mcpt_primary_hits", "mcpt_tone_map",
+           "mcpt_write_bmp"]
 
 
 def lib():
@@ -106,6 +107,7 @@ def lib():
         L.mcpt_closest_hit.argtypes = [P, I, dp, dp, ip, I, ip, dp]
         L.mcpt_light_prep.argtypes = [P, I, dp, dp, dp, dp, ip, ip]
         L.mcpt_primary_hits.argtypes = [P, C.POINTER(Camera), ip, dp]
+        L.mcpt_debug_prep_bench.argtypes = [P, I, dp, dp, dp, I, I, C.POINTER(C.c_double), dp, ip]
         L.mcpt_tone_map.argtypes = [dp, I, I, D, D, u8]
         L.mcpt_write_bmp.argtypes = [C.c_char_p, u8, I, I]
         _lib = L
@@ -214,6 +216,15 @@ def light_prep(scene, x1, normal, u):
     ws, cnt, pick = np.zeros(n), np.zeros(n, np.int32), np.zeros(n, np.int32)
     _check(lib().mcpt_light_prep(scene.h, n, x1, normal, u, ws, cnt, pick))
     return ws, cnt, pick
+
+
+def debug_prep_bench(scene, x1, normal, u, variant=-1, iters=5):
+    """Diagnostics: mean ms per launch of a light-prep kernel variant (see include/mcpt.h)."""
+    x1, normal, u = _d(x1, (-1, 3)), _d(normal, (-1, 3)), _d(u, (-1,))
+    n = x1.shape[0]
+    ms, ws, pick = C.c_double(), np.zeros(n), np.zeros(n, np.int32)
+    _check(lib().mcpt_debug_prep_bench(scene.h, n, x1, normal, u, int(variant), int(iters), C.byref(ms), ws, pick))
+    return ms.value, ws, pick
 
 
 def primary_hits(scene, camera):

@@ -360,9 +360,9 @@ __device__ inline NodeF node_f(d3 x1, d3 n, float scene_bound) {
     return NodeF{(float)x1.x, (float)x1.y, (float)x1.z, (float)n.x, (float)n.y, (float)n.z,
                  0x1.0p-19f * (X + scene_bound) + 1e-30f};
 }
-__device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n, const NodeF& nf) {
+__device__ inline int prep_stage_regs(const DScene& S, int li, float4 a, float4 b, float4 c, d3 x1, d3 n,
+                                      const NodeF& nf) {
     if (li >= S.NL) return 3;
-    const float4 a = S.lt_v[3 * li], b = S.lt_v[3 * li + 1], c = S.lt_v[3 * li + 2];
     constexpr float kEps = 1e-8f;
     const float s1 = fmaf(a.w, nf.x - a.x, fmaf(b.w, nf.y - a.y, c.w * (nf.z - a.z)));
     if (s1 < kEps - nf.err) return 1;
@@ -376,6 +376,10 @@ __device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n, const Nod
     }
     const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
     return light_cheap_stage(f3(a), f3(b), f3(c), mk3(ln.x, ln.y, ln.z), x1, n);
+}
+__device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n, const NodeF& nf) {
+    if (li >= S.NL) return 3;
+    return prep_stage_regs(S, li, S.lt_v[3 * li], S.lt_v[3 * li + 1], S.lt_v[3 * li + 2], x1, n, nf);
 }
 
 constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
@@ -507,6 +511,138 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
         }
         surv_acc += survivors;
         cand_acc += candidates;
+        c1_acc += culled1;
+        wave_lds_sync();
+    }
+    if (lane == 0 && stats) {
+        if (surv_acc) atomicAdd(stats + 1, surv_acc);
+        if (cand_acc) atomicAdd(stats + 5, cand_acc);
+        if (c1_acc) atomicAdd(stats + 6, c1_acc);
+    }
+}
+
+// Light prep, stored-candidate-list form (used when the per-wave list fits in LDS): pass 1 appends
+// every candidate's light index to a per-wave LDS list (uint16); batch k is list[64k, 64k+64), so
+// pass 2 re-evaluates exactly one batch without re-running the cheap stages.  kPrefetch issues the
+// next chunk's light-vertex loads before the current chunk's tests (software pipelining).
+template <bool kPrefetch>
+__global__ __launch_bounds__(256) void k_prep_list(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
+                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                                   const double* __restrict__ u_override, double* __restrict__ wsum_out,
+                                                   int* __restrict__ pick_out, int* __restrict__ count_out,
+                                                   unsigned long long* stats, int nchunks, int wave_bytes) {
+    extern __shared__ double prep_lds[];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
+    unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const int nwaves = gridDim.x * (blockDim.x >> 6);
+    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
+    for (int node = blockIdx.x * (blockDim.x >> 6) + wib; node < n; node += nwaves) {
+        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        const NodeF nf = node_f(x1, nn, S.light_bound);
+        int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
+        float4 pa = make_float4(0, 0, 0, 0), pb = pa, pc = pa;
+        if (kPrefetch && lane < S.NL) {
+            pa = S.lt_v[3 * lane];
+            pb = S.lt_v[3 * lane + 1];
+            pc = S.lt_v[3 * lane + 2];
+        }
+        for (int c = 0; c < nchunks; c++) {
+            const int li = c * 64 + lane;
+            float4 a, b, cc;
+            if (kPrefetch) {
+                a = pa;
+                b = pb;
+                cc = pc;
+                const int ln = li + 64;
+                if (c + 1 < nchunks && ln < S.NL) {
+                    pa = S.lt_v[3 * ln];
+                    pb = S.lt_v[3 * ln + 1];
+                    pc = S.lt_v[3 * ln + 2];
+                }
+            } else if (li < S.NL) {
+                a = S.lt_v[3 * li];
+                b = S.lt_v[3 * li + 1];
+                cc = S.lt_v[3 * li + 2];
+            }
+            const int stage = prep_stage_regs(S, li, a, b, cc, x1, nn, nf);
+            const uint64_t m = __ballot(stage == 0);
+            if (stage == 0) lst[ncand + __popcll(m & lt_mask)] = (unsigned short)li;
+            ncand += __popcll(m);
+            culled1 += __popcll(__ballot(stage == 1));
+            while (ncand - 64 * nb >= 64 || (c == nchunks - 1 && ncand > 64 * nb)) {
+                wave_lds_sync();
+                const int k = 64 * nb + lane;
+                const bool act = k < ncand;
+                double w = 0;
+                bool ok = false;
+                if (act) {
+                    const PrepLight L = load_light(S, lst[k]);
+                    SphTri st;
+                    ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
+                    if (ok) w = st.w;
+                }
+                const double sc = wave_incl_scan(w, lane);
+                survivors += __popcll(__ballot(ok));
+                if (lane == 63) bt[nb] = sc;
+                nb++;
+            }
+        }
+        wave_lds_sync();
+        double wsum = 0;
+        for (int b = 0; b < nb; b++) wsum += bt[b];
+        int pick = -1;
+        if (!(fabs(wsum) < MCPT_EPS)) {
+            double u;
+            if (u_override) u = u_override[node];
+            else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+            const double target = u * wsum;
+            int kb = -1, lastpos = -1;
+            double cum = 0, base = 0;
+            for (int b = 0; b < nb; b++) {
+                const double nxt = cum + bt[b];
+                if (bt[b] > 0) lastpos = b;
+                if (kb < 0 && nxt >= target && bt[b] > 0) {
+                    kb = b;
+                    base = cum;
+                }
+                cum = nxt;
+            }
+            if (kb < 0) {
+                kb = lastpos;
+                base = 0;
+                for (int b = 0; b < kb; b++) base += bt[b];
+            }
+            const int k = 64 * kb + lane;
+            const bool act = k < ncand;
+            const int lj = act ? (int)lst[k] : 0;
+            double w = 0;
+            bool ok = false;
+            if (act) {
+                const PrepLight L = load_light(S, lj);
+                SphTri st;
+                ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
+                if (ok) w = st.w;
+            }
+            const double sc = wave_incl_scan(w, lane);
+            const uint64_t candm = __ballot(ok && (base + sc >= target));
+            const uint64_t okm = __ballot(ok);
+            int pl = -1;
+            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+            else if (okm) pl = 63 - __clzll((long long)okm);
+            if (pl >= 0) pick = __shfl(lj, pl);
+        }
+        if (lane == 0) {
+            wsum_out[node] = wsum;
+            pick_out[node] = pick;
+            if (count_out) count_out[node] = survivors;
+        }
+        surv_acc += survivors;
+        cand_acc += ncand;
         c1_acc += culled1;
         wave_lds_sync();
     }
@@ -824,6 +960,31 @@ int validate_camera(const mcpt_camera* cam) {
 
 int prep_chunks(int NL) { return std::max(1, (NL + 63) / 64); }
 size_t prep_lds_bytes(int nchunks) { return 4 * ((size_t)nchunks * sizeof(double) + kPrepQueue * sizeof(int)); }
+// per-wave bytes of k_prep_list: batch totals + uint16 candidate list, 16-byte aligned
+int prep_list_wave_bytes(int nchunks) { return (int)((nchunks * 8 + nchunks * 64 * 2 + 15) / 16 * 16); }
+constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
+
+// variant: -1 auto (list+prefetch when it fits, else queue), 0 queue, 1 list, 2 list+prefetch
+hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
+                       const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
+                       int* pick, int* count, unsigned long long* stats, hipStream_t st) {
+    const int nchunks = prep_chunks(d.NL);
+    const int wb = prep_list_wave_bytes(nchunks);
+    const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
+    if (variant < 0) variant = list_ok ? 2 : 0;
+    if (variant > 0 && !list_ok) variant = 0;
+    const int blocks = std::min((n + 3) / 4, 1 << 20);
+    if (variant == 0)
+        hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
+                           qsample, qnode, u, wsum, pick, count, stats, nchunks);
+    else if (variant == 1)
+        hipLaunchKernelGGL(k_prep_list<false>, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
+                           qnode, u, wsum, pick, count, stats, nchunks, wb);
+    else
+        hipLaunchKernelGGL(k_prep_list<true>, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
+                           qnode, u, wsum, pick, count, stats, nchunks, wb);
+    return hipGetLastError();
+}
 
 // the wavefront render into a device framebuffer already resident on D's device
 int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o,
@@ -894,12 +1055,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             gens++;
             nodes_total += (uint64_t)n;
             if (o->mode == MCPT_MODE_MIS) {
-                const int blocks = std::min((n + 3) / 4, 1 << 20);
                 HIP_OK(hipEventRecord(D.evp0, st));
-                hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds, st, D.d, o->seed, n, cur->p, cur->n,
-                                   cur->pixel, cur->sample, cur->node, (const double*)nullptr, cur->wsum, cur->pick,
-                                   (int*)nullptr, P.stats, nchunks);
-                HIP_OK(hipGetLastError());
+                HIP_OK(launch_prep(-1, D.d, o->seed, n, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
+                                   cur->wsum, cur->pick, nullptr, P.stats, st));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 prep_launches++;
             }
@@ -934,10 +1092,11 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->light_rays = hs[3];
         stats->generations = gens;
         stats->shading_nodes = nodes_total;
+
+        stats->light_evals_total = (uint64_t)nodes_total * (o->mode == MCPT_MODE_MIS ? (uint64_t)D.d.NL : 0ull);
         stats->light_evals_culled_backface = hs[6];
         stats->light_evals_candidates = hs[5];
         stats->light_evals_culled_plane = stats->light_evals_total - hs[5] - hs[6];
-        stats->light_evals_total = (uint64_t)nodes_total * (o->mode == MCPT_MODE_MIS ? (uint64_t)D.d.NL : 0ull);
         stats->prep_seconds = prep_ms * 1e-3;
         stats->prep_launches = prep_launches;
     }
@@ -1164,18 +1323,52 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
-    const int nchunks = prep_chunks(D->d.NL);
-    hipLaunchKernelGGL(k_prep, dim3((n + 3) / 4), dim3(256), prep_lds_bytes(nchunks), D->stream, D->d,
-                       (uint64_t)0, n, (const double*)dp, (const double*)dn, (const int*)nullptr, (const int*)nullptr,
-                       (const uint64_t*)nullptr, (const double*)du, (double*)dw, (int*)dk, (int*)dc,
-                       (unsigned long long*)nullptr, nchunks);
-    HIP_OK(hipGetLastError());
+    HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+                       (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, D->stream));
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(count, dc, 4ull * n, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
     for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
     void* bufs[] = {dp, dn, du, dw, dc, dk};
+    for (void* b : bufs) (void)hipFree(b);
+    return MCPT_OK;
+}
+
+int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const double* nrm, const double* u,
+                          int32_t variant, int32_t iters, double* ms, double* wsum, int32_t* pick) {
+    if (!sc || n <= 0 || !x1 || !nrm || !u || iters <= 0 || !ms || !wsum || !pick) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(sc->mu);
+    DeviceState* D;
+    int rc;
+    if ((rc = get_device_state(sc, -1, &D))) return rc;
+    void *dp, *dn, *du, *dw, *dk;
+    HIP_OK(hipMalloc(&dp, 24ull * n));
+    HIP_OK(hipMalloc(&dn, 24ull * n));
+    HIP_OK(hipMalloc(&du, 8ull * n));
+    HIP_OK(hipMalloc(&dw, 8ull * n));
+    HIP_OK(hipMalloc(&dk, 4ull * n));
+    HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
+    HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+                       (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, D->stream));  // warm-up
+    HIP_OK(hipEventRecord(D->ev0, D->stream));
+    for (int it = 0; it < iters; it++)
+        HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+                           (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, D->stream));
+    HIP_OK(hipEventRecord(D->ev1, D->stream));
+    HIP_OK(hipEventSynchronize(D->ev1));
+    float t = 0;
+    HIP_OK(hipEventElapsedTime(&t, D->ev0, D->ev1));
+    *ms = t / iters;
+    HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
+    for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
+    void* bufs[] = {dp, dn, du, dw, dk};
     for (void* b : bufs) (void)hipFree(b);
     return MCPT_OK;
 }

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""A/B the light-prep kernel variants in one process (interleaved rounds) on the shading points
+of the 800x600 primary hits of the Veach-MIS stand-in.  GPU only.
+
+    python tools/prep_variants.py [--variants 0,1,2] [--rounds 3] [--iters 5]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import monte_carlo_path_tracing_amd as mcpt  # noqa: E402
+
+
+def shading_points(scene, W=800, H=600):
+    f, tbg = mcpt.primary_hits(scene, mcpt.Camera.reference(W, H))
+    a = scene.arrays()
+    hit = f >= 0
+    f, b, g = f[hit], tbg[hit, 1], tbg[hit, 2]
+    P = a["positions"].astype(np.float64).reshape(-1, 3, 3)[f]
+    Nv = a["normals"].astype(np.float64).reshape(-1, 3, 3)[f]
+    w0 = (1.0 - b - g)[:, None]
+    x1 = P[:, 0] * w0 + P[:, 1] * b[:, None] + P[:, 2] * g[:, None]
+    n = Nv[:, 0] * w0 + Nv[:, 1] * b[:, None] + Nv[:, 2] * g[:, None]
+    n /= np.linalg.norm(n, axis=1)[:, None]
+    isl = np.zeros(len(a["positions"]), bool)
+    isl[a["light_facet"]] = True
+    keep = ~isl[f]
+    return x1[keep], n[keep]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=5)
+    args = ap.parse_args()
+    scene = mcpt.Scene.load(os.path.join(ROOT, "scenes/veach-mis/veach-mis.obj"),
+                            os.path.join(ROOT, "scenes/veach-mis/veach-mis.xml"))
+    x1, n = shading_points(scene)
+    u = np.random.default_rng(1).random(len(x1))
+    variants = [int(v) for v in args.variants.split(",")]
+    times = {v: [] for v in variants}
+    outs = {}
+    for r in range(args.rounds):
+        for v in variants:
+            ms, ws, pick = mcpt.debug_prep_bench(scene, x1, n, u, variant=v, iters=args.iters)
+            times[v].append(ms)
+            outs[v] = (ws, pick)
+    base = variants[0]
+    for v in variants:
+        ws, pick = outs[v]
+        rel = np.abs(ws - outs[base][0]) / np.maximum(np.abs(outs[base][0]), 1e-300)
+        print("variant %d: %d points, median %.3f ms (min %.3f) = %.2f M nodes/s; vs %d: max rel wsum %.1e, "
+              "pick mismatches %d" % (v, len(x1), np.median(times[v]), np.min(times[v]),
+                                     len(x1) / np.median(times[v]) / 1e3, base, rel.max(),
+                                     (pick != outs[base][1]).sum()))
+
+
+if __name__ == "__main__":
+    main()
