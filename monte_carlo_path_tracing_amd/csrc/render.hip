@@ -383,13 +383,14 @@ __device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n, const Nod
 }
 
 constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
+constexpr int kPrepGrab = 4;     // nodes a wave takes per work-counter atomic
 
 __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                               const double* __restrict__ qn, const int* __restrict__ qpixel,
                                               const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                               const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                               int* __restrict__ pick_out, int* __restrict__ count_out,
-                                              unsigned long long* stats, int nchunks) {
+                                              unsigned long long* stats, int nchunks, unsigned* __restrict__ work) {
     extern __shared__ double prep_lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
@@ -397,9 +398,19 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
     double* bt = prep_lds + (size_t)wib * (nchunks + kPrepQueue / 2);
     int* q = reinterpret_cast<int*>(bt + nchunks);
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const int nwaves = gridDim.x * (blockDim.x >> 6);
     unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
-    for (int node = blockIdx.x * (blockDim.x >> 6) + wib; node < n; node += nwaves) {
+    int grab = 0, left = 0;
+    while (true) {
+        // dynamic distribution: a wave grabs kPrepGrab nodes per atomic (node costs vary ~10x)
+        if (left == 0) {
+            unsigned b = 0;
+            if (lane == 0) b = atomicAdd(work, (unsigned)kPrepGrab);
+            grab = __shfl((int)b, 0);
+            left = kPrepGrab;
+        }
+        const int node = grab++;
+        left--;
+        if (node >= n) break;
         const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
         const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
         const NodeF nf = node_f(x1, nn, S.light_bound);
@@ -531,16 +542,27 @@ __global__ __launch_bounds__(256) void k_prep_list(DScene S, uint64_t seed, int 
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                    const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                    int* __restrict__ pick_out, int* __restrict__ count_out,
-                                                   unsigned long long* stats, int nchunks, int wave_bytes) {
+                                                   unsigned long long* stats, int nchunks, int wave_bytes,
+                                                   unsigned* __restrict__ work) {
     extern __shared__ double prep_lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
     unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const int nwaves = gridDim.x * (blockDim.x >> 6);
     unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
-    for (int node = blockIdx.x * (blockDim.x >> 6) + wib; node < n; node += nwaves) {
+    int grab = 0, left = 0;
+    while (true) {
+        // dynamic distribution: a wave grabs kPrepGrab nodes per atomic (node costs vary ~10x)
+        if (left == 0) {
+            unsigned b = 0;
+            if (lane == 0) b = atomicAdd(work, (unsigned)kPrepGrab);
+            grab = __shfl((int)b, 0);
+            left = kPrepGrab;
+        }
+        const int node = grab++;
+        left--;
+        if (node >= n) break;
         const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
         const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
         const NodeF nf = node_f(x1, nn, S.light_bound);
@@ -817,7 +839,7 @@ struct DeviceState {
     std::vector<void*> allocs;
     hipStream_t stream = nullptr;
     // reusable work buffers
-    DevBuf hit_f, hit_tbg, fb, stats, qa[14], qb[14];
+    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14];
     unsigned* pinned_count = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr;
 };
@@ -965,24 +987,28 @@ int prep_list_wave_bytes(int nchunks) { return (int)((nchunks * 8 + nchunks * 64
 constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 
 // variant: -1 auto (list+prefetch when it fits, else queue), 0 queue, 1 list, 2 list+prefetch
+// work: a device word, zeroed here before the launch (the kernel's dynamic node counter)
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
-                       int* pick, int* count, unsigned long long* stats, hipStream_t st) {
+                       int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st) {
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
     if (variant < 0) variant = list_ok ? 2 : 0;
     if (variant > 0 && !list_ok) variant = 0;
-    const int blocks = std::min((n + 3) / 4, 1 << 20);
+    // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
+    const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
+    hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
     if (variant == 0)
         hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
-                           qsample, qnode, u, wsum, pick, count, stats, nchunks);
+                           qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
     else if (variant == 1)
         hipLaunchKernelGGL(k_prep_list<false>, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
-                           qnode, u, wsum, pick, count, stats, nchunks, wb);
+                           qnode, u, wsum, pick, count, stats, nchunks, wb, work);
     else
         hipLaunchKernelGGL(k_prep_list<true>, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
-                           qnode, u, wsum, pick, count, stats, nchunks, wb);
+                           qnode, u, wsum, pick, count, stats, nchunks, wb, work);
     return hipGetLastError();
 }
 
@@ -1008,7 +1034,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int qf = o->queue_factor > 0 ? o->queue_factor : 2;
     const int cap = (int)std::min<long long>((long long)qf * roots + 1024, (1ll << 30));
     int rc;
-    if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) || (rc = ensure(D.stats, 64)))
+    if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) || (rc = ensure(D.stats, 64)) ||
+        (rc = ensure(D.work, 256)))
         return rc;
     Queue qa, qb;
     if ((rc = alloc_queue(D.qa, cap, qa)) || (rc = alloc_queue(D.qb, cap, qb))) return rc;
@@ -1057,7 +1084,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             if (o->mode == MCPT_MODE_MIS) {
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, n, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                   cur->wsum, cur->pick, nullptr, P.stats, st));
+                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 prep_launches++;
             }
@@ -1184,7 +1211,7 @@ void mcpt_scene_destroy(mcpt_scene* sc) {
     for (auto& D : sc->devs) {
         (void)hipSetDevice(D->device);
         for (void* p : D->allocs) (void)hipFree(p);
-        DevBuf* bufs[] = {&D->hit_f, &D->hit_tbg, &D->fb, &D->stats};
+        DevBuf* bufs[] = {&D->hit_f, &D->hit_tbg, &D->fb, &D->stats, &D->work};
         for (DevBuf* b : bufs)
             if (b->p) (void)hipFree(b->p);
         for (int k = 0; k < 14; k++) {
@@ -1323,8 +1350,9 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
+    if ((rc = ensure(D->work, 256))) return rc;
     HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
-                       (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, D->stream));
+                       (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream));
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(count, dc, 4ull * n, hipMemcpyDeviceToHost));
@@ -1354,12 +1382,13 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
+    if ((rc = ensure(D->work, 256))) return rc;
     HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
-                       (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, D->stream));  // warm-up
+                       (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream));
     HIP_OK(hipEventRecord(D->ev0, D->stream));
     for (int it = 0; it < iters; it++)
         HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
-                           (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, D->stream));
+                           (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream));
     HIP_OK(hipEventRecord(D->ev1, D->stream));
     HIP_OK(hipEventSynchronize(D->ev1));
     float t = 0;
