@@ -219,14 +219,47 @@ __device__ inline d3 funit(d3 a) {
 }
 __device__ inline double clamp1(double x) { return fmax(-1.0, fmin(1.0, x)); }
 
+// atan2(y, x) for y >= 0 in fp64 (<= ~4 ulp): one division and a degree-9 polynomial in z^2 on
+// |z| <= tan(pi/8), fitted in extended precision (tools/fit_atan.py); ~40 instructions instead of
+// ocml's ~100.  Octant reduction: y <= k|x|: z = y/|x|; |x| <= k y: z = -|x|/y (+pi/2);
+// otherwise z = (y-|x|)/(y+|x|) (+pi/4); then pi - r for x < 0.
+__device__ inline double atan2_pos(double y, double x) {
+    constexpr double k = 0.41421356237309503;  // tan(pi/8)
+    const double ax = fabs(x);
+    const bool A = y <= k * ax, D = !A && ax <= k * y;
+    const double num = A ? y : (D ? -ax : y - ax);
+    const double den = A ? ax : (D ? y : y + ax);
+    const double r0 = A ? 0.0 : (D ? 1.5707963267948966 : 0.7853981633974483);
+    const double z = num / den, s = z * z;
+    double p = 0.023022964535612277;
+    p = fma(p, s, -0.045054138438556275);
+    p = fma(p, s, 0.05743860627393907);
+    p = fma(p, s, -0.0665101622857059);
+    p = fma(p, s, 0.07691210259772996);
+    p = fma(p, s, -0.09090862908839843);
+    p = fma(p, s, 0.11111110041613353);
+    p = fma(p, s, -0.14285714274661848);
+    p = fma(p, s, 0.19999999999980458);
+    p = fma(p, s, -0.33333333333333476);
+    const double a = r0 + fma(z * s, p, z);
+    return x < 0 ? 3.141592653589793 - a : a;
+}
+
+// Weight of one light triangle for the prep kernel (Mylight.cpp:360-413): the same quantity as
+// light_full's w without the parts only Arvo's sampler needs (orientation, alpha, c).  The edge
+// culls a,b,c < 1e-8 are kept (as clamp(cos) >= 1); the vertex-angle culls alpha,beta,gamma < 1e-8
+// mark a degenerate (zero-area) spherical triangle, which here is sA <= 0.  Returns false if culled.
+__device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, double* w_out);
+
 // Stage 3 (Mylight.cpp:360-413) in fp64 with fewer instructions than the reference's literal
 // formulation; identical up to rounding (DESIGN.md "light prep numerics"):
 //  * unit vectors by rsqrt instead of sqrt + 3 divisions; the B/C orientation test on the
 //    un-normalised edge vectors (normalising by positive lengths cannot change the sign);
 //  * the edge-length culls a,b,c < 1e-8 rad as clamp(cos) >= 1: in fp64, acos(x) < 1e-8 iff x
 //    rounds to 1 (acos of the largest double below 1 is 1.49e-8), so no acos is needed for them;
-//  * the vertex-angle culls alpha, beta, gamma < 1e-8 likewise as clamp(-cos) >= 1, with the
-//    cosines from the un-normalised cross products scaled by rsqrt;
+//  * the vertex-angle culls alpha, beta, gamma < 1e-8 (a degenerate, zero-area spherical
+//    triangle) as sA <= 0 -- identical to light_weight, so the prep kernel and this function agree
+//    on every survivor;
 //  * the spherical excess sA = alpha + beta + gamma - pi by the Van Oosterom-Strackee identity
 //    sA = 2 atan2(|A.(BxC)|, 1 + A.B + B.C + C.A) (one atan2 instead of three acos, and free of the
 //    cancellation of alpha+beta+gamma-pi for small triangles);
@@ -241,29 +274,38 @@ __device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, d3 n,
         B = C;
         C = t;
     }
-    const double cab = clamp1(fdot(A, B));
-    if (clamp1(fdot(B, C)) >= 1.0 || clamp1(fdot(A, C)) >= 1.0 || cab >= 1.0) return false;
-    const d3 u1 = fcross(B, A), u2 = fcross(A, C), u3 = fcross(C, B);
-    const double r1 = rsqrt(fdot(u1, u1)), r2 = rsqrt(fdot(u2, u2)), r3 = rsqrt(fdot(u3, u3));
-    const double ca = clamp1(-(fdot(u1, u2) * r1 * r2));
-    const double cb = clamp1(-(fdot(u3, u1) * r3 * r1));
-    const double cg = clamp1(-(fdot(u2, u3) * r2 * r3));
-    if (ca >= 1.0 || cb >= 1.0 || cg >= 1.0) return false;
-    const double num = fabs(fdot(A, fcross(B, C)));
-    const double den = 1.0 + fdot(A, B) + fdot(B, C) + fdot(C, A);
-    const double sA = 2.0 * atan2(num, den);
-    if (sA < 0) return false;
+    const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
+    if (clamp1(bc) >= 1.0 || clamp1(ca) >= 1.0 || clamp1(ab) >= 1.0) return false;
+    const double sA = 2.0 * atan2_pos(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
+    if (!(sA > 0)) return false;  // degenerate: the vertex-angle culls (see light_weight)
     const double w = sA * lsum;
     if (w < 0 || isinf(w) || isnan(w)) return false;
     if (o) {
         o->A = A;
         o->B = B;
         o->C = C;
-        o->alpha = want_c ? acos(ca) : 0.0;
-        o->c = want_c ? acos(cab) : 0.0;
+        o->alpha = 0.0;
+        o->c = 0.0;
+        if (want_c) {  // alpha = angle at A between the great arcs AB and AC (Mylight.cpp:385)
+            const d3 u1 = fcross(B, A), u2 = fcross(A, C);
+            o->alpha = acos(clamp1(-(fdot(u1, u2) * rsqrt(fdot(u1, u1)) * rsqrt(fdot(u2, u2)))));
+            o->c = acos(clamp1(ab));
+        }
         o->sA = sA;
         o->w = w;
     }
+    return true;
+}
+
+__device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, double* w_out) {
+    const d3 A = funit(sub(p0, x1)), B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
+    const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
+    if (clamp1(bc) >= 1.0 || clamp1(ca) >= 1.0 || clamp1(ab) >= 1.0) return false;
+    const double sA = 2.0 * atan2_pos(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
+    if (!(sA > 0)) return false;
+    const double w = sA * lsum;
+    if (w < 0 || isinf(w) || isnan(w)) return false;
+    *w_out = w;
     return true;
 }
 

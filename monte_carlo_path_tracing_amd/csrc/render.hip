@@ -434,9 +434,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
                 bool ok = false;
                 if (act) {
                     const PrepLight L = load_light(S, lj);
-                    SphTri st;
-                    ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
-                    if (ok) w = st.w;
+                    ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
+                    if (!ok) w = 0;
                 }
                 const double sc = wave_incl_scan(w, lane);
                 survivors += __popcll(__ballot(ok));
@@ -503,9 +502,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
             bool ok = false;
             if (act) {
                 const PrepLight L = load_light(S, lj);
-                SphTri st;
-                ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
-                if (ok) w = st.w;
+                ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
+                if (!ok) w = 0;
             }
             const double sc = wave_incl_scan(w, lane);
             const uint64_t candm = __ballot(ok && (base + sc >= target));
@@ -604,9 +602,8 @@ __global__ __launch_bounds__(256) void k_prep_list(DScene S, uint64_t seed, int 
                 bool ok = false;
                 if (act) {
                     const PrepLight L = load_light(S, lst[k]);
-                    SphTri st;
-                    ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
-                    if (ok) w = st.w;
+                    ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
+                    if (!ok) w = 0;
                 }
                 const double sc = wave_incl_scan(w, lane);
                 survivors += __popcll(__ballot(ok));
@@ -646,9 +643,8 @@ __global__ __launch_bounds__(256) void k_prep_list(DScene S, uint64_t seed, int 
             bool ok = false;
             if (act) {
                 const PrepLight L = load_light(S, lj);
-                SphTri st;
-                ok = light_full(L.p0, L.p1, L.p2, L.lsum, x1, nn, &st, false);
-                if (ok) w = st.w;
+                ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
+                if (!ok) w = 0;
             }
             const double sc = wave_incl_scan(w, lane);
             const uint64_t candm = __ballot(ok && (base + sc >= target));
@@ -746,8 +742,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur,
                 if (hl.f >= 0 && !(fabs(wsum) < MCPT_EPS)) {
                     const int li = S.tri_light[hl.f];
                     const PrepLight L = load_light(S, li);
-                    if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) &&
-                        light_full(L.p0, L.p1, L.p2, L.lsum, p, N, nullptr, false))
+                    double wl_unused;
+                    if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) && light_weight(L.p0, L.p1, L.p2, L.lsum, p, &wl_unused))
                         lpdf = S.light_sum[li] / wsum;  // fresh-state eval (Mylight.cpp:484-493)
                 }
                 tp2 = mul(hmul(tp, b), dot(wi, N) / (pdf + lpdf) / MCPT_P_RR);
