@@ -323,12 +323,23 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
 //          1) re-runs the cheap stages to rebuild only the batch that holds the target and
 //          re-evaluates those <= 64 candidates.
 // u_override / count_out: test entry (mcpt_light_prep).
+// Inclusive wave64 prefix sum of doubles with DPP (GFX9 row_shr / row_bcast; no LDS traffic).
+// Out-of-range sources read 0 (update_dpp's `old` operand), so every step is a plain add.
+template <int kCtrl, int kRowMask>
+__device__ inline double dpp_shift(double v) {
+    const unsigned long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, kCtrl, kRowMask, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), kCtrl, kRowMask, 0xf, false);
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
 __device__ inline double wave_incl_scan(double v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        double t = __shfl_up(v, o);
-        if (lane >= o) v += t;
-    }
+    (void)lane;
+    v += dpp_shift<0x111, 0xf>(v);  // row_shr:1
+    v += dpp_shift<0x112, 0xf>(v);  // row_shr:2
+    v += dpp_shift<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_shift<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_shift<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp_shift<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
@@ -534,8 +545,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
 // every candidate's light index to a per-wave LDS list (uint16); batch k is list[64k, 64k+64), so
 // pass 2 re-evaluates exactly one batch without re-running the cheap stages.  kPrefetch issues the
 // next chunk's light-vertex loads before the current chunk's tests (software pipelining).
-template <bool kPrefetch>
-__global__ __launch_bounds__(256) void k_prep_list(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
+template <bool kPrefetch, int kMinWavesPerSimd>
+__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_list(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                    const double* __restrict__ qn, const int* __restrict__ qpixel,
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                    const double* __restrict__ u_override, double* __restrict__ wsum_out,
@@ -990,21 +1001,28 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = list_ok ? 2 : 0;
+    if (variant < 0) variant = list_ok ? 1 : 0;
     if (variant > 0 && !list_ok) variant = 0;
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
     hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
     if (e != hipSuccess) return e;
-    if (variant == 0)
-        hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
-                           qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
-    else if (variant == 1)
-        hipLaunchKernelGGL(k_prep_list<false>, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
-                           qnode, u, wsum, pick, count, stats, nchunks, wb, work);
-    else
-        hipLaunchKernelGGL(k_prep_list<true>, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
-                           qnode, u, wsum, pick, count, stats, nchunks, wb, work);
+#define MCPT_PREP_LIST(PF, W)                                                                                \
+    hipLaunchKernelGGL((k_prep_list<PF, W>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample, \
+                       qnode, u, wsum, pick, count, stats, nchunks, wb, work)
+    switch (variant) {
+        case 0:
+            hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
+                               qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
+            break;
+        case 1: MCPT_PREP_LIST(false, 1); break;
+        case 2: MCPT_PREP_LIST(true, 1); break;
+        case 3: MCPT_PREP_LIST(false, 5); break;
+        case 4: MCPT_PREP_LIST(false, 6); break;
+        case 5: MCPT_PREP_LIST(true, 5); break;
+        default: MCPT_PREP_LIST(false, 1); break;
+    }
+#undef MCPT_PREP_LIST
     return hipGetLastError();
 }
 
