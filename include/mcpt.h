@@ -127,9 +127,10 @@ int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const doubl
  * -1 if empty or weights_sum < 1e-8). */
 int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                     double* weights_sum, int32_t* count, int32_t* pick);
-/* diagnostics: run the light-prep kernel variant `variant` (-1 auto, 0 LDS queue, 1 stored LDS
- * candidate list, 2 stored list + software prefetch) `iters` times on the n points and report the
- * mean device time per launch; outputs as mcpt_light_prep (pick = facet). */
+/* diagnostics: run the light-prep kernel variant `variant` (-1 auto = 3; 0 LDS candidate queue,
+ * 1 stored LDS candidate list, 2 list + software prefetch, 3 list at 5 waves/SIMD, 4 list at 6
+ * waves/SIMD, 5 list + prefetch at 5 waves/SIMD) `iters` times on the n points and report the mean
+ * device time per launch; outputs as mcpt_light_prep (pick = facet). */
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 /* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */

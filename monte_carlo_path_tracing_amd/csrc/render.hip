@@ -1001,7 +1001,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = list_ok ? 1 : 0;
+    if (variant < 0) variant = list_ok ? 3 : 0;  // A/B on MI355X: tools/prep_variants.py
     if (variant > 0 && !list_ok) variant = 0;
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
