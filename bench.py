@@ -33,6 +33,9 @@ HBM_PEAK_GBS = 8000.0
 FLOPS_CULL_BACKFACE = 8
 FLOPS_CULL_PLANE = 32
 FLOPS_FULL = 269
+# algorithmic HBM bytes of one prep node: reads p, N (48 B) + pixel, sample, node id (16 B) for the
+# RNG key; writes weights_sum + pick (12 B).  The light table (240 KB) is L2/MALL resident.
+PREP_BYTES_PER_NODE = 76
 SCENE = os.path.join(ROOT, "scenes", "veach-mis")
 
 
@@ -157,7 +160,7 @@ def main():
                     "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
                     "traffic": traffic, "avg_launch_ms": round(prep_s / launches * 1e3, 3), "launches": launches,
                     "flop_per_launch": flops / launches, "share_of_device_time": round(prep_s / max(totals["seconds"], 1e-12), 3),
-                    "hbm_algorithmic_GBs": round(totals.get("shading_nodes", 0) * 60 / prep_s / 1e9, 3),
+                    "hbm_algorithmic_GBs": round(totals.get("shading_nodes", 0) * PREP_BYTES_PER_NODE / prep_s / 1e9, 3),
                     "hbm_peak_GBs": HBM_PEAK_GBS}
     else:
         roofline = {"bound": "valu_fp64", "kernel": "k_extend_brdf", "achieved": None, "peak": FP64_VECTOR_PEAK_TFLOPS,

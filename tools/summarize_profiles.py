@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Turns the rocprofv3 CSVs of a GPU run (gpurun_out/) into the committed summaries (profiles/).
+
+    python tools/summarize_profiles.py --tag round1 --stats gpurun_out/prof_r1 \
+        --fetch gpurun_out/pmc_r1_fetch --write gpurun_out/pmc_r1_write --sq gpurun_out/pmc_r1_sq \
+        --bench gpurun_out/bench_default.log
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) is doubled (gfx950 tallies the 128-B
+requests of 16-B-per-lane loads at 64 B), WRITE_SIZE is taken as is; both come from separate
+--pmc passes.  They are L2 fabric-side requests, so Infinity-Cache hits are included (an upper
+bound on HBM bytes).
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def counters(d):
+    path = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+    return {k: dict(v, dispatches=len(disp[k])) for k, v in agg.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--stats", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--sq")
+    ap.add_argument("--bench")
+    a = ap.parse_args()
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    stats_csv = glob.glob(os.path.join(a.stats, "*kernel_stats.csv"))[0]
+    rows = list(csv.DictReader(open(stats_csv)))
+    with open(os.path.join(out, "%s_kernel_stats.csv" % a.tag), "w") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "total_ms", "avg_us", "percent", "min_us", "max_us"])
+        for r in rows:
+            w.writerow([short(r["Name"]), r["Calls"], "%.3f" % (float(r["TotalDurationNs"]) / 1e6),
+                        "%.2f" % (float(r["AverageNs"]) / 1e3), "%.2f" % float(r["Percentage"]),
+                        "%.2f" % (float(r["MinNs"]) / 1e3), "%.2f" % (float(r["MaxNs"]) / 1e3)])
+    summary = {"kernel_stats": {short(r["Name"]): {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
+                                                   "percent": float(r["Percentage"])} for r in rows}}
+    if a.fetch and a.write:
+        fc, wc = counters(a.fetch), counters(a.write)
+        hbm = {}
+        for k in fc:
+            if k not in wc:
+                continue
+            fetch_b = 2 * fc[k]["FETCH_SIZE"] * 1024
+            write_b = wc[k]["WRITE_SIZE"] * 1024
+            n = fc[k]["dispatches"]
+            hbm[k] = {"dispatches": n, "fetch_bytes_per_dispatch": fetch_b / n,
+                      "write_bytes_per_dispatch": write_b / wc[k]["dispatches"],
+                      "grbm_gui_active": wc[k].get("GRBM_GUI_ACTIVE")}
+        summary["hbm"] = hbm
+    if a.sq:
+        summary["sq"] = counters(a.sq)
+    if a.bench and os.path.exists(a.bench):
+        for line in open(a.bench):
+            if line.startswith("{"):
+                summary["bench"] = json.loads(line)
+            if line.startswith("rank 0 totals:"):
+                summary["bench_totals"] = json.loads(line.split(":", 1)[1])
+    with open(os.path.join(out, "%s_summary.json" % a.tag), "w") as f:
+        json.dump(summary, f, indent=1, sort_keys=True)
+    print(json.dumps({k: summary[k] for k in summary if k != "sq"}, indent=1)[:3000])
+
+
+if __name__ == "__main__":
+    main()
