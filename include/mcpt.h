@@ -127,10 +127,11 @@ int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const doubl
  * -1 if empty or weights_sum < 1e-8). */
 int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                     double* weights_sum, int32_t* count, int32_t* pick);
-/* diagnostics: run the light-prep kernel variant `variant` (-1 auto = 3; 0 LDS candidate queue,
+/* diagnostics: run the light-prep kernel variant `variant` (-1 auto = 6; 0 LDS candidate queue,
  * 1 stored LDS candidate list, 2 list + software prefetch, 3 list at 5 waves/SIMD, 4 list at 6
- * waves/SIMD, 5 list + prefetch at 5 waves/SIMD) `iters` times on the n points and report the mean
- * device time per launch; outputs as mcpt_light_prep (pick = facet). */
+ * waves/SIMD, 5 list + prefetch at 5 waves/SIMD, 6 packed-fp32 cheap stages + branch-free fp64
+ * batches at 5 waves/SIMD, 7 the same at 4 waves/SIMD) `iters` times on the n points and report
+ * the mean device time per launch; outputs as mcpt_light_prep (pick = facet). */
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 /* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */

@@ -213,13 +213,26 @@ __device__ inline double fdot(d3 a, d3 b) { return fma(a.x, b.x, fma(a.y, b.y, a
 __device__ inline d3 fcross(d3 a, d3 b) {
     return d3{fma(a.y, b.z, -a.z * b.y), fma(a.z, b.x, -a.x * b.z), fma(a.x, b.y, -a.y * b.x)};
 }
+// a / |a| by the hardware rsqrt estimate plus one third-order Newton step (the refinement ocml's
+// rsqrt uses, without its zero/inf class fix-ups: a zero vector gives NaN either way, which every
+// caller culls)
 __device__ inline d3 funit(d3 a) {
-    const double r = rsqrt(fdot(a, a));
+    const double s = fdot(a, a);
+    const double y = __builtin_amdgcn_rsq(s);
+    const double e = fma(-s * y, y, 1.0);  // 1 - s y^2
+    const double r = fma(y * e, fma(e, 0.375, 0.5), y);
     return d3{a.x * r, a.y * r, a.z * r};
+}
+// num / den for den > 0 (finite): hardware reciprocal estimate plus one third-order step
+// (r (1 + e + e^2), e = 1 - den r), then one rounding in the product (<= ~1.5 ulp)
+__device__ inline double fdiv_pos(double num, double den) {
+    const double r = __builtin_amdgcn_rcp(den);
+    const double e = fma(-den, r, 1.0);
+    return num * fma(r, fma(e, e, e), r);
 }
 __device__ inline double clamp1(double x) { return fmax(-1.0, fmin(1.0, x)); }
 
-// atan2(y, x) for y >= 0 in fp64 (<= ~4 ulp): one division and a degree-9 polynomial in z^2 on
+// atan2(y, x) for y >= 0 in fp64 (<= ~5 ulp): one division and a degree-9 polynomial in z^2 on
 // |z| <= tan(pi/8), fitted in extended precision (tools/fit_atan.py); ~40 instructions instead of
 // ocml's ~100.  Octant reduction: y <= k|x|: z = y/|x|; |x| <= k y: z = -|x|/y (+pi/2);
 // otherwise z = (y-|x|)/(y+|x|) (+pi/4); then pi - r for x < 0.
@@ -230,7 +243,7 @@ __device__ inline double atan2_pos(double y, double x) {
     const double num = A ? y : (D ? -ax : y - ax);
     const double den = A ? ax : (D ? y : y + ax);
     const double r0 = A ? 0.0 : (D ? 1.5707963267948966 : 0.7853981633974483);
-    const double z = num / den, s = z * z;
+    const double z = fdiv_pos(num, den), s = z * z;
     double p = 0.023022964535612277;
     p = fma(p, s, -0.045054138438556275);
     p = fma(p, s, 0.05743860627393907);
@@ -307,6 +320,19 @@ __device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, dou
     if (w < 0 || isinf(w) || isnan(w)) return false;
     *w_out = w;
     return true;
+}
+
+// light_weight without branches, for the prep kernel's dense batches: vertices in fp64, every
+// lane evaluates straight through and the culls become one predicate at the end.  clamp1(x) >= 1
+// (light_full's edge culls) is !(x < 1), NaN included.  Returns w, or 0 if culled (*ok = false).
+__device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, bool* ok) {
+    const d3 A = funit(sub(p0, x1)), B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
+    const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
+    const double sA = 2.0 * atan2_pos(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
+    const double w = sA * lsum;
+    const bool good = (ab < 1.0) & (bc < 1.0) & (ca < 1.0) & (sA > 0) & (w >= 0) & (w <= __DBL_MAX__);
+    *ok = good;
+    return good ? w : 0.0;
 }
 
 // Arvo SampleTriangle (Mylight.cpp:453-461)

@@ -49,6 +49,9 @@ struct DScene {
     const float4* lt_v;       // NL*3 light vertices (reference order); .w = float(unique normal)
     float light_bound;        // max |coordinate| over light vertices
     const double4* lt_n;      // NL: unique normal xyz, w = RadianceRGB::sum()
+    const float4* lt_pk;      // NL*3: (p0.x, p1.x, p2.x, nl.x), (.. .y), (.. .z) -- packed cheap stages
+    const float* lt_d;        // NL: float(nl . p0)
+    const double2* lt_w;      // NL*5: p0, p1, p2 (fp64), RadianceRGB::sum()
     const BvhNode* bvh;       // all facets
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
     const BvhNode* lbvh;      // light facets only
@@ -682,6 +685,151 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_list(DScene S, u
     }
 }
 
+// Light prep, packed form (the default): the stored-candidate-list scheme of k_prep_list with
+//  * cheap stages in packed fp32 (v_pk_fma_f32): lt_pk[3l..3l+2] = X, Y, Z with
+//    X = (p0.x, p1.x, p2.x, nl.x) etc. and lt_d[l] = float(nl.p0), so that
+//    (t0, t1) = n.(p0, p1) - n.x1 and (t2, s1) = (n.p2 - n.x1, nl.x1 - nl.p0) are four packed
+//    FMA chains; n.x1 is rounded once per node.  The error bound of node_f still holds
+//    (DESIGN.md "light prep numerics");
+//  * dense batches in fp64 from lt_w (p0, p1, p2, lsum as 5 double2, no conversions), evaluated
+//    branch-free (light_weight_bf) on every lane.
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ inline int prep_stage_pk(const DScene& S, int li, float4 X, float4 Y, float4 Z, float dl, v2f nx2, v2f ny2,
+                                    v2f nz2, v2f nxs, v2f nys, v2f nzs, float cn, d3 x1, d3 n, float err) {
+    constexpr float kEps = 1e-8f;
+    const v2f tab = __builtin_elementwise_fma(nx2, v2f{X.x, X.y}, __builtin_elementwise_fma(ny2, v2f{Y.x, Y.y}, nz2 * v2f{Z.x, Z.y})) - v2f{cn, cn};
+    const v2f tcs = __builtin_elementwise_fma(nxs, v2f{X.z, X.w}, __builtin_elementwise_fma(nys, v2f{Y.z, Y.w}, nzs * v2f{Z.z, Z.w})) - v2f{cn, dl};
+    const float s1 = tcs.y;
+    if (li >= S.NL) return 3;
+    if (s1 < kEps - err) return 1;
+    const float tm = fmaxf(fmaxf(tab.x, tab.y), tcs.x);
+    if (s1 > kEps + err) {
+        if (tm < kEps - err) return 2;
+        if (tm > kEps + err) return 0;
+    }
+    const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
+    return light_cheap_stage(mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(ln.x, ln.y, ln.z), x1, n);
+}
+__device__ inline double prep_weight_pk(const DScene& S, int li, d3 x1, bool* ok) {
+    const double2* w = S.lt_w + 5 * li;
+    const double2 a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+    return light_weight_bf(mk3(a.x, a.y, b.x), mk3(b.y, c.x, c.y), mk3(d.x, d.y, e.x), e.y, x1, ok);
+}
+
+template <int kMinWavesPerSimd>
+__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
+                                                 const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                                 const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                                 const double* __restrict__ u_override, double* __restrict__ wsum_out,
+                                                 int* __restrict__ pick_out, int* __restrict__ count_out,
+                                                 unsigned long long* stats, int nchunks, int wave_bytes,
+                                                 unsigned* __restrict__ work) {
+    extern __shared__ double prep_lds[];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
+    unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
+    int grab = 0, left = 0;
+    while (true) {
+        if (left == 0) {
+            unsigned b = 0;
+            if (lane == 0) b = atomicAdd(work, (unsigned)kPrepGrab);
+            grab = __shfl((int)b, 0);
+            left = kPrepGrab;
+        }
+        const int node = grab++;
+        left--;
+        if (node >= n) break;
+        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        const NodeF nf = node_f(x1, nn, S.light_bound);
+        const float cn = (float)dot(nn, x1);
+        const v2f nx2{nf.nx, nf.nx}, ny2{nf.ny, nf.ny}, nz2{nf.nz, nf.nz};
+        const v2f nxs{nf.nx, nf.x}, nys{nf.ny, nf.y}, nzs{nf.nz, nf.z};
+        int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
+        for (int c = 0; c < nchunks; c++) {
+            const int li = c * 64 + lane;
+            const int lc = li < S.NL ? li : S.NL - 1;
+            const float4 X = S.lt_pk[3 * lc], Y = S.lt_pk[3 * lc + 1], Z = S.lt_pk[3 * lc + 2];
+            const float dl = S.lt_d[lc];
+            const int stage = prep_stage_pk(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
+            const uint64_t m = __ballot(stage == 0);
+            if (stage == 0) lst[ncand + __popcll(m & lt_mask)] = (unsigned short)li;
+            ncand += __popcll(m);
+            culled1 += __popcll(__ballot(stage == 1));
+            while (ncand - 64 * nb >= 64 || (c == nchunks - 1 && ncand > 64 * nb)) {
+                wave_lds_sync();
+                const int k = 64 * nb + lane;
+                const bool act = k < ncand;
+                bool ok;
+                double w = prep_weight_pk(S, act ? (int)lst[k] : 0, x1, &ok);
+                ok = ok && act;
+                w = act ? w : 0.0;
+                const double sc = wave_incl_scan(w, lane);
+                survivors += __popcll(__ballot(ok));
+                if (lane == 63) bt[nb] = sc;
+                nb++;
+            }
+        }
+        wave_lds_sync();
+        double wsum = 0;
+        for (int b = 0; b < nb; b++) wsum += bt[b];
+        int pick = -1;
+        if (!(fabs(wsum) < MCPT_EPS)) {
+            double u;
+            if (u_override) u = u_override[node];
+            else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+            const double target = u * wsum;
+            int kb = -1, lastpos = -1;
+            double cum = 0, base = 0;
+            for (int b = 0; b < nb; b++) {
+                const double nxt = cum + bt[b];
+                if (bt[b] > 0) lastpos = b;
+                if (kb < 0 && nxt >= target && bt[b] > 0) {
+                    kb = b;
+                    base = cum;
+                }
+                cum = nxt;
+            }
+            if (kb < 0) {
+                kb = lastpos;
+                base = 0;
+                for (int b = 0; b < kb; b++) base += bt[b];
+            }
+            const int k = 64 * kb + lane;
+            const bool act = k < ncand;
+            const int lj = act ? (int)lst[k] : 0;
+            bool ok;
+            double w = prep_weight_pk(S, lj, x1, &ok);
+            ok = ok && act;
+            w = act ? w : 0.0;
+            const double sc = wave_incl_scan(w, lane);
+            const uint64_t candm = __ballot(ok && (base + sc >= target));
+            const uint64_t okm = __ballot(ok);
+            int pl = -1;
+            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+            else if (okm) pl = 63 - __clzll((long long)okm);
+            if (pl >= 0) pick = __shfl(lj, pl);
+        }
+        if (lane == 0) {
+            wsum_out[node] = wsum;
+            pick_out[node] = pick;
+            if (count_out) count_out[node] = survivors;
+        }
+        surv_acc += survivors;
+        cand_acc += ncand;
+        c1_acc += culled1;
+        wave_lds_sync();
+    }
+    if (lane == 0 && stats) {
+        if (surv_acc) atomicAdd(stats + 1, surv_acc);
+        if (cand_acc) atomicAdd(stats + 5, cand_acc);
+        if (c1_acc) atomicAdd(stats + 6, c1_acc);
+    }
+}
+
 // one MIS node (main.cpp:440-493), lane per node; children go through node_entry.
 __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur, int n, Queue nxt) {
     __shared__ int stack[kStack * kTraceBlock];
@@ -942,6 +1090,24 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     }
     if ((rc = upload(*D, lv, &d.lt_v))) return rc;
     if ((rc = upload(*D, ln, &d.lt_n))) return rc;
+    std::vector<float4> lpk(3 * std::max(s.NL, 1));
+    std::vector<float> ld(std::max(s.NL, 1));
+    std::vector<double2> lw(5 * std::max(s.NL, 1));
+    for (int l = 0; l < s.NL; l++) {
+        const float4 a = lv[3 * l], b = lv[3 * l + 1], c = lv[3 * l + 2];
+        lpk[3 * l] = make_float4(a.x, b.x, c.x, a.w);
+        lpk[3 * l + 1] = make_float4(a.y, b.y, c.y, b.w);
+        lpk[3 * l + 2] = make_float4(a.z, b.z, c.z, c.w);
+        ld[l] = (float)(ln[l].x * a.x + ln[l].y * a.y + ln[l].z * a.z);
+        lw[5 * l] = make_double2(a.x, a.y);
+        lw[5 * l + 1] = make_double2(a.z, b.x);
+        lw[5 * l + 2] = make_double2(b.y, b.z);
+        lw[5 * l + 3] = make_double2(c.x, c.y);
+        lw[5 * l + 4] = make_double2(c.z, ln[l].w);
+    }
+    if ((rc = upload(*D, lpk, &d.lt_pk))) return rc;
+    if ((rc = upload(*D, ld, &d.lt_d))) return rc;
+    if ((rc = upload(*D, lw, &d.lt_w))) return rc;
     if ((rc = upload(*D, sc->bvh.nodes, &d.bvh))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
     if ((rc = upload(*D, sc->lbvh.nodes, &d.lbvh))) return rc;
@@ -1001,7 +1167,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = list_ok ? 3 : 0;  // A/B on MI355X: tools/prep_variants.py
+    if (variant < 0) variant = list_ok ? 6 : 0;  // A/B on MI355X: tools/prep_variants.py
     if (variant > 0 && !list_ok) variant = 0;
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
@@ -1020,6 +1186,14 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
         case 3: MCPT_PREP_LIST(false, 5); break;
         case 4: MCPT_PREP_LIST(false, 6); break;
         case 5: MCPT_PREP_LIST(true, 5); break;
+        case 6:
+            hipLaunchKernelGGL((k_prep_pk<5>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
+                               qnode, u, wsum, pick, count, stats, nchunks, wb, work);
+            break;
+        case 7:
+            hipLaunchKernelGGL((k_prep_pk<4>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
+                               qnode, u, wsum, pick, count, stats, nchunks, wb, work);
+            break;
         default: MCPT_PREP_LIST(false, 1); break;
     }
 #undef MCPT_PREP_LIST
