@@ -213,6 +213,14 @@ __device__ inline double fdot(d3 a, d3 b) { return fma(a.x, b.x, fma(a.y, b.y, a
 __device__ inline d3 fcross(d3 a, d3 b) {
     return d3{fma(a.y, b.z, -a.z * b.y), fma(a.z, b.x, -a.x * b.z), fma(a.x, b.y, -a.y * b.x)};
 }
+// a * b + c with a wave-uniform c taken from SGPRs: one v_fma_f64 (the compiler otherwise keeps
+// fp64 constants in VGPRs and copies each into a v_fmac accumulator first)
+__device__ inline double fma_s(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+
 // a / |a| by the hardware rsqrt estimate plus one third-order Newton step (the refinement ocml's
 // rsqrt uses, without its zero/inf class fix-ups: a zero vector gives NaN either way, which every
 // caller culls)
@@ -220,7 +228,9 @@ __device__ inline d3 funit(d3 a) {
     const double s = fdot(a, a);
     const double y = __builtin_amdgcn_rsq(s);
     const double e = fma(-s * y, y, 1.0);  // 1 - s y^2
-    const double r = fma(y * e, fma(e, 0.375, 0.5), y);
+    double h;  // e * 0.375 + 0.5, the 0.375 from an SGPR (see fma_s)
+    asm("v_fma_f64 %0, %1, %2, 0.5" : "=v"(h) : "v"(e), "s"(0.375));
+    const double r = fma(y * e, h, y);
     return d3{a.x * r, a.y * r, a.z * r};
 }
 // num / den for den > 0 (finite): hardware reciprocal estimate plus one third-order step
@@ -240,20 +250,22 @@ __device__ inline double atan2_pos(double y, double x) {
     constexpr double k = 0.41421356237309503;  // tan(pi/8)
     const double ax = fabs(x);
     const bool A = y <= k * ax, D = !A && ax <= k * y;
-    const double num = A ? y : (D ? -ax : y - ax);
-    const double den = A ? ax : (D ? y : y + ax);
-    const double r0 = A ? 0.0 : (D ? 1.5707963267948966 : 0.7853981633974483);
+    // (num, den, r0) = A: (y, ax, 0); D: (-ax, y, pi/2); else (y - ax, y + ax, pi/4), as
+    // num = p y - q ax, den = q y + p ax, r0 = q (pi/2 - p pi/4) with p, q in {0, 1} (exact)
+    const double pc = D ? 0.0 : 1.0, qc = A ? 0.0 : 1.0;
+    const double num = fma(pc, y, -(qc * ax));
+    const double den = fma(qc, y, pc * ax);
+    const double r0 = qc * fma(-pc, 0.7853981633974483, 1.5707963267948966);
     const double z = fdiv_pos(num, den), s = z * z;
-    double p = 0.023022964535612277;
-    p = fma(p, s, -0.045054138438556275);
-    p = fma(p, s, 0.05743860627393907);
-    p = fma(p, s, -0.0665101622857059);
-    p = fma(p, s, 0.07691210259772996);
-    p = fma(p, s, -0.09090862908839843);
-    p = fma(p, s, 0.11111110041613353);
-    p = fma(p, s, -0.14285714274661848);
-    p = fma(p, s, 0.19999999999980458);
-    p = fma(p, s, -0.33333333333333476);
+    double p = fma_s(0.023022964535612277, s, -0.045054138438556275);
+    p = fma_s(p, s, 0.05743860627393907);
+    p = fma_s(p, s, -0.0665101622857059);
+    p = fma_s(p, s, 0.07691210259772996);
+    p = fma_s(p, s, -0.09090862908839843);
+    p = fma_s(p, s, 0.11111110041613353);
+    p = fma_s(p, s, -0.14285714274661848);
+    p = fma_s(p, s, 0.19999999999980458);
+    p = fma_s(p, s, -0.33333333333333476);
     const double a = r0 + fma(z * s, p, z);
     return x < 0 ? 3.141592653589793 - a : a;
 }

@@ -335,12 +335,20 @@ __device__ inline double dpp_shift(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), kCtrl, kRowMask, 0xf, false);
     return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
 }
+// row_shr with bound_ctrl: every lane is written (source or 0), so no `old` register is needed
+template <int kCtrl>
+__device__ inline double dpp_shr(double v) {
+    const unsigned long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, kCtrl, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), kCtrl, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
 __device__ inline double wave_incl_scan(double v, int lane) {
     (void)lane;
-    v += dpp_shift<0x111, 0xf>(v);  // row_shr:1
-    v += dpp_shift<0x112, 0xf>(v);  // row_shr:2
-    v += dpp_shift<0x114, 0xf>(v);  // row_shr:4
-    v += dpp_shift<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_shr<0x111>(v);  // row_shr:1
+    v += dpp_shr<0x112>(v);  // row_shr:2
+    v += dpp_shr<0x114>(v);  // row_shr:4
+    v += dpp_shr<0x118>(v);  // row_shr:8
     v += dpp_shift<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
     v += dpp_shift<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
     return v;
