@@ -34,7 +34,8 @@ enum {
     MCPT_E_OVERFLOW = -5, /* wavefront queue overflow (raise mcpt_render_opts.queue_factor) */
 };
 
-enum { MCPT_MODE_MIS = 0, MCPT_MODE_BRDF = 1 }; /* shade_with_mis main.cpp:402 / shade_with_brdf :348 */
+/* shade_with_mis main.cpp:402 / shade_with_brdf :348 / shade :269 (the one main() calls, :575) */
+enum { MCPT_MODE_MIS = 0, MCPT_MODE_BRDF = 1, MCPT_MODE_SHADE = 2 };
 
 typedef struct mcpt_scene mcpt_scene;
 
@@ -65,7 +66,7 @@ typedef struct {
     int32_t spp;            /* samples per pixel of the whole frame (the 1/spp weight) */
     int32_t sample_begin;   /* render global sample indices [sample_begin, sample_end) */
     int32_t sample_end;     /*   (sharding across GPUs/calls; 0,0 = all) */
-    int32_t mode;           /* MCPT_MODE_MIS / MCPT_MODE_BRDF */
+    int32_t mode;           /* MCPT_MODE_MIS / MCPT_MODE_BRDF / MCPT_MODE_SHADE */
     uint64_t seed;          /* counter-RNG seed (reference default 20240430 in bench/tests) */
     int32_t samples_per_launch; /* wavefront batch: spp slices per launch (0 = auto) */
     int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2) */

@@ -16,11 +16,11 @@ import os
 import numpy as np
 
 __all__ = ["Scene", "Camera", "render", "render_device", "closest_hit", "light_prep", "primary_hits",
-           "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "Stats", "MCPTError", "LIB_PATH", "lib"]
+           "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "MODE_SHADE", "Stats", "MCPTError", "LIB_PATH", "lib"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmcpt_hip.so")
-MODE_MIS, MODE_BRDF = 0, 1
+MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2  # shade_with_mis / shade_with_brdf / shade (main.cpp:402/348/269)
 DEFAULT_SEED = 20240430
 
 
@@ -164,9 +164,11 @@ class Scene:
 def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor):
     o = RenderOpts()
     o.spp = int(spp)
-    o.mode = MODE_MIS if mode in ("mis", MODE_MIS) else MODE_BRDF if mode in ("brdf", MODE_BRDF) else -1
+    o.mode = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE}.get(mode, mode) if isinstance(mode, str) else mode
+    if o.mode not in (MODE_MIS, MODE_BRDF, MODE_SHADE):
+        o.mode = -1
     if o.mode < 0:
-        raise ValueError("mode must be 'mis' or 'brdf'")
+        raise ValueError("mode must be 'mis', 'brdf' or 'shade'")
     o.seed = int(seed)
     if sample_range is not None:
         o.sample_begin, o.sample_end = int(sample_range[0]), int(sample_range[1])

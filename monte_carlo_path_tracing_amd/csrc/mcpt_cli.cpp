@@ -5,7 +5,7 @@
 // integrator and output path are flags instead of edits to main.cpp.
 //
 //   mcpt_render --scene scenes/veach-mis/veach-mis [--width 1280 --height 720] [--spp 10]
-//               [--mode mis|brdf] [--seed 20240430] [--out test.bmp] [--hdr out.pfm]
+//               [--mode mis|brdf|shade] [--seed 20240430] [--out test.bmp] [--hdr out.pfm]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -62,7 +62,16 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[a], "--width")) W = std::atoi(next());
         else if (!std::strcmp(argv[a], "--height")) H = std::atoi(next());
         else if (!std::strcmp(argv[a], "--spp")) spp = std::atoi(next());
-        else if (!std::strcmp(argv[a], "--mode")) mode = std::strcmp(next(), "brdf") ? MCPT_MODE_MIS : MCPT_MODE_BRDF;
+        else if (!std::strcmp(argv[a], "--mode")) {
+            const char* m = next();
+            if (!std::strcmp(m, "mis")) mode = MCPT_MODE_MIS;
+            else if (!std::strcmp(m, "brdf")) mode = MCPT_MODE_BRDF;
+            else if (!std::strcmp(m, "shade")) mode = MCPT_MODE_SHADE;
+            else {
+                std::fprintf(stderr, "unknown --mode %s (mis, brdf, shade)\n", m);
+                return 2;
+            }
+        }
         else if (!std::strcmp(argv[a], "--seed")) seed = std::strtoull(next(), nullptr, 10);
         else if (!std::strcmp(argv[a], "--out")) out = next();
         else if (!std::strcmp(argv[a], "--hdr")) hdr_out = next();
@@ -101,7 +110,7 @@ int main(int argc, char** argv) {
     }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::printf("%dx%d @ %d spp (%s): %.3f s wall, %.3f s device, %.2f Msamples/s\n", W, H, spp,
-                mode == MCPT_MODE_MIS ? "MIS" : "BRDF", sec, st.seconds, st.camera_samples / st.seconds * 1e-6);
+                mode == MCPT_MODE_MIS ? "MIS" : mode == MCPT_MODE_BRDF ? "BRDF" : "shade", sec, st.seconds, st.camera_samples / st.seconds * 1e-6);
     std::vector<uint8_t> rgb8(hdr.size());
     mcpt_tone_map(hdr.data(), W, H, 380.0, 0.25, rgb8.data());  // main.cpp:583
     if (mcpt_write_bmp(out.c_str(), rgb8.data(), W, H) != MCPT_OK) {

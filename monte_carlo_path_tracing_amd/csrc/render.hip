@@ -229,6 +229,7 @@ __device__ inline void node_entry(const Params& P, bool active, int f, double be
     d3 p, N;
     bool push = false;
     if (active) {
+        // MIS: heap ids (root 1, children 2n, 2n+1); BRDF / shade: paths (node = depth + 1)
         const bool too_deep = P.mode == MCPT_MODE_MIS ? node >= (2ull << MCPT_MAX_DEPTH) : node > MCPT_MAX_DEPTH + 1;
         if (!too_deep) {
             const float4* v = S.tri_v + 3 * f;
@@ -244,6 +245,8 @@ __device__ inline void node_entry(const Params& P, bool active, int f, double be
                     unsafeAtomicAdd(px + 0, tp.x * S.light_rad[3 * li + 0] * P.inv_spp);
                     unsafeAtomicAdd(px + 1, tp.y * S.light_rad[3 * li + 1] * P.inv_spp);
                     unsafeAtomicAdd(px + 2, tp.z * S.light_rad[3 * li + 2] * P.inv_spp);
+                } else if (P.mode == MCPT_MODE_SHADE) {
+                    push = true;  // shade() samples direct light before its RR draw (main.cpp:295-327)
                 } else {
                     const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
                     push = !(counter_u(key, 0) > MCPT_P_RR);
@@ -926,6 +929,87 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur,
     }
 }
 
+// one shade() node (main.cpp:295-343), lane per node: the direct-light estimate is splatted into
+// the framebuffer here; RR, then at most one child (a Phong-sampled bounce that hits a non-emitter,
+// main.cpp:335) through node_entry.  The light point comes from the prep kernel's pick -- the
+// non-staged sampler select_a_point_from_lights_spherical_triangle (Mylight.cpp:163-318) has the
+// same culls, weights and pick as the staged pair used by MIS.
+__global__ __launch_bounds__(kTraceBlock) void k_extend_shade(Params P, Queue cur, int n, Queue nxt) {
+    __shared__ int stack[kStack * kTraceBlock];
+    int* st = stack + threadIdx.x;
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    const int ii = active ? i : 0;
+    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
+    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
+    const d3 wo = mk3(cur.wo[3 * ii], cur.wo[3 * ii + 1], cur.wo[3 * ii + 2]);
+    const d3 tp = mk3(cur.tp[3 * ii], cur.tp[3 * ii + 1], cur.tp[3 * ii + 2]);
+    const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
+    const uint64_t node = cur.node[ii];
+    const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
+    const float* m = S.mtl + 7 * S.tri_mat[f];
+    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
+    const double sh = m[6];
+    const double wsum = cur.wsum[ii];
+    const int pick = cur.pick[ii];
+    bool c = false;
+    Hit h{-1, 0, 0, 0};
+    d3 wi = mk3(0, 0, 0), tpc = mk3(0, 0, 0);
+    unsigned nrays = 0;
+    if (active) {
+        // ---- direct light (main.cpp:295-316) ----
+        d3 coord, n1 = N;
+        double lprob = 1;
+        if (pick >= 0) {
+            const double4 ln = S.lt_n[pick];
+            SphTri sph;
+            light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph,
+                       true);
+            const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
+            TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
+            coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:311-317)
+            lprob = S.light_sum[pick] / wsum;
+            n1 = mk3(ln.x, ln.y, ln.z);
+        } else {
+            // empty set: the dummy point x1 - n (Mylight.cpp:263-266); wl = -N fails wl.N > 0, so the
+            // dummy facet's normal is never read
+            coord = add(mul(N, -1), p);
+        }
+        const d3 wl = normalized(sub(coord, p));
+        if (dot(wl, N) > 0 && dot(mul(wl, -1), n1) > 0) {
+            nrays++;
+            const Hit hs = trace(S.bvh, S.leaf_v, p, wl, f, st, kTraceBlock);
+            if (pick >= 0 && hs.f >= 0 && hs.f == S.light_facet[pick]) {
+                const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
+                const d3 d = sub(coord, p);
+                const d3 I = mk3(S.light_rad[3 * pick], S.light_rad[3 * pick + 1], S.light_rad[3 * pick + 2]);
+                const d3 Ld = mul(hmul(I, b), dot(wl, N) * dot(mul(wl, -1), n1) / dot(d, d) / lprob);
+                double* px = P.fb + 3 * (size_t)pixel;
+                unsafeAtomicAdd(px + 0, tp.x * Ld.x * P.inv_spp);
+                unsafeAtomicAdd(px + 1, tp.y * Ld.y * P.inv_spp);
+                unsafeAtomicAdd(px + 2, tp.z * Ld.z * P.inv_spp);
+            }
+        }
+        // ---- indirect (main.cpp:318-343) ----
+        if (!(counter_u(key, 0) > MCPT_P_RR)) {
+            double pdf;
+            wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+            if (!(dot(wi, N) < 0)) {
+                nrays++;
+                h = trace(S.bvh, S.leaf_v, p, wi, f, st, kTraceBlock);
+                if (h.f >= 0 && S.tri_light[h.f] < 0) {
+                    const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
+                    tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
+                    c = true;
+                }
+            }
+        }
+    }
+    node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
+    if (active) atomicAdd(P.stats + 2, (unsigned long long)nrays);
+}
+
 // one BRDF-only path vertex (main.cpp:385-396)
 __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
     __shared__ int stack[kStack * kTraceBlock];
@@ -1215,7 +1299,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int W = cam->width, H = cam->height, npx = W * H;
     const int s0 = (o->sample_begin == 0 && o->sample_end == 0) ? 0 : o->sample_begin;
     const int s1 = (o->sample_begin == 0 && o->sample_end == 0) ? o->spp : o->sample_end;
-    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF)) {
+    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF && o->mode != MCPT_MODE_SHADE)) {
         set_error("invalid render options (spp %d, range [%d,%d), mode %d)", o->spp, s0, s1, o->mode);
         return MCPT_E_INVALID;
     }
@@ -1277,7 +1361,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             if (n == 0) break;
             gens++;
             nodes_total += (uint64_t)n;
-            if (o->mode == MCPT_MODE_MIS) {
+            const bool prep = o->mode != MCPT_MODE_BRDF;
+            if (prep) {
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, n, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
                                    cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
@@ -1288,11 +1373,14 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             if (o->mode == MCPT_MODE_MIS)
                 hipLaunchKernelGGL(k_extend_mis, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, P,
                                    *cur, n, *nxt);
+            else if (o->mode == MCPT_MODE_SHADE)
+                hipLaunchKernelGGL(k_extend_shade, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
+                                   P, *cur, n, *nxt);
             else
                 hipLaunchKernelGGL(k_extend_brdf, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
                                    P, *cur, n, *nxt);
             HIP_OK(hipGetLastError());
-            if (o->mode == MCPT_MODE_MIS) {
+            if (prep) {
                 float ms = 0;
                 HIP_OK(hipEventSynchronize(D.evp1));
                 HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
@@ -1316,7 +1404,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->generations = gens;
         stats->shading_nodes = nodes_total;
 
-        stats->light_evals_total = (uint64_t)nodes_total * (o->mode == MCPT_MODE_MIS ? (uint64_t)D.d.NL : 0ull);
+        stats->light_evals_total = (uint64_t)nodes_total * (o->mode != MCPT_MODE_BRDF ? (uint64_t)D.d.NL : 0ull);
         stats->light_evals_culled_backface = hs[6];
         stats->light_evals_candidates = hs[5];
         stats->light_evals_culled_plane = stats->light_evals_total - hs[5] - hs[6];

@@ -1231,6 +1231,102 @@ static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t no
     return vadd(L_light, L_brdf);
 }
 
+/* shade() (main.cpp:269-344): emission at the hit itself; direct light from one point chosen by the
+ * non-staged spherical-triangle sampler select_a_point_from_lights_spherical_triangle
+ * (Mylight.cpp:163-318 -- the same cull chain, weights, pick and Arvo sample as the staged pair),
+ * weighted as an AREA estimate I f cos cos' / r^2 / prob with the solid-angle prob = sum L / sum w
+ * (the reference's bias, kept); then RR and one Phong-sampled bounce that recurses only when it
+ * hits a non-emitter (main.cpp:335).  RefRng order: light pick + xi1 + xi2 (one engine, skipped when
+ * the set is empty), RR (one engine), sample_from_phong (one engine). */
+static v3 shade_direct(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t node) {
+    const orc_scene* s = C->s;
+    if (C->rng == ORC_RNG_COUNTER && node > COUNTER_MAX_DEPTH + 1) return mk(0, 0, 0); /* path: node = depth+1 */
+    C->stats[0]++;
+    double a0 = 1.0 - beta - gamma;
+    v3 p = vadd(vadd(vmul(fvert(s, f, 0), a0), vmul(fvert(s, f, 1), beta)), vmul(fvert(s, f, 2), gamma));
+    v3 N = vnormalized(vadd(vadd(vmul(fnorm(s, f, 0), a0), vmul(fnorm(s, f, 1), beta)), vmul(fnorm(s, f, 2), gamma)));
+    if (vdot(N, wo) < 0) return mk(0, 0, 0);                 /* main.cpp:276-280 */
+    int lf0 = s->light_of[f];
+    if (lf0 >= 0) return ld3(s->lrad + 3 * lf0);             /* main.cpp:284-289 */
+    const material* m = &s->mtl[s->mat[f]];
+    v3 kd = mk(m->kd[0], m->kd[1], m->kd[2]), ks = mk(m->ks[0], m->ks[1], m->ks[2]);
+    double sh = m->ns;
+    uint64_t key = C->rng == ORC_RNG_COUNTER ? counter_key(C->seed, C->pixel, C->sample, node) : 0;
+
+    /* direct light (main.cpp:295-316) */
+    v3 L_dir = mk(0, 0, 0);
+    C->stats[1]++;
+    light_prep(s, p, N, &C->L);
+    v3 coord, I = mk(0, 0, 0);
+    double lprob = 1;
+    int lfacet = 0;  /* sampledLightPoint(0, 0, ...) of the empty set (Mylight.cpp:263-266): facet (0,0) */
+    if (C->L.count == 0 || fabs(C->L.wsum) < EPS) {
+        coord = vadd(vmul(N, -1), p);
+    } else {
+        double k1, k2;
+        int rind;
+        if (C->rng == ORC_RNG_REF) {
+            minstd e = ref_engine(&C->ctr);
+            rind = C->L.count >= 2 ? ref_pick(&C->L, canon(&e)) : 0;
+            k1 = canon(&e);
+            k2 = canon(&e);
+        } else {
+            rind = counter_pick(&C->L, counter_u(key, 1));
+            k1 = counter_u(key, 2);
+            k2 = counter_u(key, 3);
+        }
+        int li = light_sample_after_pick(s, &C->L, rind, p, k1, k2, &coord, &lprob);
+        lfacet = s->lfacet[li];
+        I = ld3(s->lrad + 3 * li);
+    }
+    v3 n1 = ld3(s->un + 3 * lfacet);
+    v3 wl = vnormalized(vsub(coord, p));
+    if (vdot(wl, N) > 0 && vdot(vmul(wl, -1), n1) > 0) {
+        hitrec h;
+        C->stats[2]++;
+        int g = grid_trace(s, p, wl, f, 0, &h);
+        if (g >= 0 && g == lfacet) {
+            v3 brdf = brdf_phong(N, wl, wo, kd, ks, sh);
+            v3 d = vsub(coord, p);
+            L_dir = vmul(rgb_mul(I, brdf), vdot(wl, N) * vdot(vmul(wl, -1), n1) / vdot(d, d) / lprob);
+        }
+    }
+    /* indirect (main.cpp:318-343) */
+    double ksi;
+    if (C->rng == ORC_RNG_REF) {
+        minstd e = ref_engine(&C->ctr);
+        ksi = canon(&e);
+    } else {
+        ksi = counter_u(key, 0);
+    }
+    if (ksi > P_RR) return L_dir;
+    double u0, u1, u2, pdf;
+    if (C->rng == ORC_RNG_REF) {
+        minstd e = ref_engine(&C->ctr);
+        u0 = canon(&e); u1 = canon(&e); u2 = canon(&e);
+    } else {
+        u0 = counter_u(key, 4); u1 = counter_u(key, 5); u2 = counter_u(key, 6);
+    }
+    v3 wi = sample_phong(N, wo, kd, ks, sh, u0, u1, u2, &pdf);
+    if (vdot(wi, N) < 0) return L_dir;
+    hitrec h;
+    C->stats[2]++;
+    int g = grid_trace(s, p, wi, f, 0, &h);
+    v3 L_indir = mk(0, 0, 0);
+    if (g >= 0 && s->light_of[g] < 0) {
+        v3 brdf = brdf_phong(N, wi, wo, kd, ks, sh);
+        v3 Li = shade_direct(C, g, h.beta, h.gamma, vmul(wi, -1), node + 1);
+        L_indir = vmul(rgb_mul(Li, brdf), vdot(wi, N) / pdf / P_RR);
+    }
+    return vadd(L_dir, L_indir);
+}
+
+static v3 shade_root(ctx* C, int mode, int f, double beta, double gamma, v3 wo) {
+    if (mode == ORC_MODE_MIS) return shade_mis(C, f, beta, gamma, wo, 1);
+    if (mode == ORC_MODE_SHADE) return shade_direct(C, f, beta, gamma, wo, 1);
+    return shade_brdf(C, f, beta, gamma, wo, 1);
+}
+
 static void ctx_init(ctx* C, const orc_scene* s, int rng) {
     memset(C, 0, sizeof *C);
     C->s = s;
@@ -1251,10 +1347,7 @@ void orc_shade_sample(const orc_scene* s, const orc_camera* cam, int mode, int r
     hitrec h;
     int f = grid_trace(s, fr.eye, dir, -1, 0, &h);
     v3 L = mk(0, 0, 0);
-    if (f >= 0) {
-        if (mode == ORC_MODE_MIS) L = shade_mis(&C, f, h.beta, h.gamma, vmul(dir, -1), 1);
-        else L = shade_brdf(&C, f, h.beta, h.gamma, vmul(dir, -1), 1);
-    }
+    if (f >= 0) L = shade_root(&C, mode, f, h.beta, h.gamma, vmul(dir, -1));
     st3(rgb, L);
     if (draws) *draws = C.ctr - ctr_or_seed;
     ls_free(&C.L);
@@ -1294,8 +1387,7 @@ int orc_render(const orc_scene* s, const orc_camera* cam, int mode, uint64_t see
                 C.pixel = (uint64_t)i * W + j;
                 for (int k = s0; k < s1; k++) {
                     C.sample = (uint64_t)k;
-                    v3 L = mode == ORC_MODE_MIS ? shade_mis(&C, f, h.beta, h.gamma, vmul(dir, -1), 1)
-                                                : shade_brdf(&C, f, h.beta, h.gamma, vmul(dir, -1), 1);
+                    v3 L = shade_root(&C, mode, f, h.beta, h.gamma, vmul(dir, -1));
                     sum = vadd(sum, vmul(L, inv));  /* main.cpp:575-576 */
                 }
             }

@@ -4,7 +4,8 @@
  * (luotong96/Monte_Carlo_Path_Tracing): OBJ/MTL/XML loading (Myobj.cpp:10-28, Mylight.cpp:11-100,
  * the vendored tinyobjloader number parser tiny_obj_loader.h:897-1028), the uniform grid + 3D-DDA
  * closest hit (Myobj.cpp:78-162,334-622), staged spherical-triangle light sampling
- * (Mylight.cpp:322-493), the Phong BRDF (BRDF.cpp:17-133), the two integrators (main.cpp:348-494)
+ * (Mylight.cpp:322-493) and its non-staged form (:163-318), the Phong BRDF (BRDF.cpp:17-133), the
+ * three integrators (shade main.cpp:269-344, shade_with_brdf :348-399, shade_with_mis :402-494)
  * and the camera/frame loop (main.cpp:507-588).  All arithmetic is fp64 in the reference's
  * evaluation order, built with -ffp-contract=off.
  *
@@ -24,7 +25,7 @@ extern "C" {
 
 typedef struct orc_scene orc_scene;
 
-enum { ORC_MODE_MIS = 0, ORC_MODE_BRDF = 1 };
+enum { ORC_MODE_MIS = 0, ORC_MODE_BRDF = 1, ORC_MODE_SHADE = 2 }; /* main.cpp:402 / :348 / :269 */
 enum { ORC_RNG_REF = 0, ORC_RNG_COUNTER = 1 };
 
 /* camera: eye, lookat, up, fovy parameter (the reference's tan(fovy/360) quirk), eye pull-back

@@ -4,8 +4,8 @@
 // units where they lie under /root/reference (vec, matrix3d, BRDF, RadianceRGB, Myobj, Mylight,
 // pugixml), with oracle/fakeclock.h force-included so the clock-seeded RNG is replayable.
 // main.cpp is NOT compiled: it includes the Windows-only EasyX <graphics.h> (main.cpp:13), which
-// this image lacks, so it is unbuildable here.  The two integrators of main.cpp (shade_with_brdf
-// main.cpp:348-399, shade_with_mis main.cpp:402-494) and the camera of main.cpp:547-564 are
+// this image lacks, so it is unbuildable here.  The three integrators of main.cpp (shade
+// main.cpp:269-344, shade_with_brdf :348-399, shade_with_mis :402-494) and the camera of main.cpp:547-564 are
 // therefore restated below in a few lines each, calling the REAL reference components for
 // everything else (grid traversal, light prep/sampling, BRDF, RNG sites).  Outputs go to
 // tests/golden/*.npy and pin oracle/mcpt_oracle.c (tests/test_oracle_golden.py).
@@ -139,6 +139,39 @@ static RadianceRGB ref_shade_mis(intersec_result point, vec wo) {
         L_brdf = ref_shade_mis(r2, wi.dir * -1) * brdf * (wi.dir.dot_product(N) / (wi.pdf + light_pdf) / 0.6);
     }
     return L_light + L_brdf;
+}
+
+// Restatement of main.cpp:269-344 (shade, the integrator main() ships with, main.cpp:575); direct
+// light through the reference's select_a_point_from_lights_spherical_triangle (Mylight.cpp:163).
+static RadianceRGB ref_shade(intersec_result point, vec wo) {
+    vec p = interp(veach->get_vertexes_of_facet(point.s, point.f), point.beta, point.gamma);
+    vec N = interp(veach->get_normals_of_facet(point.s, point.f), point.beta, point.gamma).normalized();
+    if (N.dot_product(wo) < 0) return RadianceRGB(0, 0, 0);
+    auto li = lights->islight.find(triangle(point.s, point.f));
+    if (li != lights->islight.end()) return li->second;
+    tinyobj::material_t mtl = mat_of(point.s, point.f);
+    RadianceRGB L_dir;
+    sampledLightPoint lp = lights->select_a_point_from_lights_spherical_triangle(p, N, *veach);
+    vec x1 = lp.coord;
+    vec n1 = veach->get_unique_normal_of_facet(lp.s, lp.f);
+    vec wl = (x1 - p).normalized();
+    if (wl.dot_product(N) > 0 && (wl * -1).dot_product(n1) > 0) {
+        intersec_result r1 = veach->closet_ray_intersect(p, wl, triangle(point.s, point.f));
+        if (r1.isIntersec && r1.s == lp.s && r1.f == lp.f) {
+            BRDF brdf = BRDF::get_brdf_phong(N, wl, wo, kd_of(mtl), ks_of(mtl), mtl.shininess);
+            L_dir = lp.I * brdf * (wl.dot_product(N) * (wl * -1).dot_product(n1) / (x1 - p).dot_product(x1 - p) / lp.prob);
+        }
+    }
+    RadianceRGB L_indir;
+    if (rr_uniform() > 0.6) return L_dir + L_indir;
+    sampledRay wi = BRDF::sample_from_phong(N, wo, kd_of(mtl), ks_of(mtl), mtl.shininess);
+    if (wi.dir.dot_product(N) < 0) return L_dir + L_indir;
+    intersec_result r2 = veach->closet_ray_intersect(p, wi.dir, triangle(point.s, point.f));
+    if (r2.isIntersec && lights->islight.find(triangle(r2.s, r2.f)) == lights->islight.end()) {
+        BRDF brdf = BRDF::get_brdf_phong(N, wi.dir, wo, kd_of(mtl), ks_of(mtl), mtl.shininess);
+        L_indir = ref_shade(r2, wi.dir * -1) * brdf * (wi.dir.dot_product(N) / wi.pdf / 0.6);
+    }
+    return L_dir + L_indir;
 }
 
 // Camera of main.cpp:507-510,547-564 generalised to W x H.
@@ -422,9 +455,9 @@ int main(int argc, char** argv) {
     }
 
     // ---- G7 per-sample radiance, both integrators, RefRng replay keys -----------------------
-    for (int mode = 0; mode < 2; mode++) {
+    for (int mode = 0; mode < 3; mode++) {  // 0 shade_with_mis, 1 shade_with_brdf, 2 shade
         std::vector<double> o;
-        const int NS = mode == 0 ? 3000 : 6000;  // MIS is ~100x more expensive
+        const int NS = mode == 1 ? 6000 : 3000;  // MIS / shade run a light prep per node
         for (int r = 0; r < NS; r++) {
             int i = (int)(U(rng) * cam0.H), j = (int)(U(rng) * cam0.W);
             vec dir = cam_dir(cam0, i, j);
@@ -432,14 +465,15 @@ int main(int argc, char** argv) {
             u64 c0 = 1ull + 100000007ull * (u64)r;
             clk() = c0;
             RadianceRGB L(0, 0, 0);
-            if (rs.isIntersec) L = mode == 0 ? ref_shade_mis(rs, dir * -1) : ref_shade_brdf(rs, dir * -1);
+            if (rs.isIntersec)
+                L = mode == 0 ? ref_shade_mis(rs, dir * -1) : mode == 1 ? ref_shade_brdf(rs, dir * -1) : ref_shade(rs, dir * -1);
             o.push_back(i);
             o.push_back(j);
             o.push_back((double)c0);
             o.push_back((double)(clk() - c0));
             for (int c = 0; c < 3; c++) o.push_back(L.RGB[c]);
         }
-        npy_f64(out + (mode == 0 ? "/sample_mis.npy" : "/sample_brdf.npy"), o, 7);
+        npy_f64(out + (mode == 0 ? "/sample_mis.npy" : mode == 1 ? "/sample_brdf.npy" : "/sample_shade.npy"), o, 7);
     }
     printf("golden vectors written to %s (F=%zu)\n", out.c_str(), F);
     return 0;

@@ -120,16 +120,19 @@ def test_light_prep_vs_reference_and_oracle(scene, oscene):
     assert mism <= 2, mism
 
 
+OMODE = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF, "shade": po.MODE_SHADE}
+
+
 def _render_pair(scene, oscene, W, H, spp, mode, stride=1, nthreads=8):
     cam = mcpt.Camera.reference(W, H)
     g, st = mcpt.render(scene, cam, spp, mode=mode, seed=SEED)
     ocam = po.reference_camera(W, H)
-    c, _ = oscene.render(ocam, po.MODE_MIS if mode == "mis" else po.MODE_BRDF, SEED, spp, stride=stride,
+    c, _ = oscene.render(ocam, OMODE[mode], SEED, spp, stride=stride,
                          nthreads=nthreads)
     return g, c, st
 
 
-@pytest.mark.parametrize("mode,spp", [("mis", 8), ("brdf", 32)])
+@pytest.mark.parametrize("mode,spp", [("mis", 8), ("brdf", 32), ("shade", 8)])
 def test_render_parity_small(scene, oscene, mode, spp):
     g, c, st = _render_pair(scene, oscene, 80, 60, spp, mode)
     err = rel_l2(g, c)
@@ -138,13 +141,13 @@ def test_render_parity_small(scene, oscene, mode, spp):
     assert err <= L2_TOL
 
 
-@pytest.mark.parametrize("mode,spp", [("mis", 16), ("brdf", 64)])
+@pytest.mark.parametrize("mode,spp", [("mis", 16), ("brdf", 64), ("shade", 16)])
 def test_render_parity_full_size_pixel_subset(scene, oscene, mode, spp):
     """BASELINE size 800x600: the counter RNG is keyed per pixel, so the oracle renders every 20th
     pixel in x and y (SURVEY.md §8(d) stratified subset) and those pixels must match."""
     cam = mcpt.Camera.reference(800, 600)
     g, st = mcpt.render(scene, cam, spp, mode=mode, seed=SEED)
-    c, _ = oscene.render(po.reference_camera(800, 600), po.MODE_MIS if mode == "mis" else po.MODE_BRDF, SEED, spp,
+    c, _ = oscene.render(po.reference_camera(800, 600), OMODE[mode], SEED, spp,
                          stride=20, offset=7, nthreads=8)
     sub = (slice(7, None, 20), slice(7, None, 20))
     err = rel_l2(g[sub], c[sub])

@@ -107,9 +107,10 @@ def test_tone_mapping():
         assert np.array_equal(po.tone_map(tin[r]), tout[r].astype(np.int32)), r
 
 
-@pytest.mark.parametrize("mode,name", [(po.MODE_MIS, "sample_mis.npy"), (po.MODE_BRDF, "sample_brdf.npy")])
+@pytest.mark.parametrize("mode,name", [(po.MODE_MIS, "sample_mis.npy"), (po.MODE_BRDF, "sample_brdf.npy"),
+                                       (po.MODE_SHADE, "sample_shade.npy")])
 def test_integrator_refrng_replay_bitexact(scene, mode, name):
-    """RefRng replay of main.cpp:348-494 (DFS order, stale-pdf quirk) vs the reference components."""
+    """RefRng replay of main.cpp:269-494 (DFS order, stale-pdf quirk) vs the reference components."""
     cam = po.reference_camera(400, 300)
     gs = g(name)
     for r in range(gs.shape[0]):
