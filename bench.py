@@ -37,22 +37,47 @@ FLOPS_FULL = 269
 # RNG key; writes weights_sum + pick (12 B).  The light table (240 KB) is L2/MALL resident.
 PREP_BYTES_PER_NODE = 76
 SCENE = os.path.join(ROOT, "scenes", "veach-mis")
+SCENES = {  # --scene: (metric, data note)
+    "veach": (METRIC, "synthetic: Veach-MIS stand-in scene (scenes/gen_veach_mis.py; the reference's scene files are missing)"),
+    "cornell1m": ("Msamples/sec (whole node) + per-pixel L2 vs CPU, Cornell + 1M random triangles 800×600@1024spp",
+                  "synthetic: Cornell + 1,000,000 random triangles stand-in (scenes/gen_cornell_random.py, "
+                  "SURVEY.md §8(d) C5; generated at start-up)"),
+}
+
+
+def scene_files(name):
+    """(obj, xml, camera-from-XML?) of a --scene"""
+    if name == "veach":
+        return SCENE + "/veach-mis.obj", SCENE + "/veach-mis.xml", False
+    import subprocess
+    import tempfile
+    d = os.path.join(tempfile.gettempdir(), "mcpt_cornell_1000000_20240430")
+    obj, xml = d + "/cornell-random.obj", d + "/cornell-random.xml"
+    if not (os.path.exists(obj) and os.path.exists(xml)):
+        subprocess.run([sys.executable, os.path.join(ROOT, "scenes", "gen_cornell_random.py"), "--triangles",
+                        "1000000", "--seed", "20240430", d], check=True, capture_output=True)
+    return obj, xml, True
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(W, H, mode, seed, target_s):
+def cpu_baseline(scene_name, W, H, mode, seed, target_s):
     """The C oracle (oracle/liboracle.so), 1 thread, every 20th pixel in x and y, at an spp chosen
     so that the run takes about target_s seconds.  Returns (dict, subset image, spp)."""
     from oracle import pyoracle as po
 
-    osc = po.Scene(SCENE + "/veach-mis.obj", SCENE + "/veach-mis.xml")
-    ocam = po.reference_camera(W, H)
+    obj, xml, xml_cam = scene_files(scene_name)
+    osc = po.Scene(obj, xml)
+    if xml_cam:
+        ocam = osc.camera()
+        ocam.width, ocam.height = W, H
+    else:
+        ocam = po.reference_camera(W, H)
     e, _ = po.camera_ray(ocam, 0, 0)
     osc.build_grid(e)
-    m = po.MODE_MIS if mode == "mis" else po.MODE_BRDF
+    m = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF, "shade": po.MODE_SHADE}[mode]
     t = time.perf_counter()
     osc.render(ocam, m, seed, 1, stride=20, offset=7, nthreads=1)
     t1 = time.perf_counter() - t
@@ -75,7 +100,9 @@ def main():
     ap.add_argument("--spp-per-step", type=int, default=8)
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=600)
-    ap.add_argument("--mode", default="mis", choices=["mis", "brdf"])
+    ap.add_argument("--mode", default="mis", choices=["mis", "brdf", "shade"])
+    ap.add_argument("--scene", default="veach", choices=sorted(SCENES),
+                    help="veach: the north-star workload (C3); cornell1m: config C5")
     ap.add_argument("--seed", type=int, default=20240430)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and L2 check")
@@ -101,8 +128,13 @@ def main():
 
     W, H, S = args.width, args.height, args.spp_per_step
     frame_spp = args.steps * world * S
-    scene = mcpt.Scene.load(SCENE + "/veach-mis.obj", SCENE + "/veach-mis.xml")
-    cam = mcpt.Camera.reference(W, H)
+    obj, xml, xml_cam = scene_files(args.scene)
+    scene = mcpt.Scene.load(obj, xml)
+    if xml_cam:  # the XML camera (main.cpp:512-513 for the Cornell scene): no pull-back
+        cam = scene.camera()
+        cam.width, cam.height = W, H
+    else:
+        cam = mcpt.Camera.reference(W, H)
     fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
     scratch = torch.zeros_like(fb)
 
@@ -147,7 +179,7 @@ def main():
     cand = totals.get("light_evals_candidates", 0)
     c2 = ev_tot - c1 - cand
     flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
-    if args.mode == "mis" and prep_s > 0:
+    if args.mode != "brdf" and prep_s > 0:
         achieved = flops / launches / (prep_s / launches) / 1e12
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "k_prep_hbm_bytes_per_node.json")
@@ -170,18 +202,19 @@ def main():
     l2 = None
     if world == 1 and not args.no_cpu:
         log("cpu baseline (~%.0f s) ..." % args.cpu_seconds)
-        cpu, cimg, cspp = cpu_baseline(W, H, args.mode, args.seed, args.cpu_seconds)
+        cpu, cimg, cspp = cpu_baseline(args.scene, W, H, args.mode, args.seed, args.cpu_seconds)
         g, _ = mcpt.render(scene, cam, cspp, mode=args.mode, seed=args.seed, device=local)
         sub = (slice(7, None, 20), slice(7, None, 20))
         l2 = float(np.linalg.norm(g[sub] - cimg[sub]) / max(np.linalg.norm(cimg[sub]), 1e-300))
     if args.out:
         mcpt.write_bmp(args.out, mcpt.tone_map(fb.cpu().numpy()))
     line = {
-        "metric": METRIC, "value": round(value, 4), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "metric": SCENES[args.scene][0], "value": round(value, 4), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic: Veach-MIS stand-in scene (scenes/gen_veach_mis.py; the reference's scene files are missing)",
-        "config": {"workload": "veach-mis %s %dx%d" % (args.mode.upper(), W, H), "width": W, "height": H,
+        "data": SCENES[args.scene][1],
+        "config": {"workload": "%s %s %dx%d" % ("veach-mis" if args.scene == "veach" else "cornell-1M", args.mode.upper(), W, H),
+                   "width": W, "height": H,
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
                    "parallelism": "sample-shard x%d + 1 RCCL reduce" % world},
         "roofline": roofline,

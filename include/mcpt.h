@@ -68,7 +68,9 @@ typedef struct {
     int32_t sample_end;     /*   (sharding across GPUs/calls; 0,0 = all) */
     int32_t mode;           /* MCPT_MODE_MIS / MCPT_MODE_BRDF / MCPT_MODE_SHADE */
     uint64_t seed;          /* counter-RNG seed (reference default 20240430 in bench/tests) */
-    int32_t samples_per_launch; /* wavefront batch: spp slices per launch (0 = auto) */
+    int32_t samples_per_launch; /* wavefront working set: the node queue is refilled with camera samples
+                                 * up to samples_per_launch x width x height nodes per generation
+                                 * (0 = auto, 4 Mi nodes) */
     int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2) */
     int32_t device;         /* HIP device ordinal (-1 = current) */
     int32_t reserved;
@@ -128,11 +130,12 @@ int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const doubl
  * -1 if empty or weights_sum < 1e-8). */
 int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                     double* weights_sum, int32_t* count, int32_t* pick);
-/* diagnostics: run the light-prep kernel variant `variant` (-1 auto = 6; 0 LDS candidate queue,
+/* diagnostics: run the light-prep kernel variant `variant` (-1 auto = 8; 0 LDS candidate queue,
  * 1 stored LDS candidate list, 2 list + software prefetch, 3 list at 5 waves/SIMD, 4 list at 6
  * waves/SIMD, 5 list + prefetch at 5 waves/SIMD, 6 packed-fp32 cheap stages + branch-free fp64
- * batches at 5 waves/SIMD, 7 the same at 4 waves/SIMD) `iters` times on the n points and report
- * the mean device time per launch; outputs as mcpt_light_prep (pick = facet). */
+ * batches at 5 waves/SIMD, 7 the same at 4 waves/SIMD, 8 variant 6 with buffer-descriptor loads
+ * and a lane-parallel batch search) `iters` times on the n points and report the mean device time
+ * per launch; outputs as mcpt_light_prep (pick = facet). */
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 /* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */

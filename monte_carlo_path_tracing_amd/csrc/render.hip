@@ -299,7 +299,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 
 // roots: r in [0, nroots): pixel = r % npx, sample = s0 + r / npx
 __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
-                                               int s0, int nroots, Queue q) {
+                                               int s0, long long rbase, int nroots, Queue q) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int npx = cam.W * cam.H;
     bool active = r < nroots;
@@ -307,8 +307,9 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
     double beta = 0, gamma = 0;
     d3 wo = mk3(0, 0, 0);
     if (active) {
-        pixel = r % npx;
-        sample = s0 + r / npx;
+        const long long rg = rbase + r;  // global root index: sample-major over the frame
+        pixel = (int)(rg % npx);
+        sample = s0 + (int)(rg / npx);
         f = hit_f[pixel];
         active = f >= 0;
         if (active) {
@@ -841,6 +842,182 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk(DScene S, uin
     }
 }
 
+// k_prep_pk with (a) light-table loads through buffer descriptors (32-bit offsets, immediate
+// offsets per vertex row, hardware bounds check returning 0 past the table, so no index clamp);
+// (b) v_mbcnt for the list slot; (c) the batch totals searched lane-parallel: lane b holds batch b's
+// total, one wave scan gives every cumulative sum, the target batch is a ballot.  weights_sum is the
+// scan's total (summation order differs from the sequential one only by rounding).
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr int kBufFlags = 0x00020000;  // gfx9 raw buffer descriptor word 3
+__device__ inline float4 u4f(v4u v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ inline double u2d(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ inline double prep_weight_buf(__amdgpu_buffer_rsrc_t rw, int li, d3 x1, bool* ok) {
+    const int o = li * 80;
+    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, 0);
+    const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 16, 0, 0);
+    const v4u c = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 32, 0, 0);
+    const v4u d = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 48, 0, 0);
+    const v4u e = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 64, 0, 0);
+    return light_weight_bf(mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y)),
+                           mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
+                           mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1, ok);
+}
+__device__ inline int lane_rank(uint64_t m) {  // set bits of m below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+template <int kMinWavesPerSimd>
+__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
+                                                  const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                                  const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                                  const double* __restrict__ u_override, double* __restrict__ wsum_out,
+                                                  int* __restrict__ pick_out, int* __restrict__ count_out,
+                                                  unsigned long long* stats, int nchunks, int wave_bytes,
+                                                  unsigned* __restrict__ work) {
+    extern __shared__ double prep_lds[];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
+    unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
+    const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, S.NL * 48, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, S.NL * 4, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_w, 0, S.NL * 80, kBufFlags);
+    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
+    int grab = 0, left = 0;
+    while (true) {
+        if (left == 0) {
+            unsigned b = 0;
+            if (lane == 0) b = atomicAdd(work, (unsigned)kPrepGrab);
+            grab = __shfl((int)b, 0);
+            left = kPrepGrab;
+        }
+        const int node = grab++;
+        left--;
+        if (node >= n) break;
+        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        const NodeF nf = node_f(x1, nn, S.light_bound);
+        const float cn = (float)dot(nn, x1);
+        const v2f nx2{nf.nx, nf.nx}, ny2{nf.ny, nf.ny}, nz2{nf.nz, nf.nz};
+        const v2f nxs{nf.nx, nf.x}, nys{nf.ny, nf.y}, nzs{nf.nz, nf.z};
+        int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
+        for (int c = 0; c < nchunks; c++) {
+            const int li = c * 64 + lane;
+            const float4 X = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, li * 48, 0, 0));
+            const float4 Y = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, li * 48 + 16, 0, 0));
+            const float4 Z = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, li * 48 + 32, 0, 0));
+            const float dl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, li * 4, 0, 0));
+            const int stage = prep_stage_pk(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
+            const uint64_t m = __ballot(stage == 0);
+            if (stage == 0) lst[ncand + lane_rank(m)] = (unsigned short)li;
+            ncand += __popcll(m);
+            culled1 += __popcll(__ballot(stage == 1));
+            while (ncand - 64 * nb >= 64 || (c == nchunks - 1 && ncand > 64 * nb)) {
+                wave_lds_sync();
+                const int k = 64 * nb + lane;
+                const bool act = k < ncand;
+                bool ok;
+                double w = prep_weight_buf(rw, act ? (int)lst[k] : 0, x1, &ok);
+                ok = ok && act;
+                w = act ? w : 0.0;
+                const double sc = wave_incl_scan(w, lane);
+                survivors += __popcll(__ballot(ok));
+                if (lane == 63) bt[nb] = sc;
+                nb++;
+            }
+        }
+        wave_lds_sync();
+        double wsum = 0;
+        int pick = -1;
+        if (nb <= 64) {
+            const double v = lane < nb ? bt[lane] : 0.0;
+            const double cum = wave_incl_scan(v, lane);
+            wsum = __shfl(cum, 63);
+            if (!(fabs(wsum) < MCPT_EPS)) {
+                double u;
+                if (u_override) u = u_override[node];
+                else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+                const double target = u * wsum;
+                const uint64_t hitm = __ballot(cum >= target && v > 0);
+                const uint64_t posm = __ballot(v > 0);
+                const int kb = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63 - __clzll((long long)posm);
+                const double exc = __shfl_up(cum, 1);
+                const double base = kb == 0 ? 0.0 : __shfl(exc, kb);
+                const int k = 64 * kb + lane;
+                const bool act = k < ncand;
+                const int lj = act ? (int)lst[k] : 0;
+                bool ok;
+                double w = prep_weight_buf(rw, lj, x1, &ok);
+                ok = ok && act;
+                w = act ? w : 0.0;
+                const double sc = wave_incl_scan(w, lane);
+                const uint64_t candm = __ballot(ok && (base + sc >= target));
+                const uint64_t okm = __ballot(ok);
+                int pl = -1;
+                if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+                else if (okm) pl = 63 - __clzll((long long)okm);
+                if (pl >= 0) pick = __shfl(lj, pl);
+            }
+        } else {  // more than 64 batches (N_L > 4096 with many candidates): sequential search
+            for (int b = 0; b < nb; b++) wsum += bt[b];
+            if (!(fabs(wsum) < MCPT_EPS)) {
+                double u;
+                if (u_override) u = u_override[node];
+                else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+                const double target = u * wsum;
+                int kb = -1, lastpos = -1;
+                double cum = 0, base = 0;
+                for (int b = 0; b < nb; b++) {
+                    const double nxt = cum + bt[b];
+                    if (bt[b] > 0) lastpos = b;
+                    if (kb < 0 && nxt >= target && bt[b] > 0) {
+                        kb = b;
+                        base = cum;
+                    }
+                    cum = nxt;
+                }
+                if (kb < 0) {
+                    kb = lastpos;
+                    base = 0;
+                    for (int b = 0; b < kb; b++) base += bt[b];
+                }
+                const int k = 64 * kb + lane;
+                const bool act = k < ncand;
+                const int lj = act ? (int)lst[k] : 0;
+                bool ok;
+                double w = prep_weight_buf(rw, lj, x1, &ok);
+                ok = ok && act;
+                w = act ? w : 0.0;
+                const double sc = wave_incl_scan(w, lane);
+                const uint64_t candm = __ballot(ok && (base + sc >= target));
+                const uint64_t okm = __ballot(ok);
+                int pl = -1;
+                if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+                else if (okm) pl = 63 - __clzll((long long)okm);
+                if (pl >= 0) pick = __shfl(lj, pl);
+            }
+        }
+        if (lane == 0) {
+            wsum_out[node] = wsum;
+            pick_out[node] = pick;
+            if (count_out) count_out[node] = survivors;
+        }
+        surv_acc += survivors;
+        cand_acc += ncand;
+        c1_acc += culled1;
+        wave_lds_sync();
+    }
+    if (lane == 0 && stats) {
+        if (surv_acc) atomicAdd(stats + 1, surv_acc);
+        if (cand_acc) atomicAdd(stats + 5, cand_acc);
+        if (c1_acc) atomicAdd(stats + 6, c1_acc);
+    }
+}
+
 // one MIS node (main.cpp:440-493), lane per node; children go through node_entry.
 __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur, int n, Queue nxt) {
     __shared__ int stack[kStack * kTraceBlock];
@@ -1259,7 +1436,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = list_ok ? 6 : 0;  // A/B on MI355X: tools/prep_variants.py
+    if (variant < 0) variant = list_ok ? 8 : 0;  // A/B on MI355X: tools/prep_variants.py
     if (variant > 0 && !list_ok) variant = 0;
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
@@ -1286,6 +1463,10 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
             hipLaunchKernelGGL((k_prep_pk<4>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
                                qnode, u, wsum, pick, count, stats, nchunks, wb, work);
             break;
+        case 8:
+            hipLaunchKernelGGL((k_prep_pk2<5>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
+                               qnode, u, wsum, pick, count, stats, nchunks, wb, work);
+            break;
         default: MCPT_PREP_LIST(false, 1); break;
     }
 #undef MCPT_PREP_LIST
@@ -1303,16 +1484,19 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         set_error("invalid render options (spp %d, range [%d,%d), mode %d)", o->spp, s0, s1, o->mode);
         return MCPT_E_INVALID;
     }
-    int spb = o->samples_per_launch > 0 ? o->samples_per_launch : std::max(1, (2 << 20) / std::max(npx, 1));
-    spb = std::min(spb, std::max(1, s1 - s0));
-    const long long roots_ll = (long long)spb * npx;
-    if (roots_ll > (1ll << 30)) {
+    // Path regeneration (wavefront with refill): before every generation the current queue is
+    // topped up with fresh camera samples (roots) to `target` nodes, so every prep/extend launch
+    // is large until the final drain; roots are taken in global order r = (sample - s0) * npx +
+    // pixel.  samples_per_launch (if set) sets target = samples_per_launch * npx.
+    const long long R = (long long)(s1 - s0) * npx;
+    const long long target_ll = o->samples_per_launch > 0 ? (long long)o->samples_per_launch * npx : (4ll << 20);
+    if (target_ll > (1ll << 29)) {
         set_error("batch too large");
         return MCPT_E_INVALID;
     }
-    const int roots = (int)roots_ll;
+    const int target = (int)std::max<long long>(target_ll, 1);
     const int qf = o->queue_factor > 0 ? o->queue_factor : 2;
-    const int cap = (int)std::min<long long>((long long)qf * roots + 1024, (1ll << 30));
+    const int cap = (int)std::min<long long>((long long)qf * target + 1024, (1ll << 30));
     int rc;
     if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) || (rc = ensure(D.stats, 64)) ||
         (rc = ensure(D.work, 256)))
@@ -1340,54 +1524,65 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     }
     double prep_ms = 0;
     uint64_t gens = 0, prep_launches = 0, nodes_total = 0;
-    for (int sb = s0; sb < s1; sb += spb) {
-        const int nb = std::min(spb, s1 - sb);
-        const int nroots = nb * npx;
-        HIP_OK(hipMemsetAsync(qa.count, 0, 4, st));
-        hipLaunchKernelGGL(k_roots, dim3((nroots + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
-                           (const double*)D.hit_tbg.p, sb, nroots, qa);
-        HIP_OK(hipGetLastError());
-        Queue* cur = &qa;
-        Queue* nxt = &qb;
-        while (true) {
-            HIP_OK(hipMemcpyAsync(D.pinned_count, cur->count, 4, hipMemcpyDeviceToHost, st));
-            HIP_OK(hipMemcpyAsync(D.pinned_count + 2, (char*)D.stats.p + 32, 8, hipMemcpyDeviceToHost, st));
-            HIP_OK(hipStreamSynchronize(st));
-            if (*(unsigned long long*)(D.pinned_count + 2)) {
-                set_error("wavefront queue overflow (capacity %d); raise queue_factor", cap);
-                return MCPT_E_OVERFLOW;
-            }
-            const int n = (int)std::min<unsigned>(D.pinned_count[0], (unsigned)cap);
-            if (n == 0) break;
-            gens++;
-            nodes_total += (uint64_t)n;
-            const bool prep = o->mode != MCPT_MODE_BRDF;
-            if (prep) {
-                HIP_OK(hipEventRecord(D.evp0, st));
-                HIP_OK(launch_prep(-1, D.d, o->seed, n, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
-                HIP_OK(hipEventRecord(D.evp1, st));
-                prep_launches++;
-            }
-            HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
-            if (o->mode == MCPT_MODE_MIS)
-                hipLaunchKernelGGL(k_extend_mis, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, P,
-                                   *cur, n, *nxt);
-            else if (o->mode == MCPT_MODE_SHADE)
-                hipLaunchKernelGGL(k_extend_shade, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
-                                   P, *cur, n, *nxt);
-            else
-                hipLaunchKernelGGL(k_extend_brdf, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
-                                   P, *cur, n, *nxt);
-            HIP_OK(hipGetLastError());
-            if (prep) {
-                float ms = 0;
-                HIP_OK(hipEventSynchronize(D.evp1));
-                HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
-                prep_ms += ms;
-            }
-            std::swap(cur, nxt);
+    Queue* cur = &qa;
+    Queue* nxt = &qb;
+    HIP_OK(hipMemsetAsync(cur->count, 0, 4, st));
+    long long rnext = 0;
+    auto read_count = [&](unsigned* out) -> int {  // cur's node count; fails on a queue overflow
+        HIP_OK(hipMemcpyAsync(D.pinned_count, cur->count, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(D.pinned_count + 2, (char*)D.stats.p + 32, 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (*(unsigned long long*)(D.pinned_count + 2)) {
+            set_error("wavefront queue overflow (capacity %d); raise queue_factor", cap);
+            return MCPT_E_OVERFLOW;
         }
+        *out = std::min<unsigned>(D.pinned_count[0], (unsigned)cap);
+        return MCPT_OK;
+    };
+    while (true) {
+        unsigned n = 0;
+        if ((rc = read_count(&n))) return rc;
+        if (rnext < R && n < (unsigned)target) {  // refill with roots (appended through node_entry)
+            const int m = (int)std::min<long long>((long long)target - n, R - rnext);
+            hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
+                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur);
+            HIP_OK(hipGetLastError());
+            rnext += m;
+            if ((rc = read_count(&n))) return rc;
+        }
+        if (n == 0) {
+            if (rnext >= R) break;
+            continue;  // every root of the refill terminated at entry: refill again
+        }
+        gens++;
+        nodes_total += (uint64_t)n;
+        const int ni = (int)n;
+        const bool prep = o->mode != MCPT_MODE_BRDF;
+        if (prep) {
+            HIP_OK(hipEventRecord(D.evp0, st));
+            HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
+                               cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
+            HIP_OK(hipEventRecord(D.evp1, st));
+            prep_launches++;
+        }
+        HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
+        if (o->mode == MCPT_MODE_MIS)
+            hipLaunchKernelGGL(k_extend_mis, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, P,
+                               *cur, ni, *nxt);
+        else if (o->mode == MCPT_MODE_SHADE)
+            hipLaunchKernelGGL(k_extend_shade, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
+                               P, *cur, ni, *nxt);
+        else
+            hipLaunchKernelGGL(k_extend_brdf, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
+                               P, *cur, ni, *nxt);
+        HIP_OK(hipGetLastError());
+        if (prep) {
+            float ms = 0;
+            HIP_OK(hipEventSynchronize(D.evp1));
+            HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
+            prep_ms += ms;
+        }
+        std::swap(cur, nxt);
     }
     HIP_OK(hipEventRecord(D.ev1, st));
     HIP_OK(hipEventSynchronize(D.ev1));

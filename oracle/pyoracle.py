@@ -124,6 +124,11 @@ class Scene:
         lib().orc_scene_lights(self.h, f, a)
         return f, a
 
+    def camera(self):
+        """the XML <camera> (dist_scale 1), or None if the file has none"""
+        c = Camera()
+        return c if lib().orc_scene_camera(self.h, C.byref(c)) == 0 else None
+
     def build_grid(self, camera_pos, n0=100000):
         lib().orc_grid_build(self.h, _v(camera_pos), n0)
 

@@ -10,7 +10,7 @@
 // everything else (grid traversal, light prep/sampling, BRDF, RNG sites).  Outputs go to
 // tests/golden/*.npy and pin oracle/mcpt_oracle.c (tests/test_oracle_golden.py).
 //
-// usage: ref_harness <scene.obj> <lights.xml> <outdir>
+// usage: ref_harness <scene.obj> <lights.xml> <outdir> [stat <mode> <W> <H> <spp> <row0> <row1> <clock0>]
 #define TINYOBJLOADER_IMPLEMENTATION
 #include "Myobj.h"
 #include "Mylight.h"
@@ -230,6 +230,36 @@ int main(int argc, char** argv) {
     Cam cam0 = make_cam(400, 300);
     veach->cal_scene_boundingbox(cam0.eye);
     veach->meshing(100000);
+
+    // ---- G8 statistical reference: `... <outdir> stat <mode> <W> <H> <spp> <row0>
+    // <row1> <clock0>` renders rows [row0, row1) of a W x H frame with spp fake-clock samples per
+    // pixel and writes per-pixel sum L and sum L^2 (rows x W x 6) to <outdir>/stat_<mode>_<row0>.npy.
+    // Run as several processes over disjoint rows (the reference's global state is not thread-safe).
+    if (argc >= 12 && std::string(argv[4]) == "stat") {
+        const int mode = atoi(argv[5]), W = atoi(argv[6]), H = atoi(argv[7]), spp = atoi(argv[8]);
+        const int r0 = atoi(argv[9]), r1 = atoi(argv[10]);
+        clk() = strtoull(argv[11], nullptr, 10);
+        Cam c = make_cam(W, H);
+        std::vector<double> o;
+        for (int i = r0; i < r1; i++)
+            for (int j = 0; j < W; j++) {
+                vec dir = cam_dir(c, i, j);
+                intersec_result rs = veach->closet_ray_intersect(c.eye, dir, triangle(-1, -1));
+                double s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
+                for (int k = 0; k < spp && rs.isIntersec; k++) {
+                    RadianceRGB L = mode == 0 ? ref_shade_mis(rs, dir * -1)
+                                    : mode == 1 ? ref_shade_brdf(rs, dir * -1) : ref_shade(rs, dir * -1);
+                    for (int q = 0; q < 3; q++) {
+                        s1[q] += L.RGB[q];
+                        s2[q] += L.RGB[q] * L.RGB[q];
+                    }
+                }
+                for (int q = 0; q < 3; q++) o.push_back(s1[q]);
+                for (int q = 0; q < 3; q++) o.push_back(s2[q]);
+            }
+        npy_f64(out + "/stat_" + std::to_string(mode) + "_" + std::to_string(r0) + ".npy", o, 6);
+        return 0;
+    }
 
     // ---- G0/G6 loader, unique normals, light table ------------------------------------
     {

@@ -1,6 +1,8 @@
 import os
 import pathlib
+import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -26,3 +28,14 @@ def _built():
     if not (ROOT / "oracle" / "liboracle.so").exists():
         os.system("make -s -C %s" % (ROOT / "oracle"))
     yield
+
+
+def cornell_scene(triangles, seed=20240430):
+    """(obj, xml) of the Cornell + random-triangles stand-in (scenes/gen_cornell_random.py, config C5),
+    generated once per (triangles, seed) into the temp directory."""
+    d = pathlib.Path(tempfile.gettempdir()) / ("mcpt_cornell_%d_%d" % (triangles, seed))
+    obj, xml = d / "cornell-random.obj", d / "cornell-random.xml"
+    if not (obj.exists() and xml.exists()):
+        subprocess.run([sys.executable, str(ROOT / "scenes" / "gen_cornell_random.py"), "--triangles",
+                        str(triangles), "--seed", str(seed), str(d)], check=True, capture_output=True)
+    return str(obj), str(xml)
