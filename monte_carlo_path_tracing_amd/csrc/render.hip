@@ -178,6 +178,96 @@ __device__ inline Hit trace(const BvhNode* __restrict__ nodes, const float4* __r
     return best;
 }
 
+// trace() for the split pipeline's ray kernels: a short LDS stack of kLds entries per lane with a
+// private (scratch) overflow up to kStack, slab tests as one FMA per plane (origin * inverse
+// precomputed; the boxes' conservative margins absorb the extra rounding), and a sign pre-test
+// that rejects beta < 0, gamma < 0 and t < 0 before the three fp64 divisions of the reference's
+// Cramer rule (a nonzero quotient has the sign of its operands; the divisions of the surviving
+// candidates are exactly tri_hit's, so accepted hits are bit-identical).
+template <int kLds>
+__device__ inline Hit trace_s(const BvhNode* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
+                              int exclude, int* __restrict__ lds, int stride) {
+    Hit best{-1, DBL_MAX, 0, 0};
+    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
+    int spill[kStack - kLds];
+    auto inv = [](double d) {
+        float f = (float)d;
+        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
+        return 1.0f / f;
+    };
+    const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
+    const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
+    float tlimit = FLT_MAX;
+    int sp = 0;
+    int node = 0;
+    while (true) {
+        const BvhNode nd = nodes[node];
+        float tn[2];
+        bool hitc[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const float tx0 = fmaf(nd.lo[k][0], ix, -oix), tx1 = fmaf(nd.hi[k][0], ix, -oix);
+            const float ty0 = fmaf(nd.lo[k][1], iy, -oiy), ty1 = fmaf(nd.hi[k][1], iy, -oiy);
+            const float tz0 = fmaf(nd.lo[k][2], iz, -oiz), tz1 = fmaf(nd.hi[k][2], iz, -oiz);
+            const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+            const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+            hitc[k] = t0 <= t1 * 1.00001f + 1e-6f;
+            tn[k] = t0;
+        }
+        int next[2];
+        int nn = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (!hitc[k]) continue;
+            const int c = nd.child[k];
+            if (c >= 0) {
+                next[nn++] = c;
+                continue;
+            }
+            const int first = ~c, cnt = nd.count[k];
+            for (int q = first; q < first + cnt; q++) {
+                const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
+                const int fac = __float_as_int(a4.w);
+                if (fac == exclude) continue;
+                const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
+                const double detA = det3(ab, ac, rd);
+                if (fabs(detA) < MCPT_EPS) continue;
+                const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
+                const bool neg = detA < 0;
+                if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
+                    continue;  // beta, gamma or t < 0
+                const double beta = nb / detA, gamma = ng / detA, t = nt / detA;
+                if (beta < 0 || gamma < 0 || beta + gamma > 1 || t < 0 || fabs(t) < MCPT_EPS) continue;
+                if (t < best.t || (t == best.t && fac < best.f)) {
+                    best.f = fac;
+                    best.t = t;
+                    best.beta = beta;
+                    best.gamma = gamma;
+                    tlimit = (float)t * 1.0001f + 1e-5f;
+                }
+            }
+        }
+        if (nn == 2) {
+            int nearc = next[0], farc = next[1];
+            if (tn[1] < tn[0]) {
+                nearc = next[1];
+                farc = next[0];
+            }
+            if (sp < kLds) lds[sp * stride] = farc;
+            else if (sp < kStack) spill[sp - kLds] = farc;
+            sp = sp < kStack ? sp + 1 : sp;
+            node = nearc;
+        } else if (nn == 1) {
+            node = next[0];
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = sp < kLds ? lds[sp * stride] : spill[sp - kLds];
+        }
+    }
+    return best;
+}
+
 // ============================================================================================
 // wavefront queue (SoA)
 // ============================================================================================
@@ -1106,6 +1196,145 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur,
     }
 }
 
+// ---- MIS node split into three kernels (ray generation / traversal / combination) -------------
+// k_extend_mis does everything per lane with three inlined traversals (152 VGPRs, 3 waves/SIMD).
+// Split, the traversal kernel runs at high occupancy on a short LDS stack, and the shading
+// kernels carry no traversal state.  Per node in `Aux` (capacity = queue capacity):
+//   d1, d2   light / BRDF directions (3 doubles each)
+//   w1       tp * f(wl) * cos / (p_light + p_phong) / 0.6  -- the light child's throughput
+//   w2       tp * f(wi); c2 = (pdf, cos) of the BRDF sample -- the BRDF child's throughput needs
+//            the light pdf of the light-only hit (main.cpp:482-487)
+//   flags    bit 0 trace d1, bit 1 trace d2, bit 2 trace d2 against the light BVH
+//   hf/hbg   ray set k in [k*cap, (k+1)*cap): hit facet, (beta, gamma)
+struct Aux {
+    double *d1, *d2, *w1, *w2, *c2, *hbg;
+    int *flags, *hf;
+    int cap;
+};
+constexpr int kRayBlock = 256;
+constexpr int kRayLds = 16;  // LDS stack entries per lane (16 KB per 256-lane block)
+
+__global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux A) {
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const d3 p = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
+    const d3 N = mk3(cur.n[3 * i], cur.n[3 * i + 1], cur.n[3 * i + 2]);
+    const d3 wo = mk3(cur.wo[3 * i], cur.wo[3 * i + 1], cur.wo[3 * i + 2]);
+    const d3 tp = mk3(cur.tp[3 * i], cur.tp[3 * i + 1], cur.tp[3 * i + 2]);
+    const int f = cur.f[i];
+    const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
+    const float* m = S.mtl + 7 * S.tri_mat[f];
+    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
+    const double sh = m[6];
+    const double wsum = cur.wsum[i];
+    const int pick = cur.pick[i];
+    int flags = 0;
+    // ---- light branch (main.cpp:443-466) ----
+    d3 coord;
+    double lprob = 1;
+    if (pick >= 0) {
+        const double4 ln = S.lt_n[pick];
+        SphTri sph;
+        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph, true);
+        const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
+        TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
+        coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:475-481)
+        lprob = S.light_sum[pick] / wsum;
+    } else {
+        coord = add(mul(N, -1), p);  // Mylight.cpp:427-430
+    }
+    const d3 wl = normalized(sub(coord, p));
+    d3 w1 = mk3(0, 0, 0);
+    if (dot(wl, N) > 0) {
+        flags |= 1;
+        const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
+        const double pp = phong_pdf(N, wl, wo, kd, ks, sh);
+        w1 = mul(hmul(tp, b), dot(wl, N) / (lprob + pp) / MCPT_P_RR);
+    }
+    // ---- BRDF branch (main.cpp:469-493) ----
+    double pdf;
+    const d3 wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+    d3 w2 = mk3(0, 0, 0);
+    if (!(dot(wi, N) < 0)) {
+        flags |= 2;
+        if (!(fabs(wsum) < MCPT_EPS)) flags |= 4;  // light pdf can only be nonzero with a light set
+        w2 = hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh));
+    }
+    A.d1[3 * i] = wl.x, A.d1[3 * i + 1] = wl.y, A.d1[3 * i + 2] = wl.z;
+    A.d2[3 * i] = wi.x, A.d2[3 * i + 1] = wi.y, A.d2[3 * i + 2] = wi.z;
+    A.w1[3 * i] = w1.x, A.w1[3 * i + 1] = w1.y, A.w1[3 * i + 2] = w1.z;
+    A.w2[3 * i] = w2.x, A.w2[3 * i + 1] = w2.y, A.w2[3 * i + 2] = w2.z;
+    A.c2[2 * i] = pdf, A.c2[2 * i + 1] = dot(wi, N);
+    A.flags[i] = flags;
+}
+
+// closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
+// queue's shading points, excluding the origin facet
+__global__ __launch_bounds__(kRayBlock) void k_mis_rays(DScene S, Queue cur, int n, Aux A) {
+    __shared__ int stack[kRayLds * kRayBlock];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int set = blockIdx.y;
+    if (i >= n) return;
+    const int fl = A.flags[i];
+    int f = -1;
+    double beta = 0, gamma = 0;
+    if (fl & (1 << set)) {
+        const double* d = set == 0 ? A.d1 : A.d2;
+        const d3 ro = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
+        const d3 rd = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        const Hit h = set == 2 ? trace_s<kRayLds>(S.lbvh, S.lleaf_v, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock)
+                               : trace_s<kRayLds>(S.bvh, S.leaf_v, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
+        f = h.f;
+        beta = h.beta;
+        gamma = h.gamma;
+    }
+    const size_t o = (size_t)set * A.cap + i;
+    A.hf[o] = f;
+    if (set < 2) {
+        A.hbg[2 * o] = beta;
+        A.hbg[2 * o + 1] = gamma;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt) {
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    const int ii = active ? i : 0;
+    const int fl = A.flags[ii];
+    const int pixel = cur.pixel[ii], sample = cur.sample[ii];
+    const uint64_t node = cur.node[ii];
+    const size_t o1 = ii, o2 = (size_t)A.cap + ii, ol = 2 * (size_t)A.cap + ii;
+    const bool c1 = active && (fl & 1) && A.hf[o1] >= 0;
+    const bool c2 = active && (fl & 2) && A.hf[o2] >= 0;
+    d3 tp2 = mk3(0, 0, 0);
+    if (c2) {
+        double lpdf = 0;
+        const int lf = (fl & 4) ? A.hf[ol] : -1;
+        if (lf >= 0) {
+            const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
+            const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
+            const int li = S.tri_light[lf];
+            const PrepLight L = load_light(S, li);
+            double wl_unused;
+            if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) && light_weight(L.p0, L.p1, L.p2, L.lsum, p, &wl_unused))
+                lpdf = S.light_sum[li] / cur.wsum[ii];  // fresh-state eval (Mylight.cpp:484-493)
+        }
+        tp2 = mul(mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]), A.c2[2 * ii + 1] / (A.c2[2 * ii] + lpdf) / MCPT_P_RR);
+    }
+    const d3 d1 = mk3(A.d1[3 * ii], A.d1[3 * ii + 1], A.d1[3 * ii + 2]);
+    const d3 d2 = mk3(A.d2[3 * ii], A.d2[3 * ii + 1], A.d2[3 * ii + 2]);
+    const d3 tp1 = mk3(A.w1[3 * ii], A.w1[3 * ii + 1], A.w1[3 * ii + 2]);
+    node_entry(P, c1, c1 ? A.hf[o1] : -1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), tp1, pixel, sample, 2 * node, nxt);
+    node_entry(P, c2, c2 ? A.hf[o2] : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), tp2, pixel, sample, 2 * node + 1, nxt);
+    if (active) {
+        const unsigned nr = (fl & 1) + ((fl >> 1) & 1);
+        atomicAdd(P.stats + 2, (unsigned long long)nr);
+        if (c2) atomicAdd(P.stats + 3, 1ull);
+    }
+}
+
 // one shade() node (main.cpp:295-343), lane per node: the direct-light estimate is splatted into
 // the framebuffer here; RR, then at most one child (a Phong-sampled bounce that hits a non-emitter,
 // main.cpp:335) through node_entry.  The light point comes from the prep kernel's pick -- the
@@ -1263,7 +1492,7 @@ struct DeviceState {
     std::vector<void*> allocs;
     hipStream_t stream = nullptr;
     // reusable work buffers
-    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14];
+    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14], aux[8];
     unsigned* pinned_count = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr;
 };
@@ -1392,6 +1621,25 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     return MCPT_OK;
 }
 
+int alloc_aux(DevBuf* b, int cap, Aux& a) {
+    const size_t c = (size_t)cap;
+    const size_t sz[8] = {24 * c, 24 * c, 24 * c, 24 * c, 16 * c, 2 * 16 * c, 4 * c, 3 * 4 * c};
+    for (int k = 0; k < 8; k++) {
+        int rc = ensure(b[k], sz[k]);
+        if (rc) return rc;
+    }
+    a.d1 = (double*)b[0].p;
+    a.d2 = (double*)b[1].p;
+    a.w1 = (double*)b[2].p;
+    a.w2 = (double*)b[3].p;
+    a.c2 = (double*)b[4].p;
+    a.hbg = (double*)b[5].p;
+    a.flags = (int*)b[6].p;
+    a.hf = (int*)b[7].p;
+    a.cap = cap;
+    return MCPT_OK;
+}
+
 int alloc_queue(DevBuf* b, int cap, Queue& q) {
     const size_t c = (size_t)cap;
     const size_t sz[14] = {24 * c, 24 * c, 24 * c, 24 * c, 4 * c, 4 * c, 4 * c, 8 * c, 8 * c, 4 * c, 64, 0, 0, 0};
@@ -1503,6 +1751,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         return rc;
     Queue qa, qb;
     if ((rc = alloc_queue(D.qa, cap, qa)) || (rc = alloc_queue(D.qb, cap, qb))) return rc;
+    static const bool fused_mis = getenv("MCPT_FUSED_MIS") != nullptr;  // A/B: the single-kernel form
+    Aux aux{};
+    if (o->mode == MCPT_MODE_MIS && !fused_mis && (rc = alloc_aux(D.aux, cap, aux))) return rc;
     hipStream_t st = D.stream;
     Params P;
     P.S = D.d;
@@ -1566,7 +1817,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             prep_launches++;
         }
         HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
-        if (o->mode == MCPT_MODE_MIS)
+        if (o->mode == MCPT_MODE_MIS && !fused_mis) {
+            hipLaunchKernelGGL(k_mis_gen, dim3((ni + 255) / 256), dim3(256), 0, st, P, *cur, ni, aux);
+            hipLaunchKernelGGL(k_mis_rays, dim3((ni + kRayBlock - 1) / kRayBlock, 3), dim3(kRayBlock), 0, st, D.d, *cur,
+                               ni, aux);
+            hipLaunchKernelGGL(k_mis_combine, dim3((ni + 255) / 256), dim3(256), 0, st, P, *cur, ni, aux, *nxt);
+        } else if (o->mode == MCPT_MODE_MIS)
             hipLaunchKernelGGL(k_extend_mis, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, P,
                                *cur, ni, *nxt);
         else if (o->mode == MCPT_MODE_SHADE)

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """TEST INFRASTRUCTURE ONLY -- G8, the statistical reference of SURVEY.md §8(c): the compiled
 reference (oracle/_ref/ref_harness, fake clock) renders a 32x24 frame of the Veach-MIS stand-in at
-1024 spp per integrator; the per-pixel mean and variance of one sample go to
-tests/golden/stat_<mode>_32x24x1024.npy (H x W x 6: mean rgb, var rgb).  8 processes over disjoint
+1024 spp per integrator (65536 for the heavy-tailed BRDF-only one); the per-pixel mean and
+variance of one sample go to tests/golden/stat_<mode>_32x24x<spp>.npy (H x W x 6: mean rgb, var rgb).  8 processes over disjoint
 row bands, each with its own fake-clock start.  Run in this container only (needs /root/reference):
 
-    python oracle/make_g8.py [--modes 0,1,2] [--spp 1024] [--jobs 8]
+    python oracle/make_g8.py --modes 0,2 --spp 1024 && python oracle/make_g8.py --modes 1 --spp 65536
 """
 import argparse
 import os
