@@ -2,9 +2,11 @@
 """Benchmark: Msamples/s of the MI355X path tracer on the Veach-MIS stand-in (BASELINE.json).
 
 Workload (BASELINE.json configs[2]): MIS (light + BRDF sampling), 800x600, frame of
-steps x gpus x spp_per_step samples per pixel (default 128 x 1 x 8 = 1024 spp).  A "step" is one
+steps x gpus x spp_per_step samples per pixel (default 32 x 1 x 32 = 1024 spp).  A "step" is one
 pass of the hot path over one batch: spp_per_step samples of every pixel of the 800x600 frame,
-rendered by the wavefront kernels into an fp64 framebuffer resident in HBM.
+rendered by one mcpt_render_device call (wavefront kernels, fp64 framebuffer resident in HBM).
+Each call computes everything it uses, including its root-point light-prep cache (DESIGN.md §4.4);
+nothing is carried from one step to the next except the framebuffer.
 
 Multi-GPU (torchrun, one process per GPU): weak scaling by sample-range sharding -- rank r renders
 global samples [(k*G + r)*S, (k*G + r + 1)*S) in step k -- and ONE RCCL reduce of the framebuffer
@@ -95,9 +97,9 @@ def cpu_baseline(scene_name, W, H, mode, seed, target_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--spp-per-step", type=int, default=8)
+    ap.add_argument("--spp-per-step", type=int, default=32)
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--mode", default="mis", choices=["mis", "brdf", "shade"])
@@ -186,13 +188,14 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 per_node = json.load(f).get("hbm_bytes_per_node")
-            nodes = totals.get("shading_nodes", 0)
+            nodes = totals.get("prep_full_nodes", 0)
             traffic = per_node * nodes / launches if per_node is not None else None
         roofline = {"bound": "valu_fp64", "kernel": "k_prep", "achieved": round(achieved, 3),
                     "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
                     "traffic": traffic, "avg_launch_ms": round(prep_s / launches * 1e3, 3), "launches": launches,
                     "flop_per_launch": flops / launches, "share_of_device_time": round(prep_s / max(totals["seconds"], 1e-12), 3),
-                    "hbm_algorithmic_GBs": round(totals.get("shading_nodes", 0) * PREP_BYTES_PER_NODE / prep_s / 1e9, 3),
+                    "hbm_algorithmic_GBs": round(totals.get("prep_full_nodes", 0) * PREP_BYTES_PER_NODE / prep_s / 1e9, 3),
+                    "full_prep_nodes": totals.get("prep_full_nodes", 0), "cached_root_nodes": totals.get("prep_cached_nodes", 0),
                     "hbm_peak_GBs": HBM_PEAK_GBS}
     else:
         roofline = {"bound": "valu_fp64", "kernel": "k_extend_brdf", "achieved": None, "peak": FP64_VECTOR_PEAK_TFLOPS,

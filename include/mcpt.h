@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 10000 /* 1.0.0 */
+#define MCPT_VERSION 10100 /* 1.1.0 */
 
 enum {
     MCPT_OK = 0,
@@ -86,10 +86,12 @@ typedef struct {
     uint64_t generations;   /* wavefront generations launched */
     double prep_seconds;    /* device time inside the light-prep kernel (HIP events, its stream) */
     uint64_t prep_launches;
-    uint64_t light_evals_total;           /* shading nodes x light triangles (MIS) */
+    uint64_t light_evals_total;           /* prep_full_nodes x light triangles (MIS, shade) */
     uint64_t light_evals_culled_backface; /* culled by the light-side test (Mylight.cpp:340-345) */
     uint64_t light_evals_culled_plane;    /* culled by the tangent-plane test (Mylight.cpp:347-357) */
     uint64_t light_evals_candidates;      /* passed both; evaluated in full (Mylight.cpp:360-413) */
+    uint64_t prep_full_nodes;   /* prep nodes that ran the O(N_L) stages (incl. root-cache builds) */
+    uint64_t prep_cached_nodes; /* root nodes served by the per-pixel root-point cache (pick only) */
 } mcpt_stats;
 
 int mcpt_version(void);

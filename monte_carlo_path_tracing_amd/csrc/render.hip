@@ -291,7 +291,8 @@ struct Params {
     uint64_t seed;
     double inv_spp;
     double* fb;                  // W*H*3 fp64
-    unsigned long long* stats;   // [0] nodes pushed [1] light survivors [2] rays [3] light rays [4] overflow
+    unsigned long long* stats;   // [0] cached root preps [1] light survivors [2] rays [3] light rays [4] overflow
+                                 // [5] prep candidates [6] light-side culls [7] full preps
     int mode;
 };
 
@@ -310,6 +311,17 @@ __device__ inline int wave_append(unsigned* counter, bool want) {
     return want ? (int)(base + __popcll(below)) : -1;
 }
 
+// shading point and normal of a hit (main.cpp:406-407: interpolated position, normalised
+// interpolation of the vertex normals)
+__device__ inline void node_point(const DScene& S, int f, double beta, double gamma, d3* p, d3* N) {
+    const float4* v = S.tri_v + 3 * f;
+    const float* nv = S.tri_n + 9 * f;
+    const double a0 = 1.0 - beta - gamma;
+    *p = add(add(mul(f3(v[0]), a0), mul(f3(v[1]), beta)), mul(f3(v[2]), gamma));
+    *N = normalized(add(add(mul(mk3(nv[0], nv[1], nv[2]), a0), mul(mk3(nv[3], nv[4], nv[5]), beta)),
+                        mul(mk3(nv[6], nv[7], nv[8]), gamma)));
+}
+
 // node entry of shade_with_* (main.cpp:406-437 / :351-383): interpolate, back-face -> 0,
 // emitter -> emit, Russian roulette; survivors are appended to the queue.
 // Must be called by ALL lanes of the wave (wave_append); `active` masks the lane.
@@ -322,12 +334,7 @@ __device__ inline void node_entry(const Params& P, bool active, int f, double be
         // MIS: heap ids (root 1, children 2n, 2n+1); BRDF / shade: paths (node = depth + 1)
         const bool too_deep = P.mode == MCPT_MODE_MIS ? node >= (2ull << MCPT_MAX_DEPTH) : node > MCPT_MAX_DEPTH + 1;
         if (!too_deep) {
-            const float4* v = S.tri_v + 3 * f;
-            const float* nv = S.tri_n + 9 * f;
-            const double a0 = 1.0 - beta - gamma;
-            p = add(add(mul(f3(v[0]), a0), mul(f3(v[1]), beta)), mul(f3(v[2]), gamma));
-            N = normalized(add(add(mul(mk3(nv[0], nv[1], nv[2]), a0), mul(mk3(nv[3], nv[4], nv[5]), beta)),
-                               mul(mk3(nv[6], nv[7], nv[8]), gamma)));
+            node_point(S, f, beta, gamma, &p, &N);
             if (!(dot(N, wo) < 0)) {
                 const int li = S.tri_light[f];
                 if (li >= 0) {
@@ -409,6 +416,29 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
         }
     }
     node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
+}
+
+// root shading points of the pixels whose primary hit is a front-facing non-emitter (the nodes
+// that reach the light prep at the root), compacted into q for the root-cache build
+__global__ __launch_bounds__(256) void k_root_points(DScene S, CamFrame cam, const int* hit_f, const double* hit_tbg,
+                                                     Queue q) {
+    const int px = blockIdx.x * blockDim.x + threadIdx.x;
+    const int npx = cam.W * cam.H;
+    bool want = false;
+    d3 p = mk3(0, 0, 0), N = mk3(0, 0, 0);
+    if (px < npx) {
+        const int f = hit_f[px];
+        if (f >= 0 && S.tri_light[f] < 0) {
+            node_point(S, f, hit_tbg[3 * px + 1], hit_tbg[3 * px + 2], &p, &N);
+            want = !(dot(N, mul(cam_dir(cam, px / cam.W, px % cam.W), -1)) < 0);
+        }
+    }
+    const int slot = wave_append(q.count, want);
+    if (want && slot < q.cap) {
+        q.p[3 * slot] = p.x, q.p[3 * slot + 1] = p.y, q.p[3 * slot + 2] = p.z;
+        q.n[3 * slot] = N.x, q.n[3 * slot + 1] = N.y, q.n[3 * slot + 2] = N.z;
+        q.pixel[slot] = px;
+    }
 }
 
 // Light prep, one wave per node (Mylight.cpp:322-422).
@@ -812,6 +842,24 @@ __device__ inline int prep_stage_pk(const DScene& S, int li, float4 X, float4 Y,
     const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
     return light_cheap_stage(mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(ln.x, ln.y, ln.z), x1, n);
 }
+// prep_stage_pk with the sure outcomes as predicates and one rarely-taken branch for the
+// ambiguous lanes (exact fp64 reference arithmetic)
+__device__ inline int prep_stage_pk_bf(const DScene& S, int li, float4 X, float4 Y, float4 Z, float dl, v2f nx2,
+                                       v2f ny2, v2f nz2, v2f nxs, v2f nys, v2f nzs, float cn, d3 x1, d3 n, float err) {
+    constexpr float kEps = 1e-8f;
+    const v2f tab = __builtin_elementwise_fma(nx2, v2f{X.x, X.y}, __builtin_elementwise_fma(ny2, v2f{Y.x, Y.y}, nz2 * v2f{Z.x, Z.y})) - v2f{cn, cn};
+    const v2f tcs = __builtin_elementwise_fma(nxs, v2f{X.z, X.w}, __builtin_elementwise_fma(nys, v2f{Y.z, Y.w}, nzs * v2f{Z.z, Z.w})) - v2f{cn, dl};
+    const float s1 = tcs.y;
+    const float tm = fmaxf(fmaxf(tab.x, tab.y), tcs.x);
+    const float lo = kEps - err, hi = kEps + err;
+    const bool s1_out = s1 < lo, s1_in = s1 > hi, t_out = tm < lo, t_in = tm > hi;
+    int stage = li >= S.NL ? 3 : s1_out ? 1 : (s1_in && t_out) ? 2 : (s1_in && t_in) ? 0 : -1;
+    if (stage < 0) {
+        const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
+        stage = light_cheap_stage(mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(ln.x, ln.y, ln.z), x1, n);
+    }
+    return stage;
+}
 __device__ inline double prep_weight_pk(const DScene& S, int li, d3 x1, bool* ok) {
     const double2* w = S.lt_w + 5 * li;
     const double2 a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
@@ -960,23 +1008,103 @@ __device__ inline int lane_rank(uint64_t m) {  // set bits of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-template <int kMinWavesPerSimd>
+// Root-point cache.  Every camera sample of a pixel starts at the same shading point (the
+// reference re-traces the identical primary ray per sample, main.cpp:572), so the light prep of a
+// root node (x1, n) -- batch totals and candidate list -- is a function of the pixel alone; only the
+// pick (u, dim 1) differs per sample.  A render call with >= 2 samples per pixel builds the cache
+// once over the pixels (build = 1) and root nodes then take the pick-only path (use = 1): the same
+// scan over the same batch totals and the same batch re-evaluation as the full path, so results
+// are identical.
+struct PrepCache {
+    double* bt;           // [npx][nchunks]
+    unsigned short* lst;  // [npx][lstride] candidate list (light indices, index order)
+    double* w;            // [npx][lstride] candidate weights (-1 = culled by the full stage)
+    int4* info;           // [npx] (nb, ncand, survivors, 0)
+    int lstride;
+    int build;            // this launch builds entries of pixel qpixel[node] (qpixel == nullptr: node)
+    int use;              // host side: root nodes go to k_prep_pick
+};
+
+// inverse-CDF pick from the batch totals bt[0, nb) and candidate list lst (LDS or global): returns
+// weights_sum and the picked light (-1 if weights_sum < eps).  u_of() gives dim 1 when needed.
+template <class U>
+__device__ inline double prep_select(const double* bt, const unsigned short* lst, int nb, int ncand, int lane,
+                                     __amdgpu_buffer_rsrc_t rw, d3 x1, U u_of, int* pick_out) {
+    double wsum = 0;
+    int pick = -1;
+    int kb = -1;
+    double base = 0, target = 0;
+    if (nb <= 64) {
+        const double v = lane < nb ? bt[lane] : 0.0;
+        const double cum = wave_incl_scan(v, lane);
+        wsum = __shfl(cum, 63);
+        if (!(fabs(wsum) < MCPT_EPS)) {
+            target = u_of() * wsum;
+            const uint64_t hitm = __ballot(cum >= target && v > 0);
+            const uint64_t posm = __ballot(v > 0);
+            kb = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63 - __clzll((long long)posm);
+            const double exc = __shfl_up(cum, 1);
+            base = kb == 0 ? 0.0 : __shfl(exc, kb);
+        }
+    } else {  // more than 64 batches (N_L > 4096 with many candidates): sequential search
+        for (int b = 0; b < nb; b++) wsum += bt[b];
+        if (!(fabs(wsum) < MCPT_EPS)) {
+            target = u_of() * wsum;
+            int lastpos = -1;
+            double cum = 0;
+            for (int b = 0; b < nb; b++) {
+                const double nxt = cum + bt[b];
+                if (bt[b] > 0) lastpos = b;
+                if (kb < 0 && nxt >= target && bt[b] > 0) {
+                    kb = b;
+                    base = cum;
+                }
+                cum = nxt;
+            }
+            if (kb < 0) {
+                kb = lastpos;
+                base = 0;
+                for (int b = 0; b < kb; b++) base += bt[b];
+            }
+        }
+    }
+    if (kb >= 0) {
+        const int k = 64 * kb + lane;
+        const bool act = k < ncand;
+        const int lj = act ? (int)lst[k] : 0;
+        bool ok;
+        double w = prep_weight_buf(rw, lj, x1, &ok);
+        ok = ok && act;
+        w = act ? w : 0.0;
+        const double sc = wave_incl_scan(w, lane);
+        const uint64_t candm = __ballot(ok && (base + sc >= target));
+        const uint64_t okm = __ballot(ok);
+        int pl = -1;
+        if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+        else if (okm) pl = 63 - __clzll((long long)okm);
+        if (pl >= 0) pick = __shfl(lj, pl);
+    }
+    *pick_out = pick;
+    return wsum;
+}
+
+template <int kMinWavesPerSimd, bool kBuild>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                   const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                   int* __restrict__ pick_out, int* __restrict__ count_out,
                                                   unsigned long long* stats, int nchunks, int wave_bytes,
-                                                  unsigned* __restrict__ work) {
+                                                  unsigned* __restrict__ work, PrepCache C) {
     extern __shared__ double prep_lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
     unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
-    const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, S.NL * 48, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, S.NL * 4, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_w, 0, S.NL * 80, kBufFlags);
-    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
+    const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, nchunks * 3072, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, nchunks * 256, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_w, 0, nchunks * 5120, kBufFlags);
+    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0, full_acc = 0;
     int grab = 0, left = 0;
     while (true) {
         if (left == 0) {
@@ -989,6 +1117,10 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         left--;
         if (node >= n) break;
         const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+        auto u_of = [&]() {
+            return u_override ? u_override[node]
+                              : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+        };
         const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
         const NodeF nf = node_f(x1, nn, S.light_bound);
         const float cn = (float)dot(nn, x1);
@@ -997,11 +1129,13 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
         for (int c = 0; c < nchunks; c++) {
             const int li = c * 64 + lane;
-            const float4 X = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, li * 48, 0, 0));
-            const float4 Y = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, li * 48 + 16, 0, 0));
-            const float4 Z = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, li * 48 + 32, 0, 0));
-            const float dl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, li * 4, 0, 0));
-            const int stage = prep_stage_pk(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
+            // lane offset in VGPR (loop-invariant), chunk offset in SGPR; the tables are padded to
+            // whole chunks, so lanes past N_L read zeros
+            const float4 X = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48, c * 3072, 0));
+            const float4 Y = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 16, c * 3072, 0));
+            const float4 Z = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 32, c * 3072, 0));
+            const float dl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, lane * 4, c * 256, 0));
+            const int stage = prep_stage_pk_bf(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
             const uint64_t m = __ballot(stage == 0);
             if (stage == 0) lst[ncand + lane_rank(m)] = (unsigned short)li;
             ncand += __popcll(m);
@@ -1014,6 +1148,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                 double w = prep_weight_buf(rw, act ? (int)lst[k] : 0, x1, &ok);
                 ok = ok && act;
                 w = act ? w : 0.0;
+                if (kBuild && act) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
                 const double sc = wave_incl_scan(w, lane);
                 survivors += __popcll(__ballot(ok));
                 if (lane == 63) bt[nb] = sc;
@@ -1021,46 +1156,75 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             }
         }
         wave_lds_sync();
+        full_acc++;
+        surv_acc += survivors;
+        cand_acc += ncand;
+        c1_acc += culled1;
+        if (kBuild) {  // store the entry of this pixel (C.build)
+            const int px = qpixel ? qpixel[node] : node;
+            for (int b = lane; b < nb; b += 64) C.bt[(size_t)px * nchunks + b] = bt[b];
+            for (int k = lane; k < ncand; k += 64) C.lst[(size_t)px * C.lstride + k] = lst[k];
+            if (lane == 0) C.info[px] = make_int4(nb, ncand, survivors, 0);
+            wave_lds_sync();
+            continue;
+        }
+        int pick;
+        const double wsum = prep_select(bt, lst, nb, ncand, lane, rw, x1, u_of, &pick);
+        if (lane == 0) {
+            wsum_out[node] = wsum;
+            pick_out[node] = pick;
+            if (count_out) count_out[node] = survivors;
+        }
+        wave_lds_sync();
+    }
+    if (lane == 0 && stats) {
+        if (surv_acc) atomicAdd(stats + 1, surv_acc);
+        if (cand_acc) atomicAdd(stats + 5, cand_acc);
+        if (c1_acc) atomicAdd(stats + 6, c1_acc);
+        if (full_acc) atomicAdd(stats + 7, full_acc);
+    }
+}
+
+// root nodes (node id 1) from the root-point cache: prep_select's search with the cached batch
+// totals and candidate weights -- the same scans over the same values, so the same pick -- and no
+// light-triangle arithmetic at all.  One wave per node; no LDS.
+__global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
+                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                                   double* __restrict__ wsum_out, int* __restrict__ pick_out,
+                                                   unsigned long long* stats, int nchunks, unsigned* __restrict__ work,
+                                                   PrepCache C) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long cached = 0;
+    // static wave-strided assignment: a root costs ~the same everywhere, and a shared work counter
+    // would serialise on its one address at this node rate
+    (void)work;
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    for (int node = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); node < n; node += waves) {
+        const int px = qpixel[node];
+        const int4 inf = C.info[px];
+        const int nb = inf.x, ncand = inf.y;
+        const double* bt = C.bt + (size_t)px * nchunks;
         double wsum = 0;
-        int pick = -1;
+        int kb = -1;
+        double base = 0, target = 0;
         if (nb <= 64) {
             const double v = lane < nb ? bt[lane] : 0.0;
             const double cum = wave_incl_scan(v, lane);
             wsum = __shfl(cum, 63);
             if (!(fabs(wsum) < MCPT_EPS)) {
-                double u;
-                if (u_override) u = u_override[node];
-                else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-                const double target = u * wsum;
+                target = counter_u(counter_key(seed, (uint64_t)px, (uint64_t)qsample[node], qnode[node]), 1) * wsum;
                 const uint64_t hitm = __ballot(cum >= target && v > 0);
                 const uint64_t posm = __ballot(v > 0);
-                const int kb = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63 - __clzll((long long)posm);
+                kb = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63 - __clzll((long long)posm);
                 const double exc = __shfl_up(cum, 1);
-                const double base = kb == 0 ? 0.0 : __shfl(exc, kb);
-                const int k = 64 * kb + lane;
-                const bool act = k < ncand;
-                const int lj = act ? (int)lst[k] : 0;
-                bool ok;
-                double w = prep_weight_buf(rw, lj, x1, &ok);
-                ok = ok && act;
-                w = act ? w : 0.0;
-                const double sc = wave_incl_scan(w, lane);
-                const uint64_t candm = __ballot(ok && (base + sc >= target));
-                const uint64_t okm = __ballot(ok);
-                int pl = -1;
-                if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-                else if (okm) pl = 63 - __clzll((long long)okm);
-                if (pl >= 0) pick = __shfl(lj, pl);
+                base = kb == 0 ? 0.0 : __shfl(exc, kb);
             }
-        } else {  // more than 64 batches (N_L > 4096 with many candidates): sequential search
+        } else {
             for (int b = 0; b < nb; b++) wsum += bt[b];
             if (!(fabs(wsum) < MCPT_EPS)) {
-                double u;
-                if (u_override) u = u_override[node];
-                else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-                const double target = u * wsum;
-                int kb = -1, lastpos = -1;
-                double cum = 0, base = 0;
+                target = counter_u(counter_key(seed, (uint64_t)px, (uint64_t)qsample[node], qnode[node]), 1) * wsum;
+                int lastpos = -1;
+                double cum = 0;
                 for (int b = 0; b < nb; b++) {
                     const double nxt = cum + bt[b];
                     if (bt[b] > 0) lastpos = b;
@@ -1075,37 +1239,29 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                     base = 0;
                     for (int b = 0; b < kb; b++) base += bt[b];
                 }
-                const int k = 64 * kb + lane;
-                const bool act = k < ncand;
-                const int lj = act ? (int)lst[k] : 0;
-                bool ok;
-                double w = prep_weight_buf(rw, lj, x1, &ok);
-                ok = ok && act;
-                w = act ? w : 0.0;
-                const double sc = wave_incl_scan(w, lane);
-                const uint64_t candm = __ballot(ok && (base + sc >= target));
-                const uint64_t okm = __ballot(ok);
-                int pl = -1;
-                if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-                else if (okm) pl = 63 - __clzll((long long)okm);
-                if (pl >= 0) pick = __shfl(lj, pl);
             }
+        }
+        int pick = -1;
+        if (kb >= 0) {
+            const int k = 64 * kb + lane;
+            const bool act = k < ncand;
+            const double wc = act ? C.w[(size_t)px * C.lstride + k] : -1.0;
+            const bool ok = wc >= 0;
+            const double sc = wave_incl_scan(ok ? wc : 0.0, lane);
+            const uint64_t candm = __ballot(ok && (base + sc >= target));
+            const uint64_t okm = __ballot(ok);
+            int pl = -1;
+            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+            else if (okm) pl = 63 - __clzll((long long)okm);
+            if (pl >= 0) pick = C.lst[(size_t)px * C.lstride + 64 * kb + pl];
         }
         if (lane == 0) {
             wsum_out[node] = wsum;
             pick_out[node] = pick;
-            if (count_out) count_out[node] = survivors;
         }
-        surv_acc += survivors;
-        cand_acc += ncand;
-        c1_acc += culled1;
-        wave_lds_sync();
+        cached++;
     }
-    if (lane == 0 && stats) {
-        if (surv_acc) atomicAdd(stats + 1, surv_acc);
-        if (cand_acc) atomicAdd(stats + 5, cand_acc);
-        if (c1_acc) atomicAdd(stats + 6, c1_acc);
-    }
+    if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
 }
 
 // one MIS node (main.cpp:440-493), lane per node; children go through node_entry.
@@ -1271,10 +1427,10 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 
 // closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
 // queue's shading points, excluding the origin facet
-__global__ __launch_bounds__(kRayBlock) void k_mis_rays(DScene S, Queue cur, int n, Aux A) {
+__global__ __launch_bounds__(kRayBlock) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set) {
     __shared__ int stack[kRayLds * kRayBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int set = blockIdx.y;
+    const int set = blockIdx.y + first_set;
     if (i >= n) return;
     const int fl = A.flags[i];
     int f = -1;
@@ -1333,6 +1489,130 @@ __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n,
         atomicAdd(P.stats + 2, (unsigned long long)nr);
         if (c2) atomicAdd(P.stats + 3, 1ull);
     }
+}
+
+// ---- shade() and shade_with_brdf nodes in the same split form (k_mis_rays traces sets 0-1 / 1) ----
+// shade: gen samples the light point (d1, its facet in hf[2 cap + i], the splat tp * L_dir / spp
+// in w1) and, after RR, the bounce (d2, the child's throughput in w2); combine splats L_dir if the
+// shadow ray's first hit is the sampled light facet (main.cpp:306-315) and spawns the bounce child
+// if it hits a non-emitter (main.cpp:335).
+__global__ __launch_bounds__(256) void k_shade_gen(Params P, Queue cur, int n, Aux A) {
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const d3 p = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
+    const d3 N = mk3(cur.n[3 * i], cur.n[3 * i + 1], cur.n[3 * i + 2]);
+    const d3 wo = mk3(cur.wo[3 * i], cur.wo[3 * i + 1], cur.wo[3 * i + 2]);
+    const d3 tp = mk3(cur.tp[3 * i], cur.tp[3 * i + 1], cur.tp[3 * i + 2]);
+    const int f = cur.f[i];
+    const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
+    const float* m = S.mtl + 7 * S.tri_mat[f];
+    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
+    const double sh = m[6];
+    const int pick = cur.pick[i];
+    int flags = 0;
+    // ---- direct light (main.cpp:295-316) ----
+    d3 coord, n1 = N, w1 = mk3(0, 0, 0);
+    double lprob = 1;
+    if (pick >= 0) {
+        const double4 ln = S.lt_n[pick];
+        SphTri sph;
+        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph, true);
+        const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
+        TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
+        coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:311-317)
+        lprob = S.light_sum[pick] / cur.wsum[i];
+        n1 = mk3(ln.x, ln.y, ln.z);
+    } else {
+        coord = add(mul(N, -1), p);  // empty set: x1 - n (Mylight.cpp:263-266); wl = -N never passes wl.N > 0
+    }
+    const d3 wl = normalized(sub(coord, p));
+    if (pick >= 0 && dot(wl, N) > 0 && dot(mul(wl, -1), n1) > 0) {
+        flags |= 1;
+        const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
+        const d3 d = sub(coord, p);
+        const d3 I = mk3(S.light_rad[3 * pick], S.light_rad[3 * pick + 1], S.light_rad[3 * pick + 2]);
+        const d3 Ld = mul(hmul(I, b), dot(wl, N) * dot(mul(wl, -1), n1) / dot(d, d) / lprob);
+        w1 = mk3(tp.x * Ld.x * P.inv_spp, tp.y * Ld.y * P.inv_spp, tp.z * Ld.z * P.inv_spp);
+    }
+    // ---- indirect (main.cpp:318-343) ----
+    d3 wi = mk3(0, 0, 0), w2 = mk3(0, 0, 0);
+    if (!(counter_u(key, 0) > MCPT_P_RR)) {
+        double pdf;
+        wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+        if (!(dot(wi, N) < 0)) {
+            flags |= 2;
+            w2 = mul(hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
+        }
+    }
+    A.d1[3 * i] = wl.x, A.d1[3 * i + 1] = wl.y, A.d1[3 * i + 2] = wl.z;
+    A.d2[3 * i] = wi.x, A.d2[3 * i + 1] = wi.y, A.d2[3 * i + 2] = wi.z;
+    A.w1[3 * i] = w1.x, A.w1[3 * i + 1] = w1.y, A.w1[3 * i + 2] = w1.z;
+    A.w2[3 * i] = w2.x, A.w2[3 * i + 1] = w2.y, A.w2[3 * i + 2] = w2.z;
+    A.hf[2 * (size_t)A.cap + i] = pick >= 0 ? S.light_facet[pick] : -1;
+    A.flags[i] = flags;
+}
+
+__global__ __launch_bounds__(256) void k_shade_combine(Params P, Queue cur, int n, Aux A, Queue nxt) {
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    const int ii = active ? i : 0;
+    const int fl = A.flags[ii];
+    const size_t o1 = ii, o2 = (size_t)A.cap + ii;
+    if (active && (fl & 1) && A.hf[o1] >= 0 && A.hf[o1] == A.hf[2 * (size_t)A.cap + ii]) {
+        double* px = P.fb + 3 * (size_t)cur.pixel[ii];
+        unsafeAtomicAdd(px + 0, A.w1[3 * ii]);
+        unsafeAtomicAdd(px + 1, A.w1[3 * ii + 1]);
+        unsafeAtomicAdd(px + 2, A.w1[3 * ii + 2]);
+    }
+    const int h2 = A.hf[o2];
+    const bool c = active && (fl & 2) && h2 >= 0 && S.tri_light[h2] < 0;
+    const d3 d2 = mk3(A.d2[3 * ii], A.d2[3 * ii + 1], A.d2[3 * ii + 2]);
+    const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
+    node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
+               cur.node[ii] + 1, nxt);
+    if (active) atomicAdd(P.stats + 2, (unsigned long long)((fl & 1) + ((fl >> 1) & 1)));
+}
+
+// shade_with_brdf (main.cpp:385-396): gen samples the bounce, combine spawns the child on any hit
+__global__ __launch_bounds__(256) void k_brdf_gen(Params P, Queue cur, int n, Aux A) {
+    const DScene& S = P.S;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const d3 N = mk3(cur.n[3 * i], cur.n[3 * i + 1], cur.n[3 * i + 2]);
+    const d3 wo = mk3(cur.wo[3 * i], cur.wo[3 * i + 1], cur.wo[3 * i + 2]);
+    const d3 tp = mk3(cur.tp[3 * i], cur.tp[3 * i + 1], cur.tp[3 * i + 2]);
+    const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
+    const float* m = S.mtl + 7 * S.tri_mat[cur.f[i]];
+    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
+    const double sh = m[6];
+    double pdf;
+    const d3 wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+    int flags = 0;
+    d3 w2 = mk3(0, 0, 0);
+    if (!(dot(wi, N) < 0)) {
+        flags = 2;
+        w2 = mul(hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
+    }
+    A.d2[3 * i] = wi.x, A.d2[3 * i + 1] = wi.y, A.d2[3 * i + 2] = wi.z;
+    A.w2[3 * i] = w2.x, A.w2[3 * i + 1] = w2.y, A.w2[3 * i + 2] = w2.z;
+    A.flags[i] = flags;
+}
+
+__global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n, Aux A, Queue nxt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    const int ii = active ? i : 0;
+    const int fl = A.flags[ii];
+    const size_t o2 = (size_t)A.cap + ii;
+    const int h2 = A.hf[o2];
+    const bool c = active && (fl & 2) && h2 >= 0;
+    const d3 d2 = mk3(A.d2[3 * ii], A.d2[3 * ii + 1], A.d2[3 * ii + 2]);
+    const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
+    node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
+               cur.node[ii] + 1, nxt);
+    if (active && (fl & 2)) atomicAdd(P.stats + 2, 1ull);
 }
 
 // one shade() node (main.cpp:295-343), lane per node: the direct-light estimate is splatted into
@@ -1492,7 +1772,7 @@ struct DeviceState {
     std::vector<void*> allocs;
     hipStream_t stream = nullptr;
     // reusable work buffers
-    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14], aux[8];
+    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14], aux[8], cache_bt, cache_lst, cache_info, cache_w;
     unsigned* pinned_count = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr;
 };
@@ -1546,6 +1826,8 @@ std::vector<float4> leaf_vertices(const HostScene& s, const Bvh& b) {
     return v;
 }
 
+int prep_chunks(int NL);
+
 int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if (device < 0) HIP_OK(hipGetDevice(&device));
     for (auto& d : sc->devs)
@@ -1588,9 +1870,10 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     }
     if ((rc = upload(*D, lv, &d.lt_v))) return rc;
     if ((rc = upload(*D, ln, &d.lt_n))) return rc;
-    std::vector<float4> lpk(3 * std::max(s.NL, 1));
-    std::vector<float> ld(std::max(s.NL, 1));
-    std::vector<double2> lw(5 * std::max(s.NL, 1));
+    const int nl_pad = 64 * prep_chunks(s.NL);  // whole chunks: the prep kernel reads past N_L unchecked
+    std::vector<float4> lpk(3 * nl_pad, make_float4(0, 0, 0, 0));
+    std::vector<float> ld(nl_pad, 0.0f);
+    std::vector<double2> lw(5 * nl_pad, make_double2(0, 0));
     for (int l = 0; l < s.NL; l++) {
         const float4 a = lv[3 * l], b = lv[3 * l + 1], c = lv[3 * l + 2];
         lpk[3 * l] = make_float4(a.x, b.x, c.x, a.w);
@@ -1680,12 +1963,14 @@ constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 // work: a device word, zeroed here before the launch (the kernel's dynamic node counter)
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
-                       int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st) {
+                       int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
+                       const PrepCache& cache = PrepCache{}) {
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
     if (variant < 0) variant = list_ok ? 8 : 0;  // A/B on MI355X: tools/prep_variants.py
     if (variant > 0 && !list_ok) variant = 0;
+    if (cache.build && variant != 8) return hipErrorInvalidValue;  // the cache is built by variant 8
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
     hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
@@ -1712,8 +1997,12 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
                                qnode, u, wsum, pick, count, stats, nchunks, wb, work);
             break;
         case 8:
-            hipLaunchKernelGGL((k_prep_pk2<5>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
-                               qnode, u, wsum, pick, count, stats, nchunks, wb, work);
+            if (cache.build)
+                hipLaunchKernelGGL((k_prep_pk2<5, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+                                   qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
+            else
+                hipLaunchKernelGGL((k_prep_pk2<5, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+                                   qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
             break;
         default: MCPT_PREP_LIST(false, 1); break;
     }
@@ -1751,9 +2040,13 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         return rc;
     Queue qa, qb;
     if ((rc = alloc_queue(D.qa, cap, qa)) || (rc = alloc_queue(D.qb, cap, qb))) return rc;
-    static const bool fused_mis = getenv("MCPT_FUSED_MIS") != nullptr;  // A/B: the single-kernel form
+    // extension kernels: MIS and shade split into gen / rays / combine (measured faster), BRDF-only
+    // keeps the single kernel (one ray per node; measured faster).  A/B switches:
+    static const bool fused_env = getenv("MCPT_FUSED_EXTEND") != nullptr;
+    static const bool split_brdf = getenv("MCPT_SPLIT_BRDF") != nullptr;
+    const bool fused = fused_env || (o->mode == MCPT_MODE_BRDF && !split_brdf);
     Aux aux{};
-    if (o->mode == MCPT_MODE_MIS && !fused_mis && (rc = alloc_aux(D.aux, cap, aux))) return rc;
+    if (!fused && (rc = alloc_aux(D.aux, cap, aux))) return rc;
     hipStream_t st = D.stream;
     Params P;
     P.S = D.d;
@@ -1774,7 +2067,46 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         return MCPT_E_SCENE;
     }
     double prep_ms = 0;
-    uint64_t gens = 0, prep_launches = 0, nodes_total = 0;
+    uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0;
+    // root-point cache (see PrepCache): built here when the call has >= 2 samples per pixel and the
+    // entries fit in a 64 GiB budget of HBM (800x600 with N_L = 3012: 15 GB)
+    PrepCache pc{};
+    const int lstride = 64 * nchunks;
+    const size_t cache_bytes = (size_t)npx * ((size_t)nchunks * 8 + (size_t)lstride * 10 + 16);
+    static const bool no_cache = getenv("MCPT_NO_ROOT_CACHE") != nullptr;  // A/B switch
+    if (o->mode != MCPT_MODE_BRDF && s1 - s0 >= 2 && cache_bytes <= (64ull << 30) && !no_cache &&
+        prep_list_wave_bytes(nchunks) * 4 <= kPrepListMaxLds && D.d.NL <= 65535) {
+        if ((rc = ensure(D.cache_bt, (size_t)npx * nchunks * 8)) || (rc = ensure(D.cache_lst, (size_t)npx * lstride * 2)) ||
+            (rc = ensure(D.cache_info, (size_t)npx * 16)) || (rc = ensure(D.cache_w, (size_t)npx * lstride * 8)))
+            return rc;
+        pc.w = (double*)D.cache_w.p;
+        pc.bt = (double*)D.cache_bt.p;
+        pc.lst = (unsigned short*)D.cache_lst.p;
+        pc.info = (int4*)D.cache_info.p;
+        pc.lstride = lstride;
+        HIP_OK(hipMemsetAsync(qb.count, 0, 4, st));
+        hipLaunchKernelGGL(k_root_points, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
+                           (const double*)D.hit_tbg.p, qb);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(D.pinned_count, qb.count, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        const int nr = (int)std::min<unsigned>(D.pinned_count[0], (unsigned)cap);
+        if (nr > 0) {
+            pc.build = 1;
+            HIP_OK(hipEventRecord(D.evp0, st));
+            HIP_OK(launch_prep(8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr, nullptr,
+                               nullptr, P.stats, (unsigned*)D.work.p, st, pc));
+            HIP_OK(hipEventRecord(D.evp1, st));
+            HIP_OK(hipEventSynchronize(D.evp1));
+            float ms = 0;
+            HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
+            prep_ms += ms;
+            prep_launches++;
+            cache_points = (uint64_t)nr;
+        }
+        pc.build = 0;
+        pc.use = 1;
+    }
     Queue* cur = &qa;
     Queue* nxt = &qb;
     HIP_OK(hipMemsetAsync(cur->count, 0, 4, st));
@@ -1793,6 +2125,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     while (true) {
         unsigned n = 0;
         if ((rc = read_count(&n))) return rc;
+        const unsigned n_children = n;  // [0, n_children) children, [n_children, n) fresh roots
         if (rnext < R && n < (unsigned)target) {  // refill with roots (appended through node_entry)
             const int m = (int)std::min<long long>((long long)target - n, R - rnext);
             hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
@@ -1808,20 +2141,52 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         gens++;
         nodes_total += (uint64_t)n;
         const int ni = (int)n;
-        const bool prep = o->mode != MCPT_MODE_BRDF;
-        if (prep) {
-            HIP_OK(hipEventRecord(D.evp0, st));
-            HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                               cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
-            HIP_OK(hipEventRecord(D.evp1, st));
-            prep_launches++;
+        // prep_seconds / prep_launches time the full light-prep kernel (k_prep_pk2) launches only
+        bool timed = false;
+        if (o->mode != MCPT_MODE_BRDF) {
+            if (pc.use) {  // children: full prep; roots: pick from the root-point cache
+                const int nc = (int)n_children, nr = ni - nc;
+                if (nc > 0) {
+                    HIP_OK(hipEventRecord(D.evp0, st));
+                    HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
+                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
+                    HIP_OK(hipEventRecord(D.evp1, st));
+                    timed = true;
+                }
+                if (nr > 0) {
+                    unsigned* w2 = nullptr;
+                    const int blocks = std::max(1, std::min((nr + 3) / 4, 8192));
+                    hipLaunchKernelGGL(k_prep_pick, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
+                                       cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats, nchunks,
+                                       w2, pc);
+                    HIP_OK(hipGetLastError());
+                }
+            } else {
+                HIP_OK(hipEventRecord(D.evp0, st));
+                HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
+                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
+                HIP_OK(hipEventRecord(D.evp1, st));
+                timed = true;
+            }
+            prep_launches += timed;
         }
         HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
-        if (o->mode == MCPT_MODE_MIS && !fused_mis) {
-            hipLaunchKernelGGL(k_mis_gen, dim3((ni + 255) / 256), dim3(256), 0, st, P, *cur, ni, aux);
+        const dim3 g256((ni + 255) / 256), b256(256);
+        if (!fused && o->mode == MCPT_MODE_MIS) {
+            hipLaunchKernelGGL(k_mis_gen, g256, b256, 0, st, P, *cur, ni, aux);
             hipLaunchKernelGGL(k_mis_rays, dim3((ni + kRayBlock - 1) / kRayBlock, 3), dim3(kRayBlock), 0, st, D.d, *cur,
-                               ni, aux);
-            hipLaunchKernelGGL(k_mis_combine, dim3((ni + 255) / 256), dim3(256), 0, st, P, *cur, ni, aux, *nxt);
+                               ni, aux, 0);
+            hipLaunchKernelGGL(k_mis_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
+        } else if (!fused && o->mode == MCPT_MODE_SHADE) {
+            hipLaunchKernelGGL(k_shade_gen, g256, b256, 0, st, P, *cur, ni, aux);
+            hipLaunchKernelGGL(k_mis_rays, dim3((ni + kRayBlock - 1) / kRayBlock, 2), dim3(kRayBlock), 0, st, D.d, *cur,
+                               ni, aux, 0);
+            hipLaunchKernelGGL(k_shade_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
+        } else if (!fused) {
+            hipLaunchKernelGGL(k_brdf_gen, g256, b256, 0, st, P, *cur, ni, aux);
+            hipLaunchKernelGGL(k_mis_rays, dim3((ni + kRayBlock - 1) / kRayBlock, 1), dim3(kRayBlock), 0, st, D.d, *cur,
+                               ni, aux, 1);
+            hipLaunchKernelGGL(k_brdf_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else if (o->mode == MCPT_MODE_MIS)
             hipLaunchKernelGGL(k_extend_mis, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, P,
                                *cur, ni, *nxt);
@@ -1832,7 +2197,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             hipLaunchKernelGGL(k_extend_brdf, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
                                P, *cur, ni, *nxt);
         HIP_OK(hipGetLastError());
-        if (prep) {
+        if (timed) {
             float ms = 0;
             HIP_OK(hipEventSynchronize(D.evp1));
             HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
@@ -1855,7 +2220,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->generations = gens;
         stats->shading_nodes = nodes_total;
 
-        stats->light_evals_total = (uint64_t)nodes_total * (o->mode != MCPT_MODE_BRDF ? (uint64_t)D.d.NL : 0ull);
+        // variant 8 counts its full-prep nodes (hs[7]) and cached roots (hs[0]); the older variants
+        // run every node in full
+        const uint64_t full = hs[7] ? hs[7] : (o->mode != MCPT_MODE_BRDF ? nodes_total : 0);
+        stats->prep_full_nodes = full;
+        stats->prep_cached_nodes = hs[0];
+        stats->light_evals_total = full * (uint64_t)D.d.NL;
         stats->light_evals_culled_backface = hs[6];
         stats->light_evals_candidates = hs[5];
         stats->light_evals_culled_plane = stats->light_evals_total - hs[5] - hs[6];

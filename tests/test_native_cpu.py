@@ -17,7 +17,7 @@ def test_library_exports_every_declared_symbol():
     L = mcpt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.mcpt_version() == 10000
+    assert L.mcpt_version() == 10100
 
 
 @pytest.fixture(scope="module")
