@@ -92,6 +92,7 @@ typedef struct {
     uint64_t light_evals_candidates;      /* passed both; evaluated in full (Mylight.cpp:360-413) */
     uint64_t prep_full_nodes;   /* prep nodes that ran the O(N_L) stages (incl. root-cache builds) */
     uint64_t prep_cached_nodes; /* root nodes served by the per-pixel root-point cache (pick only) */
+    uint64_t prep_cache_points; /* root points whose prep built the cache (included in prep_full_nodes) */
 } mcpt_stats;
 
 int mcpt_version(void);

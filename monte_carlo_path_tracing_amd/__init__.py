@@ -58,7 +58,7 @@ class Stats(C.Structure):
                 ("generations", C.c_uint64), ("prep_seconds", C.c_double), ("prep_launches", C.c_uint64),
                 ("light_evals_total", C.c_uint64), ("light_evals_culled_backface", C.c_uint64),
                 ("light_evals_culled_plane", C.c_uint64), ("light_evals_candidates", C.c_uint64),
-                ("prep_full_nodes", C.c_uint64), ("prep_cached_nodes", C.c_uint64)]
+                ("prep_full_nodes", C.c_uint64), ("prep_cached_nodes", C.c_uint64), ("prep_cache_points", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -2225,6 +2225,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const uint64_t full = hs[7] ? hs[7] : (o->mode != MCPT_MODE_BRDF ? nodes_total : 0);
         stats->prep_full_nodes = full;
         stats->prep_cached_nodes = hs[0];
+        stats->prep_cache_points = cache_points;
         stats->light_evals_total = full * (uint64_t)D.d.NL;
         stats->light_evals_culled_backface = hs[6];
         stats->light_evals_candidates = hs[5];
