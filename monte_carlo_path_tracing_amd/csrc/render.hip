@@ -100,6 +100,8 @@ __device__ inline d3 cam_dir(const CamFrame& f, int i, int j) {  // main.cpp:563
 // triangle test on every candidate.  Stack in LDS, [depth][thread] layout (conflict-free).
 // ============================================================================================
 constexpr int kStack = 48;
+constexpr int kRayBlock = 256;
+constexpr int kRayLds = 16;  // LDS stack entries per lane of trace_s / trace_ww (16 KB per 256 lanes)
 constexpr int kTraceBlock = 128;
 
 struct Hit {
@@ -268,6 +270,99 @@ __device__ inline Hit trace_s(const BvhNode* __restrict__ nodes, const float4* _
     return best;
 }
 
+// trace_s reorganised as Aila & Laine's "while-while" loop: a lane descends through internal nodes
+// until it holds a leaf (postponed), and the wave tests triangles only once every active lane has
+// one (or ran out of nodes), so the fp64 triangle tests run with few idle lanes.  Leaves travel on
+// the stack as ~((first << 3) | count); arithmetic and results are trace_s's.
+template <int kLds>
+__device__ inline Hit trace_ww(const BvhNode* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
+                               int exclude, int* __restrict__ lds, int stride) {
+    constexpr int kDone = 0x7fffffff;  // popped from an empty stack
+    Hit best{-1, DBL_MAX, 0, 0};
+    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
+    int spill[kStack - kLds];
+    auto inv = [](double d) {
+        float f = (float)d;
+        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
+        return 1.0f / f;
+    };
+    const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
+    const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
+    float tlimit = FLT_MAX;
+    int sp = 0;
+    auto push = [&](int v) {
+        if (sp < kLds) lds[sp * stride] = v;
+        else if (sp < kStack) spill[sp - kLds] = v;
+        sp = sp < kStack ? sp + 1 : sp;
+    };
+    auto pop = [&]() -> int {
+        if (sp == 0) return kDone;
+        --sp;
+        return sp < kLds ? lds[sp * stride] : spill[sp - kLds];
+    };
+    int node = 0;   // >= 0 internal node (or kDone), < 0 packed leaf
+    int leaf = 0;   // < 0: a postponed leaf
+    while (node != kDone || leaf < 0) {
+        while (node >= 0 && node != kDone) {
+            const BvhNode nd = nodes[node];
+            float tn[2];
+            bool hc[2];
+            int code[2];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float tx0 = fmaf(nd.lo[k][0], ix, -oix), tx1 = fmaf(nd.hi[k][0], ix, -oix);
+                const float ty0 = fmaf(nd.lo[k][1], iy, -oiy), ty1 = fmaf(nd.hi[k][1], iy, -oiy);
+                const float tz0 = fmaf(nd.lo[k][2], iz, -oiz), tz1 = fmaf(nd.hi[k][2], iz, -oiz);
+                const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+                hc[k] = t0 <= t1 * 1.00001f + 1e-6f;
+                tn[k] = t0;
+                const int c = nd.child[k];
+                code[k] = c >= 0 ? c : ~(((~c) << 3) | nd.count[k]);
+            }
+            if (!hc[0] && !hc[1]) {
+                node = pop();
+            } else {
+                const bool first0 = hc[0] && (!hc[1] || tn[0] <= tn[1]);
+                node = first0 ? code[0] : code[1];
+                if (hc[0] && hc[1]) push(first0 ? code[1] : code[0]);
+            }
+            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                leaf = node;
+                node = pop();
+            }
+            if (!__any(leaf >= 0)) break;  // every lane holds a leaf
+        }
+        while (leaf < 0) {
+            const int packed = ~leaf, first = packed >> 3, cnt = packed & 7;
+            for (int q = first; q < first + cnt; q++) {
+                const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
+                const int fac = __float_as_int(a4.w);
+                if (fac == exclude) continue;
+                const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
+                const double detA = det3(ab, ac, rd);
+                if (fabs(detA) < MCPT_EPS) continue;
+                const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
+                const bool neg = detA < 0;
+                if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
+                    continue;
+                const double beta = nb / detA, gamma = ng / detA, t = nt / detA;
+                if (beta < 0 || gamma < 0 || beta + gamma > 1 || t < 0 || fabs(t) < MCPT_EPS) continue;
+                if (t < best.t || (t == best.t && fac < best.f)) {
+                    best.f = fac;
+                    best.t = t;
+                    best.beta = beta;
+                    best.gamma = gamma;
+                    tlimit = (float)t * 1.0001f + 1e-5f;
+                }
+            }
+            leaf = node;
+            if (node < 0) node = pop();
+        }
+    }
+    return best;
+}
+
 // ============================================================================================
 // wavefront queue (SoA)
 // ============================================================================================
@@ -381,13 +476,13 @@ __device__ inline void node_entry(const Params& P, bool active, int f, double be
 // kernels
 // ============================================================================================
 __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam, int* hit_f, double* hit_tbg) {
-    __shared__ int stack[kStack * kTraceBlock];
+    __shared__ int stack[kRayLds * kTraceBlock];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int npx = cam.W * cam.H;
     if (idx >= npx) return;
     const int i = idx / cam.W, j = idx % cam.W;
     const d3 dir = cam_dir(cam, i, j);
-    Hit h = trace(S.bvh, S.leaf_v, cam.eye, dir, -1, stack + threadIdx.x, kTraceBlock);
+    Hit h = trace_ww<kRayLds>(S.bvh, S.leaf_v, cam.eye, dir, -1, stack + threadIdx.x, kTraceBlock);
     hit_f[idx] = h.f;
     hit_tbg[3 * idx] = h.f >= 0 ? h.t : 0.0;
     hit_tbg[3 * idx + 1] = h.f >= 0 ? h.beta : 0.0;
@@ -1367,8 +1462,6 @@ struct Aux {
     int *flags, *hf;
     int cap;
 };
-constexpr int kRayBlock = 256;
-constexpr int kRayLds = 16;  // LDS stack entries per lane (16 KB per 256-lane block)
 
 __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux A) {
     const DScene& S = P.S;
@@ -1427,6 +1520,7 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 
 // closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
 // queue's shading points, excluding the origin facet
+template <bool kWhileWhile>
 __global__ __launch_bounds__(kRayBlock) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set) {
     __shared__ int stack[kRayLds * kRayBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1439,8 +1533,10 @@ __global__ __launch_bounds__(kRayBlock) void k_mis_rays(DScene S, Queue cur, int
         const double* d = set == 0 ? A.d1 : A.d2;
         const d3 ro = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
         const d3 rd = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-        const Hit h = set == 2 ? trace_s<kRayLds>(S.lbvh, S.lleaf_v, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock)
-                               : trace_s<kRayLds>(S.bvh, S.leaf_v, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
+        const BvhNode* nodes = set == 2 ? S.lbvh : S.bvh;  // uniform per block
+        const float4* leafv = set == 2 ? S.lleaf_v : S.leaf_v;
+        const Hit h = kWhileWhile ? trace_ww<kRayLds>(nodes, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock)
+                                  : trace_s<kRayLds>(nodes, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
@@ -1698,7 +1794,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_shade(Params P, Queue cu
 
 // one BRDF-only path vertex (main.cpp:385-396)
 __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
-    __shared__ int stack[kStack * kTraceBlock];
+    __shared__ int stack[kRayLds * kTraceBlock];
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
@@ -1721,7 +1817,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
         wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
         if (!(dot(wi, N) < 0)) {
             atomicAdd(P.stats + 2, 1ull);
-            h = trace(S.bvh, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock);
+            h = trace_ww<kRayLds>(S.bvh, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock);
             if (h.f >= 0) {
                 const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
                 tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
@@ -1736,10 +1832,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
 __global__ __launch_bounds__(kTraceBlock) void k_trace_batch(DScene S, int n, const double* ro, const double* rd,
                                                              const int* ex, int light_only, int* f_out,
                                                              double* tbg) {
-    __shared__ int stack[kStack * kTraceBlock];
+    __shared__ int stack[kRayLds * kTraceBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Hit h = trace(light_only ? S.lbvh : S.bvh, light_only ? S.lleaf_v : S.leaf_v, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]),
+    Hit h = trace_ww<kRayLds>(light_only ? S.lbvh : S.bvh, light_only ? S.lleaf_v : S.leaf_v, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]),
                   mk3(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]), ex[i], stack + threadIdx.x, kTraceBlock);
     f_out[i] = h.f;
     tbg[3 * i] = h.f >= 0 ? h.t : 0.0;
@@ -2043,6 +2139,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // extension kernels: MIS and shade split into gen / rays / combine (measured faster), BRDF-only
     // keeps the single kernel (one ray per node; measured faster).  A/B switches:
     static const bool fused_env = getenv("MCPT_FUSED_EXTEND") != nullptr;
+    static const bool ifif = getenv("MCPT_TRACE_IFIF") != nullptr;  // A/B: trace_s instead of trace_ww
+#define K_MIS_RAYS (ifif ? k_mis_rays<false> : k_mis_rays<true>)
     static const bool split_brdf = getenv("MCPT_SPLIT_BRDF") != nullptr;
     const bool fused = fused_env || (o->mode == MCPT_MODE_BRDF && !split_brdf);
     Aux aux{};
@@ -2174,17 +2272,17 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const dim3 g256((ni + 255) / 256), b256(256);
         if (!fused && o->mode == MCPT_MODE_MIS) {
             hipLaunchKernelGGL(k_mis_gen, g256, b256, 0, st, P, *cur, ni, aux);
-            hipLaunchKernelGGL(k_mis_rays, dim3((ni + kRayBlock - 1) / kRayBlock, 3), dim3(kRayBlock), 0, st, D.d, *cur,
+            hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 3), dim3(kRayBlock), 0, st, D.d, *cur,
                                ni, aux, 0);
             hipLaunchKernelGGL(k_mis_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else if (!fused && o->mode == MCPT_MODE_SHADE) {
             hipLaunchKernelGGL(k_shade_gen, g256, b256, 0, st, P, *cur, ni, aux);
-            hipLaunchKernelGGL(k_mis_rays, dim3((ni + kRayBlock - 1) / kRayBlock, 2), dim3(kRayBlock), 0, st, D.d, *cur,
+            hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 2), dim3(kRayBlock), 0, st, D.d, *cur,
                                ni, aux, 0);
             hipLaunchKernelGGL(k_shade_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else if (!fused) {
             hipLaunchKernelGGL(k_brdf_gen, g256, b256, 0, st, P, *cur, ni, aux);
-            hipLaunchKernelGGL(k_mis_rays, dim3((ni + kRayBlock - 1) / kRayBlock, 1), dim3(kRayBlock), 0, st, D.d, *cur,
+            hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 1), dim3(kRayBlock), 0, st, D.d, *cur,
                                ni, aux, 1);
             hipLaunchKernelGGL(k_brdf_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else if (o->mode == MCPT_MODE_MIS)
