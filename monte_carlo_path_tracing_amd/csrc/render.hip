@@ -406,6 +406,14 @@ __device__ inline int wave_append(unsigned* counter, bool want) {
     return want ? (int)(base + __popcll(below)) : -1;
 }
 
+// wave-aggregated statistics counter: adds the sum of v (0..3) over the calling lanes with ONE
+// atomic (a per-lane atomic on a shared counter serialises at wavefront node rates).  Must be
+// called by every lane of the wave that may contribute.
+__device__ inline void wave_count(unsigned long long* counter, unsigned v) {
+    const unsigned long long n = (unsigned long long)__popcll(__ballot(v & 1)) + 2ull * __popcll(__ballot(v & 2));
+    if (n && lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) atomicAdd(counter, n);
+}
+
 // shading point and normal of a hit (main.cpp:406-407: interpolated position, normalised
 // interpolation of the vertex normals)
 __device__ inline void node_point(const DScene& S, int f, double beta, double gamma, d3* p, d3* N) {
@@ -1442,8 +1450,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur,
     node_entry(P, c1, h1.f, h1.beta, h1.gamma, mul(wl, -1), tp1, pixel, sample, 2 * node, nxt);
     node_entry(P, c2, h2.f, h2.beta, h2.gamma, mul(wi, -1), tp2, pixel, sample, 2 * node + 1, nxt);
     if (active) {
-        atomicAdd(P.stats + 2, (unsigned long long)nrays);
-        atomicAdd(P.stats + 3, (unsigned long long)nlrays);
+        wave_count(P.stats + 2, nrays);
+        wave_count(P.stats + 3, nlrays);
     }
 }
 
@@ -1582,8 +1590,8 @@ __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n,
     node_entry(P, c2, c2 ? A.hf[o2] : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), tp2, pixel, sample, 2 * node + 1, nxt);
     if (active) {
         const unsigned nr = (fl & 1) + ((fl >> 1) & 1);
-        atomicAdd(P.stats + 2, (unsigned long long)nr);
-        if (c2) atomicAdd(P.stats + 3, 1ull);
+        wave_count(P.stats + 2, nr);
+        wave_count(P.stats + 3, c2 ? 1u : 0u);
     }
 }
 
@@ -1668,7 +1676,7 @@ __global__ __launch_bounds__(256) void k_shade_combine(Params P, Queue cur, int 
     const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
-    if (active) atomicAdd(P.stats + 2, (unsigned long long)((fl & 1) + ((fl >> 1) & 1)));
+    wave_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u);
 }
 
 // shade_with_brdf (main.cpp:385-396): gen samples the bounce, combine spawns the child on any hit
@@ -1708,7 +1716,7 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
     const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
-    if (active && (fl & 2)) atomicAdd(P.stats + 2, 1ull);
+    wave_count(P.stats + 2, (active && (fl & 2)) ? 1u : 0u);
 }
 
 // one shade() node (main.cpp:295-343), lane per node: the direct-light estimate is splatted into
@@ -1789,7 +1797,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_shade(Params P, Queue cu
         }
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
-    if (active) atomicAdd(P.stats + 2, (unsigned long long)nrays);
+    wave_count(P.stats + 2, active ? nrays : 0u);
 }
 
 // one BRDF-only path vertex (main.cpp:385-396)
@@ -1806,6 +1814,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
     const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
     const uint64_t node = cur.node[ii];
     bool c = false;
+    unsigned traced = 0;
     Hit h{-1, 0, 0, 0};
     d3 wi = mk3(0, 0, 0), tpc = mk3(0, 0, 0);
     if (active) {
@@ -1816,7 +1825,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
         double pdf;
         wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
         if (!(dot(wi, N) < 0)) {
-            atomicAdd(P.stats + 2, 1ull);
+            traced = 1;
             h = trace_ww<kRayLds>(S.bvh, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock);
             if (h.f >= 0) {
                 const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
@@ -1826,6 +1835,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
         }
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
+    wave_count(P.stats + 2, traced);
 }
 
 // batch closest hit (test / FFI entry mcpt_closest_hit)
