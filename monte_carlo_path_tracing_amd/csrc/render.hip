@@ -544,6 +544,88 @@ __global__ __launch_bounds__(256) void k_root_points(DScene S, CamFrame cam, con
     }
 }
 
+// Light prep for scenes with few light triangles (N_L <= kSmallNL, e.g. the 2-triangle Cornell
+// light): lane per node, a sequential loop over the light table in index order -- exactly the
+// oracle's loop (exact fp64 cheap stages, light_weight_bf for the full stage), the sum in index
+// order and the pick "first survivor whose running sum >= u * weights_sum" (last survivor on
+// rounding).  A wave per node would leave 62 of 64 lanes idle here.
+constexpr int kSmallNL = 64;
+__device__ inline unsigned long long wave_sum_u64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
+                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                                   const double* __restrict__ u_override, double* __restrict__ wsum_out,
+                                                   int* __restrict__ pick_out, int* __restrict__ count_out,
+                                                   unsigned long long* stats) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    unsigned long long surv = 0, cand = 0, c1 = 0;
+    if (active) {
+        const d3 x1 = mk3(qp[3 * i], qp[3 * i + 1], qp[3 * i + 2]);
+        const d3 nn = mk3(qn[3 * i], qn[3 * i + 1], qn[3 * i + 2]);
+        auto eval = [&](int li, bool* ok) -> double {
+            const double2* w = S.lt_w + 5 * li;
+            const double2 a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+            const d3 p0 = mk3(a.x, a.y, b.x), p1 = mk3(b.y, c.x, c.y), p2 = mk3(d.x, d.y, e.x);
+            const double4 ln = S.lt_n[li];
+            const int st = light_cheap_stage(p0, p1, p2, mk3(ln.x, ln.y, ln.z), x1, nn);
+            if (st != 0) {
+                *ok = false;
+                return st;  // 1 or 2: the culling stage
+            }
+            return light_weight_bf(p0, p1, p2, e.y, x1, ok);
+        };
+        double wsum = 0;
+        for (int li = 0; li < S.NL; li++) {
+            bool ok;
+            const double r = eval(li, &ok);
+            if (ok) {
+                wsum += r;
+                surv++;
+            }
+            const bool culled = !ok && (r == 1.0 || r == 2.0);
+            c1 += culled && r == 1.0;
+            cand += !culled;
+        }
+        int pick = -1;
+        if (!(fabs(wsum) < MCPT_EPS)) {
+            const double u = u_override ? u_override[i]
+                                        : counter_u(counter_key(seed, (uint64_t)qpixel[i], (uint64_t)qsample[i], qnode[i]), 1);
+            const double target = u * wsum;
+            double cum = 0;
+            int last = -1;
+            for (int li = 0; li < S.NL; li++) {
+                bool ok;
+                const double r = eval(li, &ok);
+                if (!ok) continue;
+                cum += r;
+                last = li;
+                if (cum >= target) {
+                    pick = li;
+                    break;
+                }
+            }
+            if (pick < 0) pick = last;
+        }
+        wsum_out[i] = wsum;
+        pick_out[i] = pick;
+        if (count_out) count_out[i] = (int)surv;
+    }
+    if (stats) {
+        const unsigned long long ss = wave_sum_u64(surv), cs = wave_sum_u64(cand), c1s = wave_sum_u64(c1);
+        const unsigned long long full = __popcll(__ballot(active));
+        if (lane_id() == 0) {
+            if (ss) atomicAdd(stats + 1, ss);
+            if (cs) atomicAdd(stats + 5, cs);
+            if (c1s) atomicAdd(stats + 6, c1s);
+            if (full) atomicAdd(stats + 7, full);
+        }
+    }
+}
+
 // Light prep, one wave per node (Mylight.cpp:322-422).
 //  pass 1: chunks of 64 light triangles run the cheap cull stages (light side, tangent plane);
 //          candidates are compacted into a per-wave LDS queue, and every 64 queued candidates are
@@ -2074,7 +2156,12 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = list_ok ? 8 : 0;  // A/B on MI355X: tools/prep_variants.py
+    if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? 8 : 0;  // A/B on MI355X: tools/prep_variants.py
+    if (variant == 9) {
+        hipLaunchKernelGGL(k_prep_lane, dim3((n + 255) / 256), dim3(256), 0, st, d, seed, n, qp, qn, qpixel, qsample, qnode,
+                           u, wsum, pick, count, stats);
+        return hipGetLastError();
+    }
     if (variant > 0 && !list_ok) variant = 0;
     if (cache.build && variant != 8) return hipErrorInvalidValue;  // the cache is built by variant 8
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
@@ -2182,7 +2269,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int lstride = 64 * nchunks;
     const size_t cache_bytes = (size_t)npx * ((size_t)nchunks * 8 + (size_t)lstride * 10 + 16);
     static const bool no_cache = getenv("MCPT_NO_ROOT_CACHE") != nullptr;  // A/B switch
-    if (o->mode != MCPT_MODE_BRDF && s1 - s0 >= 2 && cache_bytes <= (64ull << 30) && !no_cache &&
+    if (o->mode != MCPT_MODE_BRDF && s1 - s0 >= 2 && cache_bytes <= (64ull << 30) && !no_cache && D.d.NL > kSmallNL &&
         prep_list_wave_bytes(nchunks) * 4 <= kPrepListMaxLds && D.d.NL <= 65535) {
         if ((rc = ensure(D.cache_bt, (size_t)npx * nchunks * 8)) || (rc = ensure(D.cache_lst, (size_t)npx * lstride * 2)) ||
             (rc = ensure(D.cache_info, (size_t)npx * 16)) || (rc = ensure(D.cache_w, (size_t)npx * lstride * 8)))
