@@ -1611,7 +1611,7 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 // closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
 // queue's shading points, excluding the origin facet
 template <bool kWhileWhile>
-__global__ __launch_bounds__(kRayBlock) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set) {
+__global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set) {
     __shared__ int stack[kRayLds * kRayBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int set = blockIdx.y + first_set;
