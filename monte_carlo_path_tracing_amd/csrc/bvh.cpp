@@ -222,4 +222,69 @@ Bvh build_bvh(const HostScene& s, const std::vector<int32_t>& facets, int max_le
     return bvh;
 }
 
+namespace {
+double box_area(const float* lo, const float* hi) {
+    if (lo[0] > hi[0]) return 0;
+    const double d[3] = {(double)hi[0] - lo[0], (double)hi[1] - lo[1], (double)hi[2] - lo[2]};
+    return 2 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+}
+struct Cand {
+    int32_t child, count;
+    float lo[3], hi[3];
+};
+int32_t collapse(const Bvh& b, int32_t n2, std::vector<BvhNode4>& out) {
+    const int32_t me = static_cast<int32_t>(out.size());
+    out.push_back(BvhNode4{});
+    std::vector<Cand> cs;
+    auto add_children = [&](int32_t node) {
+        const BvhNode& nd = b.nodes[node];
+        for (int k = 0; k < 2; k++) {
+            if (nd.child[k] < 0 && nd.count[k] == 0) continue;  // empty slot (single-leaf root)
+            Cand c;
+            c.child = nd.child[k];
+            c.count = nd.count[k];
+            for (int a = 0; a < 3; a++) {
+                c.lo[a] = nd.lo[k][a];
+                c.hi[a] = nd.hi[k][a];
+            }
+            cs.push_back(c);
+        }
+    };
+    add_children(n2);
+    while (cs.size() < 4) {
+        int best = -1;
+        double ba = -1;
+        for (size_t i = 0; i < cs.size(); i++)
+            if (cs[i].child >= 0 && box_area(cs[i].lo, cs[i].hi) > ba) {
+                ba = box_area(cs[i].lo, cs[i].hi);
+                best = static_cast<int>(i);
+            }
+        if (best < 0) break;
+        const int32_t inner = cs[best].child;
+        cs.erase(cs.begin() + best);
+        add_children(inner);
+    }
+    int32_t child[4];
+    for (size_t k = 0; k < 4; k++) child[k] = kBvh4Empty;
+    for (size_t k = 0; k < cs.size(); k++) child[k] = cs[k].child >= 0 ? collapse(b, cs[k].child, out) : cs[k].child;
+    BvhNode4& o = out[me];
+    for (int k = 0; k < 4; k++) {
+        const bool used = k < static_cast<int>(cs.size());
+        for (int a = 0; a < 3; a++) {
+            o.lo[a][k] = used ? cs[k].lo[a] : FLT_MAX;
+            o.hi[a][k] = used ? cs[k].hi[a] : -FLT_MAX;
+        }
+        o.child[k] = child[k];
+        o.count[k] = used ? cs[k].count : 0;
+    }
+    return me;
+}
+}  // namespace
+
+std::vector<BvhNode4> collapse_bvh4(const Bvh& b) {
+    std::vector<BvhNode4> out;
+    if (!b.nodes.empty()) collapse(b, 0, out);
+    return out;
+}
+
 }  // namespace mcpt

@@ -49,6 +49,20 @@ struct Bvh {
 };
 Bvh build_bvh(const HostScene& s, const std::vector<int32_t>& facets, int max_leaf);
 
+// 4-wide node (128 B, two cache lines): the four children's boxes as per-axis float4s, so a
+// node visit is 8 dwordx4 loads and four independent slab tests.  Children as in BvhNode;
+// unused slots hold kBvh4Empty.
+constexpr int32_t kBvh4Empty = 0x7fffffff;
+struct BvhNode4 {
+    float lo[3][4];    // lo[axis][child]
+    float hi[3][4];
+    int32_t child[4];  // >= 0: inner node; < 0: leaf ~first slot; kBvh4Empty: no child
+    int32_t count[4];
+};
+// collapses a binary BVH into a 4-wide one (greedy: expand the largest-area inner child until
+// four children); leaves and leaf slots are shared with the binary tree
+std::vector<BvhNode4> collapse_bvh4(const Bvh& b);
+
 void set_error(const char* fmt, ...);
 
 }  // namespace mcpt

@@ -55,6 +55,8 @@ struct DScene {
     const BvhNode* bvh;       // all facets
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
     const BvhNode* lbvh;      // light facets only
+    const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves)
+    const BvhNode4* lbvh4;
     const float4* lleaf_v;
 };
 
@@ -363,6 +365,110 @@ __device__ inline Hit trace_ww(const BvhNode* __restrict__ nodes, const float4* 
     return best;
 }
 
+// trace_ww over the 4-wide tree: four slab tests per node visit, hits ordered near-to-far with
+// a 5-comparator network, the nearest followed and the rest pushed far-first.  Same candidate
+// set semantics (every triangle in a hit leaf gets the exact fp64 test), so results equal trace_s.
+template <int kLds>
+__device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
+                                int exclude, int* __restrict__ lds, int stride) {
+    constexpr int kDone = 0x7fffffff;
+    Hit best{-1, DBL_MAX, 0, 0};
+    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
+    int spill[kStack - kLds];
+    auto inv = [](double d) {
+        float f = (float)d;
+        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
+        return 1.0f / f;
+    };
+    const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
+    const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
+    float tlimit = FLT_MAX;
+    int sp = 0;
+    auto push = [&](int v) {
+        if (sp < kLds) lds[sp * stride] = v;
+        else if (sp < kStack) spill[sp - kLds] = v;
+        sp = sp < kStack ? sp + 1 : sp;
+    };
+    auto pop = [&]() -> int {
+        if (sp == 0) return kDone;
+        --sp;
+        return sp < kLds ? lds[sp * stride] : spill[sp - kLds];
+    };
+    int node = 0;
+    int leaf = 0;
+    while (node != kDone || leaf < 0) {
+        while (node >= 0 && node != kDone) {
+            const BvhNode4* nd = nodes + node;
+            const float4 lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
+                         lz = *reinterpret_cast<const float4*>(nd->lo[2]);
+            const float4 hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
+                         hz = *reinterpret_cast<const float4*>(nd->hi[2]);
+            const int4 ch = *reinterpret_cast<const int4*>(nd->child), cn = *reinterpret_cast<const int4*>(nd->count);
+            const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, lys[4] = {ly.x, ly.y, ly.z, ly.w}, lzs[4] = {lz.x, lz.y, lz.z, lz.w};
+            const float hxs[4] = {hx.x, hx.y, hx.z, hx.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
+            const int chs[4] = {ch.x, ch.y, ch.z, ch.w}, cns[4] = {cn.x, cn.y, cn.z, cn.w};
+            float t[4];
+            int code[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float tx0 = fmaf(lxs[k], ix, -oix), tx1 = fmaf(hxs[k], ix, -oix);
+                const float ty0 = fmaf(lys[k], iy, -oiy), ty1 = fmaf(hys[k], iy, -oiy);
+                const float tz0 = fmaf(lzs[k], iz, -oiz), tz1 = fmaf(hzs[k], iz, -oiz);
+                const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+                const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
+                t[k] = h ? t0 : FLT_MAX;
+                code[k] = !h ? kDone : chs[k] >= 0 ? chs[k] : ~(((~chs[k]) << 3) | cns[k]);
+            }
+            // sort (t, code) ascending; misses (FLT_MAX, kDone) sink to the end
+            auto cs = [&](int a, int b) {
+                const bool sw = t[b] < t[a];
+                const float ta = t[a], tb = t[b];
+                const int ca = code[a], cb = code[b];
+                t[a] = sw ? tb : ta, t[b] = sw ? ta : tb;
+                code[a] = sw ? cb : ca, code[b] = sw ? ca : cb;
+            };
+            cs(0, 1), cs(2, 3), cs(0, 2), cs(1, 3), cs(1, 2);
+            if (code[3] != kDone) push(code[3]);
+            if (code[2] != kDone) push(code[2]);
+            if (code[1] != kDone) push(code[1]);
+            node = code[0] != kDone ? code[0] : pop();
+            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                leaf = node;
+                node = pop();
+            }
+            if (!__any(leaf >= 0)) break;
+        }
+        while (leaf < 0) {
+            const int packed = ~leaf, first = packed >> 3, cnt = packed & 7;
+            for (int q = first; q < first + cnt; q++) {
+                const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
+                const int fac = __float_as_int(a4.w);
+                if (fac == exclude) continue;
+                const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
+                const double detA = det3(ab, ac, rd);
+                if (fabs(detA) < MCPT_EPS) continue;
+                const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
+                const bool neg = detA < 0;
+                if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
+                    continue;
+                const double beta = nb / detA, gamma = ng / detA, tt = nt / detA;
+                if (beta < 0 || gamma < 0 || beta + gamma > 1 || tt < 0 || fabs(tt) < MCPT_EPS) continue;
+                if (tt < best.t || (tt == best.t && fac < best.f)) {
+                    best.f = fac;
+                    best.t = tt;
+                    best.beta = beta;
+                    best.gamma = gamma;
+                    tlimit = (float)tt * 1.0001f + 1e-5f;
+                }
+            }
+            leaf = node;
+            if (node < 0) node = pop();
+        }
+    }
+    return best;
+}
+
 // ============================================================================================
 // wavefront queue (SoA)
 // ============================================================================================
@@ -490,7 +596,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
     if (idx >= npx) return;
     const int i = idx / cam.W, j = idx % cam.W;
     const d3 dir = cam_dir(cam, i, j);
-    Hit h = trace_ww<kRayLds>(S.bvh, S.leaf_v, cam.eye, dir, -1, stack + threadIdx.x, kTraceBlock);
+    Hit h = trace4_ww<kRayLds>(S.bvh4, S.leaf_v, cam.eye, dir, -1, stack + threadIdx.x, kTraceBlock);
     hit_f[idx] = h.f;
     hit_tbg[3 * idx] = h.f >= 0 ? h.t : 0.0;
     hit_tbg[3 * idx + 1] = h.f >= 0 ? h.beta : 0.0;
@@ -1623,10 +1729,12 @@ __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, 
         const double* d = set == 0 ? A.d1 : A.d2;
         const d3 ro = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
         const d3 rd = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-        const BvhNode* nodes = set == 2 ? S.lbvh : S.bvh;  // uniform per block
-        const float4* leafv = set == 2 ? S.lleaf_v : S.leaf_v;
-        const Hit h = kWhileWhile ? trace_ww<kRayLds>(nodes, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock)
-                                  : trace_s<kRayLds>(nodes, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
+        const float4* leafv = set == 2 ? S.lleaf_v : S.leaf_v;  // uniform per block
+        Hit h;
+        if (kWhileWhile)
+            h = trace4_ww<kRayLds>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
+        else
+            h = trace_ww<kRayLds>(set == 2 ? S.lbvh : S.bvh, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
@@ -1908,7 +2016,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
         wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
         if (!(dot(wi, N) < 0)) {
             traced = 1;
-            h = trace_ww<kRayLds>(S.bvh, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock);
+            h = trace4_ww<kRayLds>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock);
             if (h.f >= 0) {
                 const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
                 tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
@@ -1927,7 +2035,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_batch(DScene S, int n, co
     __shared__ int stack[kRayLds * kTraceBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Hit h = trace_ww<kRayLds>(light_only ? S.lbvh : S.bvh, light_only ? S.lleaf_v : S.leaf_v, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]),
+    Hit h = trace4_ww<kRayLds>(light_only ? S.lbvh4 : S.bvh4, light_only ? S.lleaf_v : S.leaf_v, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]),
                   mk3(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]), ex[i], stack + threadIdx.x, kTraceBlock);
     f_out[i] = h.f;
     tbg[3 * i] = h.f >= 0 ? h.t : 0.0;
@@ -2080,6 +2188,8 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, sc->bvh.nodes, &d.bvh))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
     if ((rc = upload(*D, sc->lbvh.nodes, &d.lbvh))) return rc;
+    if ((rc = upload(*D, collapse_bvh4(sc->bvh), &d.bvh4))) return rc;
+    if ((rc = upload(*D, collapse_bvh4(sc->lbvh), &d.lbvh4))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc(&D->pinned_count, 64));
@@ -2189,6 +2299,10 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
             hipLaunchKernelGGL((k_prep_pk<4>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
                                qnode, u, wsum, pick, count, stats, nchunks, wb, work);
             break;
+        case 10:  // A/B: variant 8 at 6 waves/SIMD
+            hipLaunchKernelGGL((k_prep_pk2<6, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+                               qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
+            break;
         case 8:
             if (cache.build)
                 hipLaunchKernelGGL((k_prep_pk2<5, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
@@ -2236,7 +2350,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // extension kernels: MIS and shade split into gen / rays / combine (measured faster), BRDF-only
     // keeps the single kernel (one ray per node; measured faster).  A/B switches:
     static const bool fused_env = getenv("MCPT_FUSED_EXTEND") != nullptr;
-    static const bool ifif = getenv("MCPT_TRACE_IFIF") != nullptr;  // A/B: trace_s instead of trace_ww
+    static const bool ifif = getenv("MCPT_TRACE_BVH2") != nullptr;  // A/B: binary-tree trace_ww instead of trace4_ww
 #define K_MIS_RAYS (ifif ? k_mis_rays<false> : k_mis_rays<true>)
     static const bool split_brdf = getenv("MCPT_SPLIT_BRDF") != nullptr;
     const bool fused = fused_env || (o->mode == MCPT_MODE_BRDF && !split_brdf);
