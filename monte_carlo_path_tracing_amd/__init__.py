@@ -165,11 +165,10 @@ class Scene:
 def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor):
     o = RenderOpts()
     o.spp = int(spp)
-    o.mode = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE}.get(mode, mode) if isinstance(mode, str) else mode
-    if o.mode not in (MODE_MIS, MODE_BRDF, MODE_SHADE):
-        o.mode = -1
-    if o.mode < 0:
+    m = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE}.get(mode, -1) if isinstance(mode, str) else int(mode)
+    if m not in (MODE_MIS, MODE_BRDF, MODE_SHADE):
         raise ValueError("mode must be 'mis', 'brdf' or 'shade'")
+    o.mode = m
     o.seed = int(seed)
     if sample_range is not None:
         o.sample_begin, o.sample_end = int(sample_range[0]), int(sample_range[1])

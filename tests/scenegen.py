@@ -1,0 +1,70 @@
+"""Small synthetic scenes for the edge-case tests, written with the Veach generator's OBJ writer
+(scenes/gen_veach_mis.py): a scene without lights, a dense light panel (more than 4096 candidates
+per shading point: the sequential batch-search path) and a very finely tessellated sphere light
+(N_L > 7680: the LDS-queue prep variant, no root cache)."""
+import os
+import sys
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT / "scenes"))
+import gen_veach_mis as gv  # noqa: E402
+
+
+def _write(outdir, name, obj, mtls, lights, cam):
+    os.makedirs(outdir, exist_ok=True)
+    obj.write(os.path.join(outdir, name + ".obj"), name + ".mtl")
+    with open(os.path.join(outdir, name + ".mtl"), "w", newline="\n") as f:
+        for m, kd, ks, ns in mtls:
+            f.write("newmtl %s\nKd %.6f %.6f %.6f\nKs %.6f %.6f %.6f\nNs %.6f\n\n" % ((m,) + kd + ks + (ns,)))
+    with open(os.path.join(outdir, name + ".xml"), "w", newline="\n") as f:
+        eye, look = cam
+        f.write('<camera type="perspective" width="16" height="12" fovy="20.1143">\n'
+                '\t<eye x="%r" y="%r" z="%r"/>\n\t<lookat x="%r" y="%r" z="%r"/>\n'
+                '\t<up x="0.0" y="1.0" z="0.0"/>\n</camera>\n' % (eye + look))
+        for m, rad in lights:
+            f.write('<light mtlname="%s" radiance="%.6f,%.6f,%.6f"/>\n' % ((m,) + rad))
+    return os.path.join(outdir, name + ".obj"), os.path.join(outdir, name + ".xml")
+
+
+def _floor(obj, mtls):
+    obj.box("floor", "floor", (0.0, -0.1, 0.0), [((1.0, 0.0, 0.0), 4.0), ((0.0, 1.0, 0.0), 0.1), ((0.0, 0.0, 1.0), 4.0)])
+    obj.box("block", "glossy", (0.5, 0.4, 0.3), [((1.0, 0.0, 0.0), 0.4), ((0.0, 1.0, 0.0), 0.4), ((0.0, 0.0, 1.0), 0.4)])
+    mtls += [("floor", (0.5, 0.5, 0.5), (0.0, 0.0, 0.0), 1.0), ("glossy", (0.1, 0.1, 0.1), (0.4, 0.4, 0.4), 50.0)]
+
+
+CAM = ((0.0, 3.0, 9.0), (0.0, 0.5, 0.0))
+
+
+def no_lights(outdir):
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    return _write(outdir, "nolight", obj, mtls, [], CAM)
+
+
+def light_panel(outdir, nx=60, nz=60):
+    """a downward-facing light panel of nx x nz quads (2 nx nz triangles) above the floor"""
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    faces = []
+    n = obj.normal((0.0, -1.0, 0.0))
+    y, x0, x1, z0, z1 = 2.5, -1.5, 1.5, -1.5, 1.5
+    for i in range(nx):
+        for k in range(nz):
+            xa, xb = x0 + (x1 - x0) * i / nx, x0 + (x1 - x0) * (i + 1) / nx
+            za, zb = z0 + (z1 - z0) * k / nz, z0 + (z1 - z0) * (k + 1) / nz
+            a, b = obj.vert((xa, y, za)), obj.vert((xb, y, za))
+            c, d = obj.vert((xb, y, zb)), obj.vert((xa, y, zb))
+            faces.append(((a, n), (b, n), (c, n)))  # (b-a) x (c-a) = -y: faces the floor
+            faces.append(((a, n), (c, n), (d, n)))
+    obj.groups.append(("panel", "panel", faces))
+    mtls.append(("panel", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0))
+    return _write(outdir, "panel", obj, mtls, [("panel", (2.0, 2.0, 2.0))], CAM)
+
+
+def dense_sphere(outdir, nseg=120, nring=60):
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    obj.sphere("bulb", "bulb", (-0.8, 1.6, 0.0), 0.5, nseg, nring)
+    mtls.append(("bulb", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0))
+    return _write(outdir, "bulb", obj, mtls, [("bulb", (20.0, 18.0, 15.0))], CAM)
