@@ -133,12 +133,16 @@ int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const doubl
  * -1 if empty or weights_sum < 1e-8). */
 int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                     double* weights_sum, int32_t* count, int32_t* pick);
-/* diagnostics: run the light-prep kernel variant `variant` (-1 auto = 8; 0 LDS candidate queue,
- * 1 stored LDS candidate list, 2 list + software prefetch, 3 list at 5 waves/SIMD, 4 list at 6
- * waves/SIMD, 5 list + prefetch at 5 waves/SIMD, 6 packed-fp32 cheap stages + branch-free fp64
- * batches at 5 waves/SIMD, 7 the same at 4 waves/SIMD, 8 variant 6 with buffer-descriptor loads
- * and a lane-parallel batch search) `iters` times on the n points and report the mean device time
- * per launch; outputs as mcpt_light_prep (pick = facet). */
+/* diagnostics: run the light-prep kernel variant `variant` `iters` times on the n points and report
+ * the mean device time per launch; outputs as mcpt_light_prep (pick = facet).  Variants: -1 auto
+ * (9 if N_L <= 64, else 14, else 0 when the candidate list does not fit in LDS); 0 LDS candidate
+ * queue; 1 stored LDS candidate list; 2 list + software prefetch; 3 list at 5 waves/SIMD; 4 list
+ * at 6 waves/SIMD; 5 list + prefetch at 5 waves/SIMD; 6 packed-fp32 cheap stages + branch-free fp64
+ * batches; 7 the same at 4 waves/SIMD; 8 variant 6 with buffer-descriptor loads and a lane-parallel
+ * batch search; 9 lane per node (small light sets); 10 variant 8 at 6 waves/SIMD; 13 variant 8
+ * with every table load pinned to chunk 0 (timing diagnostic only, results meaningless); 14 phase A
+ * split off (k_prep_cull, 4 nodes per table pass) + variant 8's phase B; 15 / 16 the same with 2 /
+ * 8 nodes per table pass. */
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 /* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */

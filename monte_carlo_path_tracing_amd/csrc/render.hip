@@ -1151,6 +1151,25 @@ __device__ inline int prep_stage_pk_bf(const DScene& S, int li, float4 X, float4
     }
     return stage;
 }
+// prep_stage_pk_bf with the fp64 node loaded only on the (rare) ambiguous path
+__device__ inline int prep_stage_pk_bf_lazy(const DScene& S, int li, float4 X, float4 Y, float4 Z, float dl, v2f nx2,
+                                            v2f ny2, v2f nz2, v2f nxs, v2f nys, v2f nzs, float cn, const double* px1,
+                                            const double* pn, float err) {
+    constexpr float kEps = 1e-8f;
+    const v2f tab = __builtin_elementwise_fma(nx2, v2f{X.x, X.y}, __builtin_elementwise_fma(ny2, v2f{Y.x, Y.y}, nz2 * v2f{Z.x, Z.y})) - v2f{cn, cn};
+    const v2f tcs = __builtin_elementwise_fma(nxs, v2f{X.z, X.w}, __builtin_elementwise_fma(nys, v2f{Y.z, Y.w}, nzs * v2f{Z.z, Z.w})) - v2f{cn, dl};
+    const float s1 = tcs.y;
+    const float tm = fmaxf(fmaxf(tab.x, tab.y), tcs.x);
+    const float lo = kEps - err, hi = kEps + err;
+    const bool s1_out = s1 < lo, s1_in = s1 > hi, t_out = tm < lo, t_in = tm > hi;
+    int stage = li >= S.NL ? 3 : s1_out ? 1 : (s1_in && t_out) ? 2 : (s1_in && t_in) ? 0 : -1;
+    if (stage < 0) {
+        const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
+        stage = light_cheap_stage(mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(ln.x, ln.y, ln.z),
+                                  mk3(px1[0], px1[1], px1[2]), mk3(pn[0], pn[1], pn[2]));
+    }
+    return stage;
+}
 __device__ inline double prep_weight_pk(const DScene& S, int li, d3 x1, bool* ok) {
     const double2* w = S.lt_w + 5 * li;
     const double2 a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
@@ -1379,22 +1398,80 @@ __device__ inline double prep_select(const double* bt, const unsigned short* lst
     return wsum;
 }
 
-template <int kMinWavesPerSimd, bool kBuild>
+constexpr int kChunkUnroll = 2;
+constexpr int kCullNodes = 4;
+// kPinTable (diagnostic variant 13 only, results meaningless): every chunk reads chunk 0's table
+// rows, to measure how much of phase A is L2 -> CU table traffic
+// Phase A of the light prep as a kernel of its own: a wave tests every 64-light chunk against
+// kCullNodes shading nodes, so each chunk's table rows are loaded once for all of them (the L2 ->
+// CU table traffic, ~40% of the fused phase A's time, drops kCullNodes-fold), and stores per node
+// and chunk the ballot word of the candidates (bit l: light 64 c + l passed both cheap stages).
+// Node constants are wave-uniform (scalar registers).
+template <int kNodes>
+__global__ __launch_bounds__(256) void k_prep_cull(DScene S, int n, const double* __restrict__ qp, const double* __restrict__ qn,
+                                                   uint64_t* __restrict__ masks, int nchunks, unsigned long long* stats) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const int nwaves = gridDim.x * (blockDim.x >> 6);
+    const int ngroups4 = (nchunks + 3) / 4;
+    const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, ngroups4 * 4 * 3072, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, ngroups4 * 4 * 256, kBufFlags);
+    unsigned long long c1_acc = 0;
+    for (int g = wave * kNodes; g < n; g += nwaves * kNodes) {
+        NodeF nf[kNodes];
+        float cn[kNodes];
+#pragma unroll
+        for (int k = 0; k < kNodes; k++) {
+            const int node = min(g + k, n - 1);
+            const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+            const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+            nf[k] = node_f(x1, nn, S.light_bound);
+            cn[k] = (float)dot(nn, x1);
+        }
+        for (int c = 0; c < nchunks; c++) {
+            const int li = c * 64 + lane;
+            const float4 X = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48, c * 3072, 0));
+            const float4 Y = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 16, c * 3072, 0));
+            const float4 Z = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 32, c * 3072, 0));
+            const float dl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, lane * 4, c * 256, 0));
+            uint64_t mine = 0;
+#pragma unroll
+            for (int k = 0; k < kNodes; k++) {
+                const NodeF& f = nf[k];
+                const v2f nx2{f.nx, f.nx}, ny2{f.ny, f.ny}, nz2{f.nz, f.nz};
+                const v2f nxs{f.nx, f.x}, nys{f.ny, f.y}, nzs{f.nz, f.z};
+                const int node = min(g + k, n - 1);
+                // the exact fallback reloads the fp64 node (rare: a value within err of 1e-8)
+                const int stage = prep_stage_pk_bf_lazy(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn[k], qp + 3 * node,
+                                                        qn + 3 * node, f.err);
+                const uint64_t m = __ballot(stage == 0);
+                mine = lane == k ? m : mine;
+                if (g + k < n) c1_acc += __popcll(__ballot(stage == 1));
+            }
+            if (lane < kNodes && g + lane < n) masks[(size_t)(g + lane) * nchunks + c] = mine;
+        }
+    }
+    if (lane == 0 && stats && c1_acc) atomicAdd(stats + 6, c1_acc);
+}
+
+template <int kMinWavesPerSimd, bool kBuild, bool kPinTable = false, bool kMaskIn = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                   const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                   int* __restrict__ pick_out, int* __restrict__ count_out,
                                                   unsigned long long* stats, int nchunks, int wave_bytes,
-                                                  unsigned* __restrict__ work, PrepCache C) {
+                                                  unsigned* __restrict__ work, PrepCache C,
+                                                  const uint64_t* __restrict__ masks = nullptr) {
     extern __shared__ double prep_lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
     unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
-    const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, nchunks * 3072, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, nchunks * 256, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_w, 0, nchunks * 5120, kBufFlags);
+    const int ngroups4 = (nchunks + 3) / 4;
+    const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, ngroups4 * 4 * 3072, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, ngroups4 * 4 * 256, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_w, 0, ngroups4 * 4 * 5120, kBufFlags);
     unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0, full_acc = 0;
     int grab = 0, left = 0;
     while (true) {
@@ -1404,7 +1481,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             grab = __shfl((int)b, 0);
             left = kPrepGrab;
         }
-        const int node = grab++;
+        const int node = __builtin_amdgcn_readfirstlane(grab++);
         left--;
         if (node >= n) break;
         const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
@@ -1412,39 +1489,61 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             return u_override ? u_override[node]
                               : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
         };
+        int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
+        if (kMaskIn) {  // phase A done by k_prep_cull: rebuild the list from the candidate words
+            for (int c0 = 0; c0 < nchunks; c0 += 64) {  // one vector load of up to 64 words, then readlanes
+                const unsigned long long mv = c0 + lane < nchunks ? masks[(size_t)node * nchunks + c0 + lane] : 0ull;
+                const int cend = min(64, nchunks - c0);
+                for (int q = 0; q < cend; q++) {
+                    const uint64_t m = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(mv >> 32), q) << 32) |
+                                       (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mv, q);
+                    if ((m >> lane) & 1) lst[ncand + lane_rank(m)] = (unsigned short)((c0 + q) * 64 + lane);
+                    ncand += __popcll(m);
+                }
+            }
+        } else {
         const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
         const NodeF nf = node_f(x1, nn, S.light_bound);
         const float cn = (float)dot(nn, x1);
         const v2f nx2{nf.nx, nf.nx}, ny2{nf.ny, nf.ny}, nz2{nf.nz, nf.nz};
         const v2f nxs{nf.nx, nf.x}, nys{nf.ny, nf.y}, nzs{nf.nz, nf.z};
-        int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
-        for (int c = 0; c < nchunks; c++) {
-            const int li = c * 64 + lane;
-            // lane offset in VGPR (loop-invariant), chunk offset in SGPR; the tables are padded to
-            // whole chunks, so lanes past N_L read zeros
-            const float4 X = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48, c * 3072, 0));
-            const float4 Y = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 16, c * 3072, 0));
-            const float4 Z = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 32, c * 3072, 0));
-            const float dl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, lane * 4, c * 256, 0));
-            const int stage = prep_stage_pk_bf(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
-            const uint64_t m = __ballot(stage == 0);
-            if (stage == 0) lst[ncand + lane_rank(m)] = (unsigned short)li;
-            ncand += __popcll(m);
-            culled1 += __popcll(__ballot(stage == 1));
-            while (ncand - 64 * nb >= 64 || (c == nchunks - 1 && ncand > 64 * nb)) {
-                wave_lds_sync();
-                const int k = 64 * nb + lane;
-                const bool act = k < ncand;
-                bool ok;
-                double w = prep_weight_buf(rw, act ? (int)lst[k] : 0, x1, &ok);
-                ok = ok && act;
-                w = act ? w : 0.0;
-                if (kBuild && act) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
-                const double sc = wave_incl_scan(w, lane);
-                survivors += __popcll(__ballot(ok));
-                if (lane == 63) bt[nb] = sc;
-                nb++;
+        // phase A: cheap stages over all chunks, kChunkUnroll chunks' table loads in flight at a
+        // time (the loop is L2-latency-bound; the tables are padded to whole groups of 4 chunks)
+        for (int c = 0; c < nchunks; c += kChunkUnroll) {
+            float4 X[kChunkUnroll], Y[kChunkUnroll], Z[kChunkUnroll];
+            float dl[kChunkUnroll];
+#pragma unroll
+            for (int q = 0; q < kChunkUnroll; q++) {
+                const int cq = kPinTable ? 0 : c + q;
+                X[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48, cq * 3072, 0));
+                Y[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 16, cq * 3072, 0));
+                Z[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 32, cq * 3072, 0));
+                dl[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, lane * 4, cq * 256, 0));
             }
+#pragma unroll
+            for (int q = 0; q < kChunkUnroll; q++) {
+                const int li = (c + q) * 64 + lane;
+                const int stage = prep_stage_pk_bf(S, li, X[q], Y[q], Z[q], dl[q], nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
+                const uint64_t m = __ballot(stage == 0);
+                if (stage == 0) lst[ncand + lane_rank(m)] = (unsigned short)li;
+                ncand += __popcll(m);
+                culled1 += __popcll(__ballot(stage == 1));
+            }
+        }
+        }
+        wave_lds_sync();
+        // phase B: dense fp64 batches of 64 consecutive candidates
+        for (nb = 0; 64 * nb < ncand; nb++) {
+            const int k = 64 * nb + lane;
+            const bool act = k < ncand;
+            bool ok;
+            double w = prep_weight_buf(rw, act ? (int)lst[k] : 0, x1, &ok);
+            ok = ok && act;
+            w = act ? w : 0.0;
+            if (kBuild && act) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
+            const double sc = wave_incl_scan(w, lane);
+            survivors += __popcll(__ballot(ok));
+            if (lane == 63) bt[nb] = sc;
         }
         wave_lds_sync();
         full_acc++;
@@ -2068,7 +2167,7 @@ struct DeviceState {
     std::vector<void*> allocs;
     hipStream_t stream = nullptr;
     // reusable work buffers
-    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14], aux[8], cache_bt, cache_lst, cache_info, cache_w;
+    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14], aux[8], cache_bt, cache_lst, cache_info, cache_w, masks;
     unsigned* pinned_count = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr;
 };
@@ -2166,7 +2265,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     }
     if ((rc = upload(*D, lv, &d.lt_v))) return rc;
     if ((rc = upload(*D, ln, &d.lt_n))) return rc;
-    const int nl_pad = 64 * prep_chunks(s.NL);  // whole chunks: the prep kernel reads past N_L unchecked
+    const int nl_pad = 256 * ((prep_chunks(s.NL) + 3) / 4);  // whole groups of 4 chunks: the prep kernel reads past N_L unchecked
     std::vector<float4> lpk(3 * nl_pad, make_float4(0, 0, 0, 0));
     std::vector<float> ld(nl_pad, 0.0f);
     std::vector<double2> lw(5 * nl_pad, make_double2(0, 0));
@@ -2262,18 +2361,19 @@ constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
-                       const PrepCache& cache = PrepCache{}) {
+                       const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr) {
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? 8 : 0;  // A/B on MI355X: tools/prep_variants.py
+    if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? 14 : 8) : 0;  // A/B: tools/prep_variants.py
     if (variant == 9) {
         hipLaunchKernelGGL(k_prep_lane, dim3((n + 255) / 256), dim3(256), 0, st, d, seed, n, qp, qn, qpixel, qsample, qnode,
                            u, wsum, pick, count, stats);
         return hipGetLastError();
     }
     if (variant > 0 && !list_ok) variant = 0;
-    if (cache.build && variant != 8) return hipErrorInvalidValue;  // the cache is built by variant 8
+    if (variant >= 14 && variant <= 16 && !masks) variant = 8;  // the split form needs the candidate-word scratch
+    if (cache.build && variant != 8 && variant != 14) return hipErrorInvalidValue;  // built by variants 8 / 14
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
     hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
@@ -2298,6 +2398,29 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
         case 7:
             hipLaunchKernelGGL((k_prep_pk<4>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
                                qnode, u, wsum, pick, count, stats, nchunks, wb, work);
+            break;
+        case 14:  // split phase A (k_prep_cull, kCullNodes nodes per table pass) + phase B / pick
+        case 15:  // A/B: 2 nodes per table pass
+        case 16: {  // A/B: 8 nodes per table pass
+            const int kn = variant == 15 ? 2 : variant == 16 ? 8 : kCullNodes;
+            const int cblocks = std::max(1, std::min((n + 4 * kn - 1) / (4 * kn), 4096));
+            if (kn == 2)
+                hipLaunchKernelGGL((k_prep_cull<2>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
+            else if (kn == 8)
+                hipLaunchKernelGGL((k_prep_cull<8>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
+            else
+                hipLaunchKernelGGL((k_prep_cull<kCullNodes>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
+            if (cache.build)
+                hipLaunchKernelGGL((k_prep_pk2<5, true, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
+                                   qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
+            else
+                hipLaunchKernelGGL((k_prep_pk2<5, false, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
+                                   qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
+            break;
+        }
+        case 13:  // diagnostic only: table loads pinned to chunk 0 (timing, results meaningless)
+            hipLaunchKernelGGL((k_prep_pk2<5, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+                               qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
             break;
         case 10:  // A/B: variant 8 at 6 waves/SIMD
             hipLaunchKernelGGL((k_prep_pk2<6, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
@@ -2377,6 +2500,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     }
     double prep_ms = 0;
     uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0;
+    // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
+    uint64_t* masks = nullptr;
+    if (o->mode != MCPT_MODE_BRDF && D.d.NL > kSmallNL) {
+        if ((rc = ensure(D.masks, (size_t)std::max(cap, npx) * nchunks * 8))) return rc;
+        masks = (uint64_t*)D.masks.p;
+    }
     // root-point cache (see PrepCache): built here when the call has >= 2 samples per pixel and the
     // entries fit in a 64 GiB budget of HBM (800x600 with N_L = 3012: 15 GB)
     PrepCache pc{};
@@ -2403,8 +2532,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (nr > 0) {
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
-            HIP_OK(launch_prep(8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, P.stats, (unsigned*)D.work.p, st, pc));
+            HIP_OK(launch_prep(masks ? 14 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
+                               nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks));
             HIP_OK(hipEventRecord(D.evp1, st));
             HIP_OK(hipEventSynchronize(D.evp1));
             float ms = 0;
@@ -2458,7 +2587,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 if (nc > 0) {
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
+                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks));
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
@@ -2473,7 +2602,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             } else {
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st));
+                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 timed = true;
             }
@@ -2755,7 +2884,8 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     DeviceState* D;
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
-    void *dp, *dn, *du, *dw, *dc, *dk;
+    void *dp, *dn, *du, *dw, *dc, *dk, *dm;
+    HIP_OK(hipMalloc(&dm, 8ull * n * prep_chunks(D->d.NL)));  // the render path's split prep (variant 14)
     HIP_OK(hipMalloc(&dp, 24ull * n));
     HIP_OK(hipMalloc(&dn, 24ull * n));
     HIP_OK(hipMalloc(&du, 8ull * n));
@@ -2767,13 +2897,14 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
     if ((rc = ensure(D->work, 256))) return rc;
     HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
-                       (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream));
+                       (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream,
+                       PrepCache{}, (uint64_t*)dm));
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(count, dc, 4ull * n, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
     for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
-    void* bufs[] = {dp, dn, du, dw, dc, dk};
+    void* bufs[] = {dp, dn, du, dw, dc, dk, dm};
     for (void* b : bufs) (void)hipFree(b);
     return MCPT_OK;
 }
@@ -2788,7 +2919,8 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     DeviceState* D;
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
-    void *dp, *dn, *du, *dw, *dk;
+    void *dp, *dn, *du, *dw, *dk, *dm;
+    HIP_OK(hipMalloc(&dm, 8ull * n * prep_chunks(D->d.NL)));
     HIP_OK(hipMalloc(&dp, 24ull * n));
     HIP_OK(hipMalloc(&dn, 24ull * n));
     HIP_OK(hipMalloc(&du, 8ull * n));
@@ -2799,11 +2931,13 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
     if ((rc = ensure(D->work, 256))) return rc;
     HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
-                       (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream));
+                       (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream,
+                       PrepCache{}, (uint64_t*)dm));
     HIP_OK(hipEventRecord(D->ev0, D->stream));
     for (int it = 0; it < iters; it++)
         HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
-                           (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream));
+                           (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream,
+                       PrepCache{}, (uint64_t*)dm));
     HIP_OK(hipEventRecord(D->ev1, D->stream));
     HIP_OK(hipEventSynchronize(D->ev1));
     float t = 0;
@@ -2812,7 +2946,7 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
     for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
-    void* bufs[] = {dp, dn, du, dw, dk};
+    void* bufs[] = {dp, dn, du, dw, dk, dm};
     for (void* b : bufs) (void)hipFree(b);
     return MCPT_OK;
 }
