@@ -1591,14 +1591,17 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
     const int waves = gridDim.x * (blockDim.x >> 6);
     for (int node = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); node < n; node += waves) {
         const int px = qpixel[node];
+        const double* bt = C.bt + (size_t)px * nchunks;
+        // the batch totals are loaded together with the entry's header (not after it): entries
+        // past nb are masked once the header has arrived
+        const double vraw = lane < nchunks ? bt[lane] : 0.0;
         const int4 inf = C.info[px];
         const int nb = inf.x, ncand = inf.y;
-        const double* bt = C.bt + (size_t)px * nchunks;
         double wsum = 0;
         int kb = -1;
         double base = 0, target = 0;
         if (nb <= 64) {
-            const double v = lane < nb ? bt[lane] : 0.0;
+            const double v = lane < nb ? vraw : 0.0;
             const double cum = wave_incl_scan(v, lane);
             wsum = __shfl(cum, 63);
             if (!(fabs(wsum) < MCPT_EPS)) {
@@ -1636,6 +1639,7 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
             const int k = 64 * kb + lane;
             const bool act = k < ncand;
             const double wc = act ? C.w[(size_t)px * C.lstride + k] : -1.0;
+            const int lj = act ? (int)C.lst[(size_t)px * C.lstride + k] : 0;  // in flight with the weights
             const bool ok = wc >= 0;
             const double sc = wave_incl_scan(ok ? wc : 0.0, lane);
             const uint64_t candm = __ballot(ok && (base + sc >= target));
@@ -1643,7 +1647,7 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
             int pl = -1;
             if (candm) pl = __ffsll((unsigned long long)candm) - 1;
             else if (okm) pl = 63 - __clzll((long long)okm);
-            if (pl >= 0) pick = C.lst[(size_t)px * C.lstride + 64 * kb + pl];
+            if (pl >= 0) pick = __shfl(lj, pl);
         }
         if (lane == 0) {
             wsum_out[node] = wsum;
