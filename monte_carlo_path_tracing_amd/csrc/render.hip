@@ -512,6 +512,33 @@ __device__ inline int wave_append(unsigned* counter, bool want) {
     return want ? (int)(base + __popcll(below)) : -1;
 }
 
+// workgroup-aggregated append: ONE atomic per workgroup.  The queue counter is a single word, and
+// one device-scope word saturates at ~88 atomic adds per microsecond (MI355X_MICROARCH.md,
+// "dequeue"), so per-wave appends capped the root and extension kernels at ~5.6 G nodes/s.
+// Must be called by every thread of the workgroup (it contains barriers).
+__device__ inline int block_append(unsigned* counter, bool want) {
+    __shared__ unsigned s_cnt[16];  // per wave, up to 1024 threads
+    __shared__ unsigned s_base;
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    const uint64_t m = __ballot(want);
+    if (lane == 0) s_cnt[wid] = (unsigned)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot = 0;
+        for (int w = 0; w < nw; w++) {
+            const unsigned c = s_cnt[w];
+            s_cnt[w] = tot;
+            tot += c;
+        }
+        s_base = tot ? atomicAdd(counter, tot) : 0u;
+    }
+    __syncthreads();
+    const unsigned base = s_base + s_cnt[wid];
+    __syncthreads();  // s_cnt / s_base are reused by the next call
+    const uint64_t below = lane == 0 ? 0ull : (m & ((~0ull) >> (64 - lane)));
+    return want ? (int)(base + __popcll(below)) : -1;
+}
+
 // wave-aggregated statistics counter: adds the sum of v (0..3) over the calling lanes with ONE
 // atomic (a per-lane atomic on a shared counter serialises at wavefront node rates).  Must be
 // called by every lane of the wave that may contribute.
@@ -533,7 +560,7 @@ __device__ inline void node_point(const DScene& S, int f, double beta, double ga
 
 // node entry of shade_with_* (main.cpp:406-437 / :351-383): interpolate, back-face -> 0,
 // emitter -> emit, Russian roulette; survivors are appended to the queue.
-// Must be called by ALL lanes of the wave (wave_append); `active` masks the lane.
+// Must be called by ALL threads of the workgroup (block_append); `active` masks the lane.
 __device__ inline void node_entry(const Params& P, bool active, int f, double beta, double gamma, d3 wo, d3 tp,
                                   int pixel, int sample, uint64_t node, Queue& q) {
     const DScene& S = P.S;
@@ -560,7 +587,7 @@ __device__ inline void node_entry(const Params& P, bool active, int f, double be
             }
         }
     }
-    const int slot = wave_append(q.count, push);
+    const int slot = block_append(q.count, push);
     if (push) {
         if (slot >= q.cap) {
             atomicOr((unsigned long long*)(P.stats + 4), 1ull);
@@ -642,7 +669,7 @@ __global__ __launch_bounds__(256) void k_root_points(DScene S, CamFrame cam, con
             want = !(dot(N, mul(cam_dir(cam, px / cam.W, px % cam.W), -1)) < 0);
         }
     }
-    const int slot = wave_append(q.count, want);
+    const int slot = block_append(q.count, want);
     if (want && slot < q.cap) {
         q.p[3 * slot] = p.x, q.p[3 * slot + 1] = p.y, q.p[3 * slot + 2] = p.z;
         q.n[3 * slot] = N.x, q.n[3 * slot + 1] = N.y, q.n[3 * slot + 2] = N.z;
