@@ -539,12 +539,24 @@ __device__ inline int block_append(unsigned* counter, bool want) {
     return want ? (int)(base + __popcll(below)) : -1;
 }
 
-// wave-aggregated statistics counter: adds the sum of v (0..3) over the calling lanes with ONE
-// atomic (a per-lane atomic on a shared counter serialises at wavefront node rates).  Must be
-// called by every lane of the wave that may contribute.
-__device__ inline void wave_count(unsigned long long* counter, unsigned v) {
-    const unsigned long long n = (unsigned long long)__popcll(__ballot(v & 1)) + 2ull * __popcll(__ballot(v & 2));
-    if (n && lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) atomicAdd(counter, n);
+// workgroup-aggregated statistics counters: adds the sums of a and b (each 0..3) over the
+// workgroup to ca / cb with one atomic each (per-lane or per-wave atomics on a shared counter
+// serialise at wavefront node rates).  Must be called by ALL threads of the workgroup.
+__device__ inline void block_count(unsigned long long* ca, unsigned a, unsigned long long* cb = nullptr,
+                                   unsigned b = 0) {
+    __shared__ unsigned s_sum[2][16];
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    const unsigned na = (unsigned)__popcll(__ballot(a & 1)) + 2u * (unsigned)__popcll(__ballot(a & 2));
+    const unsigned nb = (unsigned)__popcll(__ballot(b & 1)) + 2u * (unsigned)__popcll(__ballot(b & 2));
+    if (lane == 0) { s_sum[0][wid] = na; s_sum[1][wid] = nb; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long ta = 0, tb = 0;
+        for (int w = 0; w < nw; w++) { ta += s_sum[0][w]; tb += s_sum[1][w]; }
+        if (ta) atomicAdd(ca, ta);
+        if (cb && tb) atomicAdd(cb, tb);
+    }
+    __syncthreads();  // s_sum is reused by the next call
 }
 
 // shading point and normal of a hit (main.cpp:406-407: interpolated position, normalised
@@ -1767,10 +1779,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur,
     }
     node_entry(P, c1, h1.f, h1.beta, h1.gamma, mul(wl, -1), tp1, pixel, sample, 2 * node, nxt);
     node_entry(P, c2, h2.f, h2.beta, h2.gamma, mul(wi, -1), tp2, pixel, sample, 2 * node + 1, nxt);
-    if (active) {
-        wave_count(P.stats + 2, nrays);
-        wave_count(P.stats + 3, nlrays);
-    }
+    block_count(P.stats + 2, active ? nrays : 0u, P.stats + 3, active ? nlrays : 0u);
 }
 
 // ---- MIS node split into three kernels (ray generation / traversal / combination) -------------
@@ -1908,11 +1917,8 @@ __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n,
     const d3 tp1 = mk3(A.w1[3 * ii], A.w1[3 * ii + 1], A.w1[3 * ii + 2]);
     node_entry(P, c1, c1 ? A.hf[o1] : -1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), tp1, pixel, sample, 2 * node, nxt);
     node_entry(P, c2, c2 ? A.hf[o2] : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), tp2, pixel, sample, 2 * node + 1, nxt);
-    if (active) {
-        const unsigned nr = (fl & 1) + ((fl >> 1) & 1);
-        wave_count(P.stats + 2, nr);
-        wave_count(P.stats + 3, c2 ? 1u : 0u);
-    }
+    block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, P.stats + 3,
+                (active && c2) ? 1u : 0u);
 }
 
 // ---- shade() and shade_with_brdf nodes in the same split form (k_mis_rays traces sets 0-1 / 1) ----
@@ -1996,7 +2002,7 @@ __global__ __launch_bounds__(256) void k_shade_combine(Params P, Queue cur, int 
     const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
-    wave_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u);
+    block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u);
 }
 
 // shade_with_brdf (main.cpp:385-396): gen samples the bounce, combine spawns the child on any hit
@@ -2036,7 +2042,7 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
     const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
-    wave_count(P.stats + 2, (active && (fl & 2)) ? 1u : 0u);
+    block_count(P.stats + 2, (active && (fl & 2)) ? 1u : 0u);
 }
 
 // one shade() node (main.cpp:295-343), lane per node: the direct-light estimate is splatted into
@@ -2117,7 +2123,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_shade(Params P, Queue cu
         }
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
-    wave_count(P.stats + 2, active ? nrays : 0u);
+    block_count(P.stats + 2, active ? nrays : 0u);
 }
 
 // one BRDF-only path vertex (main.cpp:385-396)
@@ -2155,7 +2161,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
         }
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
-    wave_count(P.stats + 2, traced);
+    block_count(P.stats + 2, traced);
 }
 
 // batch closest hit (test / FFI entry mcpt_closest_hit)
