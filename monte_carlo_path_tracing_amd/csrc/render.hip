@@ -36,6 +36,17 @@ using namespace mcpt;
 // ============================================================================================
 // device scene
 // ============================================================================================
+// two consecutive light triangles (2q, 2q+1) for the lane-per-node cull, every field as an (A, B)
+// float pair so that one v_pk_fma_f32 with a scalar operand serves both lights: nl = unique normal,
+// d = float(nl . p0 + 1e-8) (the threshold folded in), p[3k+i] = coordinate i of vertex k.  Padding
+// lights (index >= N_L) have nl = 0, d = 1e30 (light-side culled).  128 B = two s_load_dwordx16.
+struct LightPair {
+    float2 nl[3];
+    float2 d;
+    float2 p[9];
+    float pad[6];
+};
+
 struct DScene {
     int F, NL;
     const float4* tri_v;      // F*3, original facet order
@@ -52,6 +63,7 @@ struct DScene {
     const float4* lt_pk;      // NL*3: (p0.x, p1.x, p2.x, nl.x), (.. .y), (.. .z) -- packed cheap stages
     const float* lt_d;        // NL: float(nl . p0)
     const double2* lt_w;      // NL*5: p0, p1, p2 (fp64), RadianceRGB::sum()
+    const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
     const BvhNode* bvh;       // all facets
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
     const BvhNode* lbvh;      // light facets only
@@ -1493,6 +1505,128 @@ __global__ __launch_bounds__(256) void k_prep_cull(DScene S, int n, const double
     if (lane == 0 && stats && c1_acc) atomicAdd(stats + 6, c1_acc);
 }
 
+// Phase A with a lane per shading node and the light table in scalar registers: each light pair
+// (LightPair, two s_load_dwordx16) is read once per 64 nodes from the scalar cache, and the two
+// cheap stages of both lights run as 13 v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 with one
+// scalar operand each -- no vector memory traffic at all in the light loop.  A lane shifts its
+// candidate bit into a 32-bit word with one v_addc_co_u32 (carry-in = the wave's compare mask);
+// after 32 lights v_bfrev puts light j at bit j, so the stored word per (node, chunk) is the same
+// as k_prep_cull's.  Values within err of the 1e-8 threshold take the exact fp64 stage, so the
+// decisions are the reference's (err as in node_f; the threshold is folded into d and cn).
+// raw v_max3_f32 / v_min_f32 (the builtins canonicalise operands that came out of packed ops
+// first; NaN handling is irrelevant here: a NaN light value never reaches the cull)
+__device__ inline float max3_raw(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ inline float min_raw(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline float min_abs_raw(float a, float b) {
+    float r;
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline unsigned shift_in(unsigned w, uint64_t carry) {
+    unsigned r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(w), "s"(carry));
+    return r;
+}
+
+// the two cheap stages of light pair T (lights A, B) for this lane's node, threshold folded in:
+// s = nl . x1 - (nl . p0 + 1e-8), t[k] = n . p_k - (n . x1 + 1e-8)
+struct CullLane {
+    v2f xx, yy, zz, nxx, nyy, nzz, ncn;
+    __device__ inline void eval(const LightPair& L, v2f* s, v2f* t) const {
+        const v2f nlx{L.nl[0].x, L.nl[0].y}, nly{L.nl[1].x, L.nl[1].y}, nlz{L.nl[2].x, L.nl[2].y};
+        *s = __builtin_elementwise_fma(xx, nlx, __builtin_elementwise_fma(yy, nly, zz * nlz)) - v2f{L.d.x, L.d.y};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const v2f px{L.p[3 * k].x, L.p[3 * k].y}, py{L.p[3 * k + 1].x, L.p[3 * k + 1].y},
+                pz{L.p[3 * k + 2].x, L.p[3 * k + 2].y};
+            t[k] = __builtin_elementwise_fma(nxx, px, __builtin_elementwise_fma(nyy, py, __builtin_elementwise_fma(nzz, pz, ncn)));
+        }
+    }
+};
+
+__global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
+                                                         const double* __restrict__ qn, uint64_t* __restrict__ masks,
+                                                         int nchunks, unsigned long long* stats) {
+    const int node = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = node < n;
+    const int nd = act ? node : n - 1;
+    const d3 x1 = mk3(qp[3 * nd], qp[3 * nd + 1], qp[3 * nd + 2]);
+    const d3 nn = mk3(qn[3 * nd], qn[3 * nd + 1], qn[3 * nd + 2]);
+    const NodeF f = node_f(x1, nn, S.light_bound);
+    const float cn = (float)(dot(nn, x1) + MCPT_EPS);
+    CullLane cl;
+    cl.xx = v2f{f.x, f.x};
+    cl.yy = v2f{f.y, f.y};
+    cl.zz = v2f{f.z, f.z};
+    cl.nxx = v2f{f.nx, f.nx};
+    cl.nyy = v2f{f.ny, f.ny};
+    cl.nzz = v2f{f.nz, f.nz};
+    cl.ncn = v2f{-cn, -cn};
+    const float err = f.err;
+    const uint64_t actm = __ballot(act);
+    unsigned long long c1 = 0;
+    const LightPair* __restrict__ T = S.lt_pair;
+    for (int c = 0; c < nchunks; c++) {
+        unsigned word[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const LightPair* __restrict__ Th = T + 32 * c + 16 * h;
+            unsigned w = 0, c1w = 0;
+            uint64_t anyam = 0;
+#pragma unroll 2
+            for (int q = 0; q < 16; q++) {
+                v2f s1, t[3];
+                cl.eval(Th[q], &s1, t);
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const float sv = s1[e];
+                    const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
+                    // ambiguous lanes (a value within err of the threshold) have s >= -err and a clear bit here
+                    anyam |= __ballot(min_abs_raw(sv, mn) <= err);
+                    c1w += __popcll(__ballot(sv < -err) & actm);
+                    w = shift_in(w, __ballot(mn > err));
+                }
+            }
+            if (anyam & actm) {  // rare: the reference's exact fp64 stages for the ambiguous (node, light) pairs
+                for (int q = 0; q < 16; q++) {
+                    v2f s1, t[3];
+                    cl.eval(Th[q], &s1, t);
+                    for (int e = 0; e < 2; e++) {
+                        const float sv = s1[e];
+                        const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
+                        const int li = 64 * c + 32 * h + 2 * q + e;
+                        int st = -1;
+                        if (act && min_abs_raw(sv, mn) <= err && li < S.NL) {
+                            const LightPair& L = Th[q];
+                            auto pc = [&](int i) { return (double)(e ? L.p[i].y : L.p[i].x); };
+                            const double4 ln = S.lt_n[li];
+                            st = light_cheap_stage(mk3(pc(0), pc(1), pc(2)), mk3(pc(3), pc(4), pc(5)),
+                                                   mk3(pc(6), pc(7), pc(8)), mk3(ln.x, ln.y, ln.z), x1, nn);
+                            if (st == 0) w |= 1u << (31 - (2 * q + e));
+                        }
+                        c1w += __popcll(__ballot(st == 1));  // uniform: every lane of the wave
+                    }
+                }
+            }
+            c1 += c1w;
+            word[h] = __builtin_bitreverse32(w);
+        }
+        if (act) masks[(size_t)node * nchunks + c] = ((uint64_t)word[1] << 32) | word[0];
+    }
+    // padding lights (index >= N_L, d = 1e30) were counted as light-side culled by every active lane
+    c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
+    if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
+}
+
 template <int kMinWavesPerSimd, bool kBuild, bool kPinTable = false, bool kMaskIn = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
@@ -2318,6 +2452,32 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
         lw[5 * l + 3] = make_double2(c.x, c.y);
         lw[5 * l + 4] = make_double2(c.z, ln[l].w);
     }
+    std::vector<LightPair> lpr(32 * (size_t)std::max(prep_chunks(s.NL), 1));
+    for (size_t q = 0; q < lpr.size(); q++) {
+        LightPair& P = lpr[q];
+        memset((void*)&P, 0, sizeof P);
+        float* nl = &P.nl[0].x;
+        float* dd = &P.d.x;
+        float* pp = &P.p[0].x;
+        for (int h = 0; h < 2; h++) {
+            const int l = (int)(2 * q) + h;
+            if (l >= s.NL) {
+                dd[h] = 1e30f;
+                continue;
+            }
+            const float4 v[3] = {lv[3 * l], lv[3 * l + 1], lv[3 * l + 2]};
+            nl[h] = (float)ln[l].x;
+            nl[2 + h] = (float)ln[l].y;
+            nl[4 + h] = (float)ln[l].z;
+            dd[h] = (float)((ln[l].x * v[0].x + ln[l].y * v[0].y + ln[l].z * v[0].z) + MCPT_EPS);
+            for (int k = 0; k < 3; k++) {
+                pp[2 * (3 * k) + h] = v[k].x;
+                pp[2 * (3 * k + 1) + h] = v[k].y;
+                pp[2 * (3 * k + 2) + h] = v[k].z;
+            }
+        }
+    }
+    if ((rc = upload(*D, lpr, &d.lt_pair))) return rc;
     if ((rc = upload(*D, lpk, &d.lt_pk))) return rc;
     if ((rc = upload(*D, ld, &d.lt_d))) return rc;
     if ((rc = upload(*D, lw, &d.lt_w))) return rc;
@@ -2393,6 +2553,13 @@ size_t prep_lds_bytes(int nchunks) { return 4 * ((size_t)nchunks * sizeof(double
 int prep_list_wave_bytes(int nchunks) { return (int)((nchunks * 8 + nchunks * 64 * 2 + 15) / 16 * 16); }
 constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 
+// the split (cull + eval) light prep used by the renderer: 17 (lane-per-node cull), or 14 (wave per
+// 4 nodes) with MCPT_CULL_TABLE set (A/B switch)
+int split_prep_variant() {
+    static const int v = getenv("MCPT_CULL_TABLE") ? 14 : 17;
+    return v;
+}
+
 // variant: -1 auto (list+prefetch when it fits, else queue), 0 queue, 1 list, 2 list+prefetch
 // work: a device word, zeroed here before the launch (the kernel's dynamic node counter)
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
@@ -2402,15 +2569,15 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? 14 : 8) : 0;  // A/B: tools/prep_variants.py
+    if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? split_prep_variant() : 8) : 0;  // A/B: tools/prep_variants.py
     if (variant == 9) {
         hipLaunchKernelGGL(k_prep_lane, dim3((n + 255) / 256), dim3(256), 0, st, d, seed, n, qp, qn, qpixel, qsample, qnode,
                            u, wsum, pick, count, stats);
         return hipGetLastError();
     }
     if (variant > 0 && !list_ok) variant = 0;
-    if (variant >= 14 && variant <= 16 && !masks) variant = 8;  // the split form needs the candidate-word scratch
-    if (cache.build && variant != 8 && variant != 14) return hipErrorInvalidValue;  // built by variants 8 / 14
+    if (variant >= 14 && variant <= 17 && !masks) variant = 8;  // the split form needs the candidate-word scratch
+    if (cache.build && variant != 8 && variant != 14 && variant != 17) return hipErrorInvalidValue;  // built by 8 / 14 / 17
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
     hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
@@ -2438,10 +2605,14 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
             break;
         case 14:  // split phase A (k_prep_cull, kCullNodes nodes per table pass) + phase B / pick
         case 15:  // A/B: 2 nodes per table pass
-        case 16: {  // A/B: 8 nodes per table pass
+        case 16:  // A/B: 8 nodes per table pass
+        case 17: {  // phase A lane per node (k_prep_cull_lanes, light table in scalar registers)
             const int kn = variant == 15 ? 2 : variant == 16 ? 8 : kCullNodes;
             const int cblocks = std::max(1, std::min((n + 4 * kn - 1) / (4 * kn), 4096));
-            if (kn == 2)
+            if (variant == 17)
+                hipLaunchKernelGGL(k_prep_cull_lanes, dim3((n + 255) / 256), dim3(256), 0, st, d, n, qp, qn, masks, nchunks,
+                                   stats);
+            else if (kn == 2)
                 hipLaunchKernelGGL((k_prep_cull<2>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
             else if (kn == 8)
                 hipLaunchKernelGGL((k_prep_cull<8>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
@@ -2569,7 +2740,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (nr > 0) {
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
-            HIP_OK(launch_prep(masks ? 14 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
+            HIP_OK(launch_prep(masks ? split_prep_variant() : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
                                nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks));
             HIP_OK(hipEventRecord(D.evp1, st));
             HIP_OK(hipEventSynchronize(D.evp1));
