@@ -1450,6 +1450,14 @@ __device__ inline double prep_select(const double* bt, const unsigned short* lst
 }
 
 constexpr int kChunkUnroll = 2;
+// chunk splits of k_prep_cull_lanes: enough waves for ~8 per SIMD (1024 SIMDs), at most 4 splits
+// and at least 4 chunks per split; MCPT_CULL_SPLITS overrides (A/B)
+inline int cull_splits(int n, int nchunks) {
+    static const int env = getenv("MCPT_CULL_SPLITS") ? atoi(getenv("MCPT_CULL_SPLITS")) : 0;
+    const int waves = (n + 63) / 64;
+    int s = env > 0 ? env : (8192 + waves - 1) / std::max(waves, 1);
+    return std::max(1, std::min({s, 4, std::max(1, nchunks / 4)}));
+}
 constexpr int kCullNodes = 4;
 // kPinTable (diagnostic variant 13 only, results meaningless): every chunk reads chunk 0's table
 // rows, to measure how much of phase A is L2 -> CU table traffic
@@ -1575,7 +1583,10 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
     const uint64_t actm = __ballot(act);
     unsigned long long c1 = 0;
     const LightPair* __restrict__ T = S.lt_pair;
-    for (int c = 0; c < nchunks; c++) {
+    // blockIdx.y splits the chunks: more waves per SIMD to hide the scalar-load latency of the table
+    const int per = (nchunks + gridDim.y - 1) / gridDim.y;
+    const int cb = blockIdx.y * per, ce = min(nchunks, cb + per);
+    for (int c = cb; c < ce; c++) {
         unsigned word[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -1623,7 +1634,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
         if (act) masks[(size_t)node * nchunks + c] = ((uint64_t)word[1] << 32) | word[0];
     }
     // padding lights (index >= N_L, d = 1e30) were counted as light-side culled by every active lane
-    c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
+    if (ce == nchunks) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
 
@@ -1750,83 +1761,116 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
 
 // root nodes (node id 1) from the root-point cache: prep_select's search with the cached batch
 // totals and candidate weights -- the same scans over the same values, so the same pick -- and no
-// light-triangle arithmetic at all.  One wave per node; no LDS.
+// light-triangle arithmetic at all.  One wave per node, kPickNodes nodes per wave at a time: a root
+// is a chain of three dependent loads (pixel -> batch totals -> one batch of weights), so the wave
+// issues each link for all of its nodes before waiting on any of them (the kernel is bound by
+// that latency, not by bandwidth).  No LDS.
+constexpr int kPickNodes = 4;
 __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                    double* __restrict__ wsum_out, int* __restrict__ pick_out,
-                                                   unsigned long long* stats, int nchunks, unsigned* __restrict__ work,
-                                                   PrepCache C) {
+                                                   unsigned long long* stats, int nchunks, PrepCache C) {
     const int lane = threadIdx.x & 63;
-    unsigned long long cached = 0;
-    // static wave-strided assignment: a root costs ~the same everywhere, and a shared work counter
-    // would serialise on its one address at this node rate
-    (void)work;
     const int waves = gridDim.x * (blockDim.x >> 6);
-    for (int node = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); node < n; node += waves) {
-        const int px = qpixel[node];
-        const double* bt = C.bt + (size_t)px * nchunks;
-        // the batch totals are loaded together with the entry's header (not after it): entries
-        // past nb are masked once the header has arrived
-        const double vraw = lane < nchunks ? bt[lane] : 0.0;
-        const int4 inf = C.info[px];
-        const int nb = inf.x, ncand = inf.y;
-        double wsum = 0;
-        int kb = -1;
-        double base = 0, target = 0;
-        if (nb <= 64) {
-            const double v = lane < nb ? vraw : 0.0;
-            const double cum = wave_incl_scan(v, lane);
-            wsum = __shfl(cum, 63);
-            if (!(fabs(wsum) < MCPT_EPS)) {
-                target = counter_u(counter_key(seed, (uint64_t)px, (uint64_t)qsample[node], qnode[node]), 1) * wsum;
-                const uint64_t hitm = __ballot(cum >= target && v > 0);
-                const uint64_t posm = __ballot(v > 0);
-                kb = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63 - __clzll((long long)posm);
-                const double exc = __shfl_up(cum, 1);
-                base = kb == 0 ? 0.0 : __shfl(exc, kb);
-            }
-        } else {
-            for (int b = 0; b < nb; b++) wsum += bt[b];
-            if (!(fabs(wsum) < MCPT_EPS)) {
-                target = counter_u(counter_key(seed, (uint64_t)px, (uint64_t)qsample[node], qnode[node]), 1) * wsum;
-                int lastpos = -1;
-                double cum = 0;
-                for (int b = 0; b < nb; b++) {
-                    const double nxt = cum + bt[b];
-                    if (bt[b] > 0) lastpos = b;
-                    if (kb < 0 && nxt >= target && bt[b] > 0) {
-                        kb = b;
-                        base = cum;
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    unsigned long long cached = 0;
+    // static assignment: a root costs ~the same everywhere, and a shared work counter would
+    // serialise on its one address at this node rate
+    for (int n0 = gw * kPickNodes; n0 < n; n0 += waves * kPickNodes) {
+        int px[kPickNodes], smp[kPickNodes];
+        uint64_t nid[kPickNodes];
+#pragma unroll
+        for (int k = 0; k < kPickNodes; k++) {
+            const int node = min(n0 + k, n - 1);
+            px[k] = qpixel[node];
+            smp[k] = qsample[node];
+            nid[k] = qnode[node];
+        }
+        double vraw[kPickNodes];
+        int4 inf[kPickNodes];
+#pragma unroll
+        for (int k = 0; k < kPickNodes; k++) {
+            vraw[k] = lane < nchunks ? C.bt[(size_t)px[k] * nchunks + lane] : 0.0;
+            inf[k] = C.info[px[k]];
+        }
+        double wsum[kPickNodes], base[kPickNodes], target[kPickNodes];
+        int kb[kPickNodes];
+#pragma unroll
+        for (int k = 0; k < kPickNodes; k++) {
+            const int nb = inf[k].x;
+            const double* bt = C.bt + (size_t)px[k] * nchunks;
+            const double u = counter_u(counter_key(seed, (uint64_t)px[k], (uint64_t)smp[k], nid[k]), 1);
+            wsum[k] = 0;
+            kb[k] = -1;
+            base[k] = 0;
+            target[k] = 0;
+            if (nb <= 64) {
+                const double v = lane < nb ? vraw[k] : 0.0;
+                const double cum = wave_incl_scan(v, lane);
+                wsum[k] = __shfl(cum, 63);
+                if (!(fabs(wsum[k]) < MCPT_EPS)) {
+                    target[k] = u * wsum[k];
+                    const uint64_t hitm = __ballot(cum >= target[k] && v > 0);
+                    const uint64_t posm = __ballot(v > 0);
+                    kb[k] = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63 - __clzll((long long)posm);
+                    const double exc = __shfl_up(cum, 1);
+                    base[k] = kb[k] == 0 ? 0.0 : __shfl(exc, kb[k]);
+                }
+            } else {  // more than 64 batches (N_L > 4096 with many candidates): sequential search
+                double ws = 0;
+                for (int b = 0; b < nb; b++) ws += bt[b];
+                wsum[k] = ws;
+                if (!(fabs(ws) < MCPT_EPS)) {
+                    target[k] = u * ws;
+                    int lastpos = -1, kk = -1;
+                    double cum = 0, bs = 0;
+                    for (int b = 0; b < nb; b++) {
+                        const double nxt = cum + bt[b];
+                        if (bt[b] > 0) lastpos = b;
+                        if (kk < 0 && nxt >= target[k] && bt[b] > 0) {
+                            kk = b;
+                            bs = cum;
+                        }
+                        cum = nxt;
                     }
-                    cum = nxt;
-                }
-                if (kb < 0) {
-                    kb = lastpos;
-                    base = 0;
-                    for (int b = 0; b < kb; b++) base += bt[b];
+                    if (kk < 0) {
+                        kk = lastpos;
+                        bs = 0;
+                        for (int b = 0; b < kk; b++) bs += bt[b];
+                    }
+                    kb[k] = kk;
+                    base[k] = bs;
                 }
             }
         }
-        int pick = -1;
-        if (kb >= 0) {
-            const int k = 64 * kb + lane;
-            const bool act = k < ncand;
-            const double wc = act ? C.w[(size_t)px * C.lstride + k] : -1.0;
-            const int lj = act ? (int)C.lst[(size_t)px * C.lstride + k] : 0;  // in flight with the weights
-            const bool ok = wc >= 0;
-            const double sc = wave_incl_scan(ok ? wc : 0.0, lane);
-            const uint64_t candm = __ballot(ok && (base + sc >= target));
-            const uint64_t okm = __ballot(ok);
-            int pl = -1;
-            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-            else if (okm) pl = 63 - __clzll((long long)okm);
-            if (pl >= 0) pick = __shfl(lj, pl);
+        double wc[kPickNodes];
+        int lj[kPickNodes];
+#pragma unroll
+        for (int k = 0; k < kPickNodes; k++) {
+            const int j = 64 * kb[k] + lane;
+            const bool act = kb[k] >= 0 && j < inf[k].y;
+            wc[k] = act ? C.w[(size_t)px[k] * C.lstride + j] : -1.0;
+            lj[k] = act ? (int)C.lst[(size_t)px[k] * C.lstride + j] : 0;
         }
-        if (lane == 0) {
-            wsum_out[node] = wsum;
-            pick_out[node] = pick;
+#pragma unroll
+        for (int k = 0; k < kPickNodes; k++) {
+            int pick = -1;
+            if (kb[k] >= 0) {
+                const bool ok = wc[k] >= 0;
+                const double sc = wave_incl_scan(ok ? wc[k] : 0.0, lane);
+                const uint64_t candm = __ballot(ok && (base[k] + sc >= target[k]));
+                const uint64_t okm = __ballot(ok);
+                int pl = -1;
+                if (candm) pl = __ffsll((unsigned long long)candm) - 1;
+                else if (okm) pl = 63 - __clzll((long long)okm);
+                if (pl >= 0) pick = __shfl(lj[k], pl);
+            }
+            if (lane == 0 && n0 + k < n) {
+                wsum_out[n0 + k] = wsum[k];
+                pick_out[n0 + k] = pick;
+            }
         }
-        cached++;
+        cached += (unsigned long long)min(kPickNodes, n - n0);
     }
     if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
 }
@@ -2610,7 +2654,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
             const int kn = variant == 15 ? 2 : variant == 16 ? 8 : kCullNodes;
             const int cblocks = std::max(1, std::min((n + 4 * kn - 1) / (4 * kn), 4096));
             if (variant == 17)
-                hipLaunchKernelGGL(k_prep_cull_lanes, dim3((n + 255) / 256), dim3(256), 0, st, d, n, qp, qn, masks, nchunks,
+                hipLaunchKernelGGL(k_prep_cull_lanes, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d, n, qp, qn, masks, nchunks,
                                    stats);
             else if (kn == 2)
                 hipLaunchKernelGGL((k_prep_cull<2>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
@@ -2800,11 +2844,10 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     timed = true;
                 }
                 if (nr > 0) {
-                    unsigned* w2 = nullptr;
-                    const int blocks = std::max(1, std::min((nr + 3) / 4, 8192));
+                    const int blocks = std::max(1, std::min((nr + 4 * kPickNodes - 1) / (4 * kPickNodes), 8192));
                     hipLaunchKernelGGL(k_prep_pick, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
                                        cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats, nchunks,
-                                       w2, pc);
+                                       pc);
                     HIP_OK(hipGetLastError());
                 }
             } else {
