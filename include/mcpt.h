@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 10100 /* 1.1.0 */
+#define MCPT_VERSION 10200 /* 1.2.0 */
 
 enum {
     MCPT_OK = 0,
@@ -32,6 +32,7 @@ enum {
     MCPT_E_SCENE = -3,    /* scene violates the reference's assumptions (e.g. facet without material) */
     MCPT_E_DEVICE = -4,   /* HIP error */
     MCPT_E_OVERFLOW = -5, /* wavefront queue overflow (raise mcpt_render_opts.queue_factor) */
+    MCPT_E_CANCELLED = -6, /* the progress callback asked to stop */
 };
 
 /* shade_with_mis main.cpp:402 / shade_with_brdf :348 / shade :269 (the one main() calls, :575) */
@@ -62,6 +63,12 @@ typedef struct {
     int32_t width, height;
 } mcpt_camera;
 
+/* progress callback (replaces the reference's per-row progress / EasyX display, main.cpp:539-592):
+ * called on the rendering host thread after every wavefront generation with the camera samples
+ * dispatched so far and the call's total; return nonzero to cancel the render (MCPT_E_CANCELLED,
+ * the framebuffer then holds a partial sum). */
+typedef int (*mcpt_progress_fn)(void* user, uint64_t samples_dispatched, uint64_t samples_total);
+
 typedef struct {
     int32_t spp;            /* samples per pixel of the whole frame (the 1/spp weight) */
     int32_t sample_begin;   /* render global sample indices [sample_begin, sample_end) */
@@ -74,6 +81,8 @@ typedef struct {
     int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2) */
     int32_t device;         /* HIP device ordinal (-1 = current) */
     int32_t reserved;
+    mcpt_progress_fn progress; /* optional (NULL = none) */
+    void* progress_user;
 } mcpt_render_opts;
 
 typedef struct {
@@ -135,14 +144,11 @@ int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double
                     double* weights_sum, int32_t* count, int32_t* pick);
 /* diagnostics: run the light-prep kernel variant `variant` `iters` times on the n points and report
  * the mean device time per launch; outputs as mcpt_light_prep (pick = facet).  Variants: -1 auto
- * (9 if N_L <= 64, else 14, else 0 when the candidate list does not fit in LDS); 0 LDS candidate
- * queue; 1 stored LDS candidate list; 2 list + software prefetch; 3 list at 5 waves/SIMD; 4 list
- * at 6 waves/SIMD; 5 list + prefetch at 5 waves/SIMD; 6 packed-fp32 cheap stages + branch-free fp64
- * batches; 7 the same at 4 waves/SIMD; 8 variant 6 with buffer-descriptor loads and a lane-parallel
- * batch search; 9 lane per node (small light sets); 10 variant 8 at 6 waves/SIMD; 13 variant 8
- * with every table load pinned to chunk 0 (timing diagnostic only, results meaningless); 14 phase A
- * split off (k_prep_cull, 4 nodes per table pass) + variant 8's phase B; 15 / 16 the same with 2 /
- * 8 nodes per table pass. */
+ * (9 if N_L <= 64, else 17, else 0 when the candidate list does not fit in LDS); 0 k_prep (per-wave
+ * LDS candidate queue, any N_L); 8 k_prep_pk2 (packed-fp32 cheap stages, stored LDS candidate list,
+ * branch-free fp64 batches, lane-parallel batch search in one kernel); 9 k_prep_lane (lane per
+ * node, small light sets); 17 k_prep_cull_lanes (lane per node, light table in scalar registers)
+ * + k_prep_pk2's fp64 phase (the renderer's form).  Other values: MCPT_E_HIP (invalid value). */
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 /* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */

@@ -22,6 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmcpt_hip.so")
 MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2  # shade_with_mis / shade_with_brdf / shade (main.cpp:402/348/269)
 DEFAULT_SEED = 20240430
+MCPT_VERSION = 10200  # include/mcpt.h MCPT_VERSION this mirror is written against
 
 
 class MCPTError(RuntimeError):
@@ -49,7 +50,11 @@ class Camera(C.Structure):
 class RenderOpts(C.Structure):
     _fields_ = [("spp", C.c_int32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32), ("mode", C.c_int32),
                 ("seed", C.c_uint64), ("samples_per_launch", C.c_int32), ("queue_factor", C.c_int32),
-                ("device", C.c_int32), ("reserved", C.c_int32)]
+                ("device", C.c_int32), ("reserved", C.c_int32), ("progress", C.c_void_p),
+                ("progress_user", C.c_void_p)]
+
+
+PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_uint64)
 
 
 class Stats(C.Structure):
@@ -162,8 +167,12 @@ class Scene:
         return c
 
 
-def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor):
+def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress=None):
+    """progress(done, total) -> truthy to cancel; the ctypes thunk is kept on the returned struct."""
     o = RenderOpts()
+    if progress is not None:
+        o._thunk = PROGRESS_FN(lambda _u, done, total: 1 if progress(int(done), int(total)) else 0)
+        o.progress = C.cast(o._thunk, C.c_void_p)
     o.spp = int(spp)
     m = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE}.get(mode, -1) if isinstance(mode, str) else int(mode)
     if m not in (MODE_MIS, MODE_BRDF, MODE_SHADE):
@@ -179,24 +188,26 @@ def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_facto
 
 
 def render(scene, camera, spp, mode="mis", seed=DEFAULT_SEED, sample_range=None, out=None, device=None,
-           samples_per_launch=0, queue_factor=0):
+           samples_per_launch=0, queue_factor=0, progress=None):
     """render(scene, camera, spp, mode) -- main.cpp:547-588.  Returns (H x W x 3 fp64 radiance, Stats).
 
-    Adds sum_k L_k / spp over samples k in `sample_range` (default all) into `out` (zeros if None)."""
+    Adds sum_k L_k / spp over samples k in `sample_range` (default all) into `out` (zeros if None).
+    progress(samples_dispatched, samples_total), called after every wavefront generation, replaces
+    the reference's per-row progress output; a truthy return cancels (MCPTError, partial sum)."""
     if out is None:
         out = np.zeros((camera.height, camera.width, 3))
     assert out.dtype == np.float64 and out.flags.c_contiguous and out.shape == (camera.height, camera.width, 3)
     st = Stats()
-    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor)
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress)
     _check(lib().mcpt_render(scene.h, C.byref(camera), C.byref(o), out.reshape(-1), C.byref(st)))
     return out, st
 
 
 def render_device(scene, camera, spp, dev_ptr, mode="mis", seed=DEFAULT_SEED, sample_range=None, device=None,
-                  samples_per_launch=0, queue_factor=0):
+                  samples_per_launch=0, queue_factor=0, progress=None):
     """Accumulate into a device buffer of H*W*3 doubles (e.g. a torch.float64 CUDA tensor's data_ptr())."""
     st = Stats()
-    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor)
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress)
     _check(lib().mcpt_render_device(scene.h, C.byref(camera), C.byref(o), C.c_void_p(int(dev_ptr)), C.byref(st)))
     return st
 

@@ -5,7 +5,9 @@
 // integrator and output path are flags instead of edits to main.cpp.
 //
 //   mcpt_render --scene scenes/veach-mis/veach-mis [--width 1280 --height 720] [--spp 10]
-//               [--mode mis|brdf|shade] [--seed 20240430] [--out test.bmp] [--hdr out.pfm]
+//               [--mode mis|brdf|shade] [--seed 20240430] [--out test.bmp] [--hdr out.pfm] [--progress]
+//   --progress prints the share of camera samples dispatched (the reference prints per-row progress
+//   and updates its EasyX window, main.cpp:539-592) through mcpt_render_opts.progress.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -17,15 +19,31 @@
 
 namespace {
 
+int print_progress(void* user, uint64_t done, uint64_t total) {
+    int* last = static_cast<int*>(user);
+    const int pct = total ? (int)(100 * done / total) : 100;
+    if (pct / 10 != *last / 10) {
+        std::fprintf(stderr, "\rrendering: %3d%% of %llu camera samples dispatched", pct, (unsigned long long)total);
+        if (pct == 100) std::fprintf(stderr, "\n");
+        *last = pct;
+    }
+    return 0;
+}
+
 // render(scene, camera, spp, mode): main.cpp:547-588 lifted into a function.
-int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, std::vector<double>& hdr,
-           mcpt_stats* st) {
+int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, bool progress,
+           std::vector<double>& hdr, mcpt_stats* st) {
     hdr.assign(3ull * cam.width * cam.height, 0.0);
     mcpt_render_opts o{};
     o.spp = spp;
     o.mode = mode;
     o.seed = seed;
     o.device = -1;
+    int last = -10;
+    if (progress) {
+        o.progress = print_progress;
+        o.progress_user = &last;
+    }
     return mcpt_render(scene, &cam, &o, hdr.data(), st);
 }
 
@@ -49,7 +67,7 @@ int main(int argc, char** argv) {
     int W = 1280, H = 720, spp = 10, mode = MCPT_MODE_MIS;
     double dist_scale = 2.0;
     uint64_t seed = 20240430;
-    bool xml_cam = false;
+    bool xml_cam = false, progress = false;
     for (int a = 1; a < argc; a++) {
         auto next = [&]() -> const char* {
             if (a + 1 >= argc) {
@@ -77,6 +95,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[a], "--hdr")) hdr_out = next();
         else if (!std::strcmp(argv[a], "--dist-scale")) dist_scale = std::atof(next());
         else if (!std::strcmp(argv[a], "--xml-camera")) xml_cam = true;
+        else if (!std::strcmp(argv[a], "--progress")) progress = true;
         else {
             std::fprintf(stderr, "unknown option %s\n", argv[a]);
             return 2;
@@ -104,7 +123,7 @@ int main(int argc, char** argv) {
     std::vector<double> hdr;
     mcpt_stats st{};
     const auto t0 = std::chrono::steady_clock::now();
-    if (render(scene, cam, spp, mode, seed, hdr, &st) != MCPT_OK) {
+    if (render(scene, cam, spp, mode, seed, progress, hdr, &st) != MCPT_OK) {
         std::fprintf(stderr, "render failed: %s\n", mcpt_last_error());
         return 1;
     }

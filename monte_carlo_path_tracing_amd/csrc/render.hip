@@ -1018,174 +1018,13 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
     }
 }
 
-// Light prep, stored-candidate-list form (used when the per-wave list fits in LDS): pass 1 appends
-// every candidate's light index to a per-wave LDS list (uint16); batch k is list[64k, 64k+64), so
-// pass 2 re-evaluates exactly one batch without re-running the cheap stages.  kPrefetch issues the
-// next chunk's light-vertex loads before the current chunk's tests (software pipelining).
-template <bool kPrefetch, int kMinWavesPerSimd>
-__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_list(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
-                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
-                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
-                                                   const double* __restrict__ u_override, double* __restrict__ wsum_out,
-                                                   int* __restrict__ pick_out, int* __restrict__ count_out,
-                                                   unsigned long long* stats, int nchunks, int wave_bytes,
-                                                   unsigned* __restrict__ work) {
-    extern __shared__ double prep_lds[];
-    const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
-    double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
-    unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
-    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
-    int grab = 0, left = 0;
-    while (true) {
-        // dynamic distribution: a wave grabs kPrepGrab nodes per atomic (node costs vary ~10x)
-        if (left == 0) {
-            unsigned b = 0;
-            if (lane == 0) b = atomicAdd(work, (unsigned)kPrepGrab);
-            grab = __shfl((int)b, 0);
-            left = kPrepGrab;
-        }
-        const int node = grab++;
-        left--;
-        if (node >= n) break;
-        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
-        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
-        const NodeF nf = node_f(x1, nn, S.light_bound);
-        int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
-        float4 pa = make_float4(0, 0, 0, 0), pb = pa, pc = pa;
-        if (kPrefetch && lane < S.NL) {
-            pa = S.lt_v[3 * lane];
-            pb = S.lt_v[3 * lane + 1];
-            pc = S.lt_v[3 * lane + 2];
-        }
-        for (int c = 0; c < nchunks; c++) {
-            const int li = c * 64 + lane;
-            float4 a, b, cc;
-            if (kPrefetch) {
-                a = pa;
-                b = pb;
-                cc = pc;
-                const int ln = li + 64;
-                if (c + 1 < nchunks && ln < S.NL) {
-                    pa = S.lt_v[3 * ln];
-                    pb = S.lt_v[3 * ln + 1];
-                    pc = S.lt_v[3 * ln + 2];
-                }
-            } else if (li < S.NL) {
-                a = S.lt_v[3 * li];
-                b = S.lt_v[3 * li + 1];
-                cc = S.lt_v[3 * li + 2];
-            }
-            const int stage = prep_stage_regs(S, li, a, b, cc, x1, nn, nf);
-            const uint64_t m = __ballot(stage == 0);
-            if (stage == 0) lst[ncand + __popcll(m & lt_mask)] = (unsigned short)li;
-            ncand += __popcll(m);
-            culled1 += __popcll(__ballot(stage == 1));
-            while (ncand - 64 * nb >= 64 || (c == nchunks - 1 && ncand > 64 * nb)) {
-                wave_lds_sync();
-                const int k = 64 * nb + lane;
-                const bool act = k < ncand;
-                double w = 0;
-                bool ok = false;
-                if (act) {
-                    const PrepLight L = load_light(S, lst[k]);
-                    ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
-                    if (!ok) w = 0;
-                }
-                const double sc = wave_incl_scan(w, lane);
-                survivors += __popcll(__ballot(ok));
-                if (lane == 63) bt[nb] = sc;
-                nb++;
-            }
-        }
-        wave_lds_sync();
-        double wsum = 0;
-        for (int b = 0; b < nb; b++) wsum += bt[b];
-        int pick = -1;
-        if (!(fabs(wsum) < MCPT_EPS)) {
-            double u;
-            if (u_override) u = u_override[node];
-            else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-            const double target = u * wsum;
-            int kb = -1, lastpos = -1;
-            double cum = 0, base = 0;
-            for (int b = 0; b < nb; b++) {
-                const double nxt = cum + bt[b];
-                if (bt[b] > 0) lastpos = b;
-                if (kb < 0 && nxt >= target && bt[b] > 0) {
-                    kb = b;
-                    base = cum;
-                }
-                cum = nxt;
-            }
-            if (kb < 0) {
-                kb = lastpos;
-                base = 0;
-                for (int b = 0; b < kb; b++) base += bt[b];
-            }
-            const int k = 64 * kb + lane;
-            const bool act = k < ncand;
-            const int lj = act ? (int)lst[k] : 0;
-            double w = 0;
-            bool ok = false;
-            if (act) {
-                const PrepLight L = load_light(S, lj);
-                ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
-                if (!ok) w = 0;
-            }
-            const double sc = wave_incl_scan(w, lane);
-            const uint64_t candm = __ballot(ok && (base + sc >= target));
-            const uint64_t okm = __ballot(ok);
-            int pl = -1;
-            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-            else if (okm) pl = 63 - __clzll((long long)okm);
-            if (pl >= 0) pick = __shfl(lj, pl);
-        }
-        if (lane == 0) {
-            wsum_out[node] = wsum;
-            pick_out[node] = pick;
-            if (count_out) count_out[node] = survivors;
-        }
-        surv_acc += survivors;
-        cand_acc += ncand;
-        c1_acc += culled1;
-        wave_lds_sync();
-    }
-    if (lane == 0 && stats) {
-        if (surv_acc) atomicAdd(stats + 1, surv_acc);
-        if (cand_acc) atomicAdd(stats + 5, cand_acc);
-        if (c1_acc) atomicAdd(stats + 6, c1_acc);
-    }
-}
-
-// Light prep, packed form (the default): the stored-candidate-list scheme of k_prep_list with
-//  * cheap stages in packed fp32 (v_pk_fma_f32): lt_pk[3l..3l+2] = X, Y, Z with
-//    X = (p0.x, p1.x, p2.x, nl.x) etc. and lt_d[l] = float(nl.p0), so that
-//    (t0, t1) = n.(p0, p1) - n.x1 and (t2, s1) = (n.p2 - n.x1, nl.x1 - nl.p0) are four packed
-//    FMA chains; n.x1 is rounded once per node.  The error bound of node_f still holds
-//    (DESIGN.md "light prep numerics");
-//  * dense batches in fp64 from lt_w (p0, p1, p2, lsum as 5 double2, no conversions), evaluated
-//    branch-free (light_weight_bf) on every lane.
+// Cheap stages of the light prep in packed fp32 (v_pk_fma_f32): lt_pk[3l..3l+2] = X, Y, Z with
+// X = (p0.x, p1.x, p2.x, nl.x) etc. and lt_d[l] = float(nl.p0), so that (t0, t1) = n.(p0, p1) - n.x1
+// and (t2, s1) = (n.p2 - n.x1, nl.x1 - nl.p0) are four packed FMA chains; n.x1 is rounded once per
+// node.  The error bound of node_f still holds (DESIGN.md "light prep numerics").  The sure
+// outcomes are predicates; the ambiguous lanes (a value within err of the 1e-8 threshold) take one
+// rarely-taken branch into the exact fp64 reference arithmetic.
 typedef float v2f __attribute__((ext_vector_type(2)));
-__device__ inline int prep_stage_pk(const DScene& S, int li, float4 X, float4 Y, float4 Z, float dl, v2f nx2, v2f ny2,
-                                    v2f nz2, v2f nxs, v2f nys, v2f nzs, float cn, d3 x1, d3 n, float err) {
-    constexpr float kEps = 1e-8f;
-    const v2f tab = __builtin_elementwise_fma(nx2, v2f{X.x, X.y}, __builtin_elementwise_fma(ny2, v2f{Y.x, Y.y}, nz2 * v2f{Z.x, Z.y})) - v2f{cn, cn};
-    const v2f tcs = __builtin_elementwise_fma(nxs, v2f{X.z, X.w}, __builtin_elementwise_fma(nys, v2f{Y.z, Y.w}, nzs * v2f{Z.z, Z.w})) - v2f{cn, dl};
-    const float s1 = tcs.y;
-    if (li >= S.NL) return 3;
-    if (s1 < kEps - err) return 1;
-    const float tm = fmaxf(fmaxf(tab.x, tab.y), tcs.x);
-    if (s1 > kEps + err) {
-        if (tm < kEps - err) return 2;
-        if (tm > kEps + err) return 0;
-    }
-    const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
-    return light_cheap_stage(mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(ln.x, ln.y, ln.z), x1, n);
-}
-// prep_stage_pk with the sure outcomes as predicates and one rarely-taken branch for the
-// ambiguous lanes (exact fp64 reference arithmetic)
 __device__ inline int prep_stage_pk_bf(const DScene& S, int li, float4 X, float4 Y, float4 Z, float dl, v2f nx2,
                                        v2f ny2, v2f nz2, v2f nxs, v2f nys, v2f nzs, float cn, d3 x1, d3 n, float err) {
     constexpr float kEps = 1e-8f;
@@ -1202,150 +1041,9 @@ __device__ inline int prep_stage_pk_bf(const DScene& S, int li, float4 X, float4
     }
     return stage;
 }
-// prep_stage_pk_bf with the fp64 node loaded only on the (rare) ambiguous path
-__device__ inline int prep_stage_pk_bf_lazy(const DScene& S, int li, float4 X, float4 Y, float4 Z, float dl, v2f nx2,
-                                            v2f ny2, v2f nz2, v2f nxs, v2f nys, v2f nzs, float cn, const double* px1,
-                                            const double* pn, float err) {
-    constexpr float kEps = 1e-8f;
-    const v2f tab = __builtin_elementwise_fma(nx2, v2f{X.x, X.y}, __builtin_elementwise_fma(ny2, v2f{Y.x, Y.y}, nz2 * v2f{Z.x, Z.y})) - v2f{cn, cn};
-    const v2f tcs = __builtin_elementwise_fma(nxs, v2f{X.z, X.w}, __builtin_elementwise_fma(nys, v2f{Y.z, Y.w}, nzs * v2f{Z.z, Z.w})) - v2f{cn, dl};
-    const float s1 = tcs.y;
-    const float tm = fmaxf(fmaxf(tab.x, tab.y), tcs.x);
-    const float lo = kEps - err, hi = kEps + err;
-    const bool s1_out = s1 < lo, s1_in = s1 > hi, t_out = tm < lo, t_in = tm > hi;
-    int stage = li >= S.NL ? 3 : s1_out ? 1 : (s1_in && t_out) ? 2 : (s1_in && t_in) ? 0 : -1;
-    if (stage < 0) {
-        const double4 ln = S.lt_n[li];  // ambiguous: exact reference arithmetic
-        stage = light_cheap_stage(mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(ln.x, ln.y, ln.z),
-                                  mk3(px1[0], px1[1], px1[2]), mk3(pn[0], pn[1], pn[2]));
-    }
-    return stage;
-}
-__device__ inline double prep_weight_pk(const DScene& S, int li, d3 x1, bool* ok) {
-    const double2* w = S.lt_w + 5 * li;
-    const double2 a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
-    return light_weight_bf(mk3(a.x, a.y, b.x), mk3(b.y, c.x, c.y), mk3(d.x, d.y, e.x), e.y, x1, ok);
-}
 
-template <int kMinWavesPerSimd>
-__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
-                                                 const double* __restrict__ qn, const int* __restrict__ qpixel,
-                                                 const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
-                                                 const double* __restrict__ u_override, double* __restrict__ wsum_out,
-                                                 int* __restrict__ pick_out, int* __restrict__ count_out,
-                                                 unsigned long long* stats, int nchunks, int wave_bytes,
-                                                 unsigned* __restrict__ work) {
-    extern __shared__ double prep_lds[];
-    const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
-    double* bt = reinterpret_cast<double*>(reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes);
-    unsigned short* lst = reinterpret_cast<unsigned short*>(bt + nchunks);
-    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0;
-    int grab = 0, left = 0;
-    while (true) {
-        if (left == 0) {
-            unsigned b = 0;
-            if (lane == 0) b = atomicAdd(work, (unsigned)kPrepGrab);
-            grab = __shfl((int)b, 0);
-            left = kPrepGrab;
-        }
-        const int node = grab++;
-        left--;
-        if (node >= n) break;
-        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
-        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
-        const NodeF nf = node_f(x1, nn, S.light_bound);
-        const float cn = (float)dot(nn, x1);
-        const v2f nx2{nf.nx, nf.nx}, ny2{nf.ny, nf.ny}, nz2{nf.nz, nf.nz};
-        const v2f nxs{nf.nx, nf.x}, nys{nf.ny, nf.y}, nzs{nf.nz, nf.z};
-        int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
-        for (int c = 0; c < nchunks; c++) {
-            const int li = c * 64 + lane;
-            const int lc = li < S.NL ? li : S.NL - 1;
-            const float4 X = S.lt_pk[3 * lc], Y = S.lt_pk[3 * lc + 1], Z = S.lt_pk[3 * lc + 2];
-            const float dl = S.lt_d[lc];
-            const int stage = prep_stage_pk(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
-            const uint64_t m = __ballot(stage == 0);
-            if (stage == 0) lst[ncand + __popcll(m & lt_mask)] = (unsigned short)li;
-            ncand += __popcll(m);
-            culled1 += __popcll(__ballot(stage == 1));
-            while (ncand - 64 * nb >= 64 || (c == nchunks - 1 && ncand > 64 * nb)) {
-                wave_lds_sync();
-                const int k = 64 * nb + lane;
-                const bool act = k < ncand;
-                bool ok;
-                double w = prep_weight_pk(S, act ? (int)lst[k] : 0, x1, &ok);
-                ok = ok && act;
-                w = act ? w : 0.0;
-                const double sc = wave_incl_scan(w, lane);
-                survivors += __popcll(__ballot(ok));
-                if (lane == 63) bt[nb] = sc;
-                nb++;
-            }
-        }
-        wave_lds_sync();
-        double wsum = 0;
-        for (int b = 0; b < nb; b++) wsum += bt[b];
-        int pick = -1;
-        if (!(fabs(wsum) < MCPT_EPS)) {
-            double u;
-            if (u_override) u = u_override[node];
-            else u = counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-            const double target = u * wsum;
-            int kb = -1, lastpos = -1;
-            double cum = 0, base = 0;
-            for (int b = 0; b < nb; b++) {
-                const double nxt = cum + bt[b];
-                if (bt[b] > 0) lastpos = b;
-                if (kb < 0 && nxt >= target && bt[b] > 0) {
-                    kb = b;
-                    base = cum;
-                }
-                cum = nxt;
-            }
-            if (kb < 0) {
-                kb = lastpos;
-                base = 0;
-                for (int b = 0; b < kb; b++) base += bt[b];
-            }
-            const int k = 64 * kb + lane;
-            const bool act = k < ncand;
-            const int lj = act ? (int)lst[k] : 0;
-            bool ok;
-            double w = prep_weight_pk(S, lj, x1, &ok);
-            ok = ok && act;
-            w = act ? w : 0.0;
-            const double sc = wave_incl_scan(w, lane);
-            const uint64_t candm = __ballot(ok && (base + sc >= target));
-            const uint64_t okm = __ballot(ok);
-            int pl = -1;
-            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-            else if (okm) pl = 63 - __clzll((long long)okm);
-            if (pl >= 0) pick = __shfl(lj, pl);
-        }
-        if (lane == 0) {
-            wsum_out[node] = wsum;
-            pick_out[node] = pick;
-            if (count_out) count_out[node] = survivors;
-        }
-        surv_acc += survivors;
-        cand_acc += ncand;
-        c1_acc += culled1;
-        wave_lds_sync();
-    }
-    if (lane == 0 && stats) {
-        if (surv_acc) atomicAdd(stats + 1, surv_acc);
-        if (cand_acc) atomicAdd(stats + 5, cand_acc);
-        if (c1_acc) atomicAdd(stats + 6, c1_acc);
-    }
-}
-
-// k_prep_pk with (a) light-table loads through buffer descriptors (32-bit offsets, immediate
-// offsets per vertex row, hardware bounds check returning 0 past the table, so no index clamp);
-// (b) v_mbcnt for the list slot; (c) the batch totals searched lane-parallel: lane b holds batch b's
-// total, one wave scan gives every cumulative sum, the target batch is a ballot.  weights_sum is the
-// scan's total (summation order differs from the sequential one only by rounding).
+// Light-table loads through buffer descriptors (32-bit offsets, immediate offsets per vertex row,
+// hardware bounds check returning 0 past the table, so no index clamp).
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr int kBufFlags = 0x00020000;  // gfx9 raw buffer descriptor word 3
 __device__ inline float4 u4f(v4u v) {
@@ -1450,69 +1148,14 @@ __device__ inline double prep_select(const double* bt, const unsigned short* lst
 }
 
 constexpr int kChunkUnroll = 2;
-// chunk splits of k_prep_cull_lanes: enough waves for ~8 per SIMD (1024 SIMDs), at most 4 splits
-// and at least 4 chunks per split; MCPT_CULL_SPLITS overrides (A/B)
+// chunk splits of k_prep_cull_lanes (more waves in flight to hide the table's scalar-load latency):
+// 4, at least 4 chunks per split; MCPT_CULL_SPLITS overrides (A/B)
 inline int cull_splits(int n, int nchunks) {
     static const int env = getenv("MCPT_CULL_SPLITS") ? atoi(getenv("MCPT_CULL_SPLITS")) : 0;
-    const int waves = (n + 63) / 64;
-    int s = env > 0 ? env : (8192 + waves - 1) / std::max(waves, 1);
-    return std::max(1, std::min({s, 4, std::max(1, nchunks / 4)}));
+    (void)n;
+    const int s = env > 0 ? env : 4;  // measured: 1 -> 305, 2 -> 316, 3 -> 323, 4 -> 323, 6 -> 321, 8 -> 312 Msamples/s
+    return std::max(1, std::min(s, std::max(1, nchunks / 4)));
 }
-constexpr int kCullNodes = 4;
-// kPinTable (diagnostic variant 13 only, results meaningless): every chunk reads chunk 0's table
-// rows, to measure how much of phase A is L2 -> CU table traffic
-// Phase A of the light prep as a kernel of its own: a wave tests every 64-light chunk against
-// kCullNodes shading nodes, so each chunk's table rows are loaded once for all of them (the L2 ->
-// CU table traffic, ~40% of the fused phase A's time, drops kCullNodes-fold), and stores per node
-// and chunk the ballot word of the candidates (bit l: light 64 c + l passed both cheap stages).
-// Node constants are wave-uniform (scalar registers).
-template <int kNodes>
-__global__ __launch_bounds__(256) void k_prep_cull(DScene S, int n, const double* __restrict__ qp, const double* __restrict__ qn,
-                                                   uint64_t* __restrict__ masks, int nchunks, unsigned long long* stats) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    const int nwaves = gridDim.x * (blockDim.x >> 6);
-    const int ngroups4 = (nchunks + 3) / 4;
-    const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, ngroups4 * 4 * 3072, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, ngroups4 * 4 * 256, kBufFlags);
-    unsigned long long c1_acc = 0;
-    for (int g = wave * kNodes; g < n; g += nwaves * kNodes) {
-        NodeF nf[kNodes];
-        float cn[kNodes];
-#pragma unroll
-        for (int k = 0; k < kNodes; k++) {
-            const int node = min(g + k, n - 1);
-            const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
-            const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
-            nf[k] = node_f(x1, nn, S.light_bound);
-            cn[k] = (float)dot(nn, x1);
-        }
-        for (int c = 0; c < nchunks; c++) {
-            const int li = c * 64 + lane;
-            const float4 X = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48, c * 3072, 0));
-            const float4 Y = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 16, c * 3072, 0));
-            const float4 Z = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 32, c * 3072, 0));
-            const float dl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, lane * 4, c * 256, 0));
-            uint64_t mine = 0;
-#pragma unroll
-            for (int k = 0; k < kNodes; k++) {
-                const NodeF& f = nf[k];
-                const v2f nx2{f.nx, f.nx}, ny2{f.ny, f.ny}, nz2{f.nz, f.nz};
-                const v2f nxs{f.nx, f.x}, nys{f.ny, f.y}, nzs{f.nz, f.z};
-                const int node = min(g + k, n - 1);
-                // the exact fallback reloads the fp64 node (rare: a value within err of 1e-8)
-                const int stage = prep_stage_pk_bf_lazy(S, li, X, Y, Z, dl, nx2, ny2, nz2, nxs, nys, nzs, cn[k], qp + 3 * node,
-                                                        qn + 3 * node, f.err);
-                const uint64_t m = __ballot(stage == 0);
-                mine = lane == k ? m : mine;
-                if (g + k < n) c1_acc += __popcll(__ballot(stage == 1));
-            }
-            if (lane < kNodes && g + lane < n) masks[(size_t)(g + lane) * nchunks + c] = mine;
-        }
-    }
-    if (lane == 0 && stats && c1_acc) atomicAdd(stats + 6, c1_acc);
-}
-
 // Phase A with a lane per shading node and the light table in scalar registers: each light pair
 // (LightPair, two s_load_dwordx16) is read once per 64 nodes from the scalar cache, and the two
 // cheap stages of both lights run as 13 v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 with one
@@ -1638,7 +1281,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
 
-template <int kMinWavesPerSimd, bool kBuild, bool kPinTable = false, bool kMaskIn = false>
+template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
@@ -1698,7 +1341,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             float dl[kChunkUnroll];
 #pragma unroll
             for (int q = 0; q < kChunkUnroll; q++) {
-                const int cq = kPinTable ? 0 : c + q;
+                const int cq = c + q;
                 X[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48, cq * 3072, 0));
                 Y[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 16, cq * 3072, 0));
                 Z[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 32, cq * 3072, 0));
@@ -2593,18 +2236,15 @@ int validate_camera(const mcpt_camera* cam) {
 
 int prep_chunks(int NL) { return std::max(1, (NL + 63) / 64); }
 size_t prep_lds_bytes(int nchunks) { return 4 * ((size_t)nchunks * sizeof(double) + kPrepQueue * sizeof(int)); }
-// per-wave bytes of k_prep_list: batch totals + uint16 candidate list, 16-byte aligned
+// per-wave LDS bytes of k_prep_pk2: batch totals + uint16 candidate list, 16-byte aligned
 int prep_list_wave_bytes(int nchunks) { return (int)((nchunks * 8 + nchunks * 64 * 2 + 15) / 16 * 16); }
 constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 
-// the split (cull + eval) light prep used by the renderer: 17 (lane-per-node cull), or 14 (wave per
-// 4 nodes) with MCPT_CULL_TABLE set (A/B switch)
-int split_prep_variant() {
-    static const int v = getenv("MCPT_CULL_TABLE") ? 14 : 17;
-    return v;
-}
-
-// variant: -1 auto (list+prefetch when it fits, else queue), 0 queue, 1 list, 2 list+prefetch
+// Light-prep dispatch.  variant: -1 auto; 0 k_prep (per-wave LDS candidate queue: any N_L); 8
+// k_prep_pk2 (cheap stages + stored LDS candidate list + fp64 batches in one kernel); 9 k_prep_lane
+// (lane per node, N_L <= kSmallNL); 17 k_prep_cull_lanes + k_prep_pk2<mask-in> (the renderer's
+// form: needs the candidate-word scratch `masks`).  Auto: 9 for few lights, else 17 with masks, 8
+// without, 0 when the candidate list does not fit in LDS.  Cache builds run 8 or 17.
 // work: a device word, zeroed here before the launch (the kernel's dynamic node counter)
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
@@ -2613,82 +2253,39 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
-    if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? split_prep_variant() : 8) : 0;  // A/B: tools/prep_variants.py
+    if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? 17 : 8) : 0;  // A/B: tools/prep_variants.py
+    if (variant != 0 && variant != 8 && variant != 9 && variant != 17) return hipErrorInvalidValue;
     if (variant == 9) {
         hipLaunchKernelGGL(k_prep_lane, dim3((n + 255) / 256), dim3(256), 0, st, d, seed, n, qp, qn, qpixel, qsample, qnode,
                            u, wsum, pick, count, stats);
         return hipGetLastError();
     }
     if (variant > 0 && !list_ok) variant = 0;
-    if (variant >= 14 && variant <= 17 && !masks) variant = 8;  // the split form needs the candidate-word scratch
-    if (cache.build && variant != 8 && variant != 14 && variant != 17) return hipErrorInvalidValue;  // built by 8 / 14 / 17
+    if (variant == 17 && !masks) variant = 8;  // the split form needs the candidate-word scratch
+    if (cache.build && variant != 8 && variant != 17) return hipErrorInvalidValue;
     // enough 4-wave blocks to fill every CU twice over; the work counter balances the load
     const int blocks = std::max(1, std::min((n + 4 * kPrepGrab - 1) / (4 * kPrepGrab), 2048));
     hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
     if (e != hipSuccess) return e;
-#define MCPT_PREP_LIST(PF, W)                                                                                \
-    hipLaunchKernelGGL((k_prep_list<PF, W>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample, \
-                       qnode, u, wsum, pick, count, stats, nchunks, wb, work)
-    switch (variant) {
-        case 0:
-            hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
-                               qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
-            break;
-        case 1: MCPT_PREP_LIST(false, 1); break;
-        case 2: MCPT_PREP_LIST(true, 1); break;
-        case 3: MCPT_PREP_LIST(false, 5); break;
-        case 4: MCPT_PREP_LIST(false, 6); break;
-        case 5: MCPT_PREP_LIST(true, 5); break;
-        case 6:
-            hipLaunchKernelGGL((k_prep_pk<5>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
-                               qnode, u, wsum, pick, count, stats, nchunks, wb, work);
-            break;
-        case 7:
-            hipLaunchKernelGGL((k_prep_pk<4>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample,
-                               qnode, u, wsum, pick, count, stats, nchunks, wb, work);
-            break;
-        case 14:  // split phase A (k_prep_cull, kCullNodes nodes per table pass) + phase B / pick
-        case 15:  // A/B: 2 nodes per table pass
-        case 16:  // A/B: 8 nodes per table pass
-        case 17: {  // phase A lane per node (k_prep_cull_lanes, light table in scalar registers)
-            const int kn = variant == 15 ? 2 : variant == 16 ? 8 : kCullNodes;
-            const int cblocks = std::max(1, std::min((n + 4 * kn - 1) / (4 * kn), 4096));
-            if (variant == 17)
-                hipLaunchKernelGGL(k_prep_cull_lanes, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d, n, qp, qn, masks, nchunks,
-                                   stats);
-            else if (kn == 2)
-                hipLaunchKernelGGL((k_prep_cull<2>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
-            else if (kn == 8)
-                hipLaunchKernelGGL((k_prep_cull<8>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
-            else
-                hipLaunchKernelGGL((k_prep_cull<kCullNodes>), dim3(cblocks), dim3(256), 0, st, d, n, qp, qn, masks, nchunks, stats);
-            if (cache.build)
-                hipLaunchKernelGGL((k_prep_pk2<5, true, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
-                                   qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
-            else
-                hipLaunchKernelGGL((k_prep_pk2<5, false, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
-                                   qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
-            break;
-        }
-        case 13:  // diagnostic only: table loads pinned to chunk 0 (timing, results meaningless)
-            hipLaunchKernelGGL((k_prep_pk2<5, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
-                               qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
-            break;
-        case 10:  // A/B: variant 8 at 6 waves/SIMD
-            hipLaunchKernelGGL((k_prep_pk2<6, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
-                               qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
-            break;
-        case 8:
-            if (cache.build)
-                hipLaunchKernelGGL((k_prep_pk2<5, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
-                                   qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
-            else
-                hipLaunchKernelGGL((k_prep_pk2<5, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
-                                   qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
-            break;
-        default: MCPT_PREP_LIST(false, 1); break;
+    if (variant == 0) {
+        hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
+                           qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
+    } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
+        hipLaunchKernelGGL(k_prep_cull_lanes, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d, n, qp,
+                           qn, masks, nchunks, stats);
+        if (cache.build)
+            hipLaunchKernelGGL((k_prep_pk2<5, true, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
+                               qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
+        else
+            hipLaunchKernelGGL((k_prep_pk2<5, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
+                               qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
+    } else if (cache.build) {
+        hipLaunchKernelGGL((k_prep_pk2<5, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+                           qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
+    } else {
+        hipLaunchKernelGGL((k_prep_pk2<5, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+                           qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
     }
-#undef MCPT_PREP_LIST
     return hipGetLastError();
 }
 
@@ -2739,11 +2336,6 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     P.fb = dfb;
     P.stats = (unsigned long long*)D.stats.p;
     P.mode = o->mode;
-    HIP_OK(hipMemsetAsync(D.stats.p, 0, 64, st));
-    HIP_OK(hipEventRecord(D.ev0, st));
-    hipLaunchKernelGGL(k_primary, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, D.d, cf,
-                       (int*)D.hit_f.p, (double*)D.hit_tbg.p);
-    HIP_OK(hipGetLastError());
     const int nchunks = prep_chunks(D.d.NL);
     const size_t prep_lds = prep_lds_bytes(nchunks);
     if (prep_lds > 160 * 1024) {
@@ -2774,6 +2366,16 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         pc.lst = (unsigned short*)D.cache_lst.p;
         pc.info = (int4*)D.cache_info.p;
         pc.lstride = lstride;
+        pc.use = 1;  // built below, inside the timed region
+    }
+    // every buffer is allocated above (first-call hipMalloc of the cache is not device work); the
+    // timed region (seconds, HIP events) starts at the primary-hit kernel
+    HIP_OK(hipMemsetAsync(D.stats.p, 0, 64, st));
+    HIP_OK(hipEventRecord(D.ev0, st));
+    hipLaunchKernelGGL(k_primary, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, D.d, cf,
+                       (int*)D.hit_f.p, (double*)D.hit_tbg.p);
+    HIP_OK(hipGetLastError());
+    if (pc.use) {
         HIP_OK(hipMemsetAsync(qb.count, 0, 4, st));
         hipLaunchKernelGGL(k_root_points, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
                            (const double*)D.hit_tbg.p, qb);
@@ -2784,7 +2386,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (nr > 0) {
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
-            HIP_OK(launch_prep(masks ? split_prep_variant() : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
+            HIP_OK(launch_prep(masks ? 17 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
                                nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks));
             HIP_OK(hipEventRecord(D.evp1, st));
             HIP_OK(hipEventSynchronize(D.evp1));
@@ -2893,6 +2495,11 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             prep_ms += ms;
         }
         std::swap(cur, nxt);
+        if (o->progress && o->progress(o->progress_user, (uint64_t)rnext, (uint64_t)R)) {
+            HIP_OK(hipStreamSynchronize(st));
+            set_error("render cancelled by the progress callback after %lld of %lld camera samples", rnext, R);
+            return MCPT_E_CANCELLED;
+        }
     }
     HIP_OK(hipEventRecord(D.ev1, st));
     HIP_OK(hipEventSynchronize(D.ev1));

@@ -198,3 +198,21 @@ def test_render_device_buffer_with_torch(scene):
     host, _ = mcpt.render(scene, cam, 4, seed=SEED)
     assert rel_l2(fb.cpu().numpy(), host) < 1e-12
     assert st.camera_samples == 64 * 48 * 4
+
+
+def test_progress_callback_and_cancel(scene):
+    """mcpt_render_opts.progress (the reference's per-row progress, main.cpp:539-592): monotone
+    reports ending at the call's total; a truthy return cancels with an error."""
+    cam = mcpt.Camera.reference(64, 48)
+    seen = []
+    img, st = mcpt.render(scene, cam, 16, seed=SEED, samples_per_launch=2,
+                          progress=lambda done, total: seen.append((done, total)) and False)
+    total = 64 * 48 * 16
+    assert seen and all(t == total for _, t in seen)
+    assert [d for d, _ in seen] == sorted(d for d, _ in seen) and seen[-1][0] == total
+    ref, _ = mcpt.render(scene, cam, 16, seed=SEED, samples_per_launch=2)
+    assert rel_l2(img, ref) < 1e-12  # fp64 atomic accumulation order only
+    calls = []
+    with pytest.raises(mcpt.MCPTError, match="cancelled"):
+        mcpt.render(scene, cam, 16, seed=SEED, samples_per_launch=2, progress=lambda d, t: calls.append(d) or True)
+    assert len(calls) == 1

@@ -17,7 +17,8 @@ def test_library_exports_every_declared_symbol():
     L = mcpt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.mcpt_version() == 10100
+    assert L.mcpt_version() == mcpt.MCPT_VERSION
+    assert int(re.search(r"#define MCPT_VERSION (\d+)", hdr).group(1)) == mcpt.MCPT_VERSION
 
 
 @pytest.fixture(scope="module")

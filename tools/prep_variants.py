@@ -2,7 +2,7 @@
 """A/B the light-prep kernel variants in one process (interleaved rounds) on the shading points
 of the 800x600 primary hits of the Veach-MIS stand-in.  GPU only.
 
-    python tools/prep_variants.py [--variants 0,1,2] [--rounds 3] [--iters 5]
+    python tools/prep_variants.py [--variants 17,8,0] [--rounds 3] [--iters 5]
 """
 import argparse
 import os
@@ -34,7 +34,7 @@ def shading_points(scene, W=800, H=600):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="17,8,0")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
     args = ap.parse_args()
