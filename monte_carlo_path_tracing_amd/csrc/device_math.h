@@ -246,6 +246,20 @@ __device__ inline double clamp1(double x) { return fmax(-1.0, fmin(1.0, x)); }
 // |z| <= tan(pi/8), fitted in extended precision (tools/fit_atan.py); ~40 instructions instead of
 // ocml's ~100.  Octant reduction: y <= k|x|: z = y/|x|; |x| <= k y: z = -|x|/y (+pi/2);
 // otherwise z = (y-|x|)/(y+|x|) (+pi/4); then pi - r for x < 0.
+// atan(z) for |z| <= tan(pi/8): z + z^3 P(z^2)
+__device__ inline double atan_core(double z) {
+    const double s = z * z;
+    double p = fma_s(0.023022964535612277, s, -0.045054138438556275);
+    p = fma_s(p, s, 0.05743860627393907);
+    p = fma_s(p, s, -0.0665101622857059);
+    p = fma_s(p, s, 0.07691210259772996);
+    p = fma_s(p, s, -0.09090862908839843);
+    p = fma_s(p, s, 0.11111110041613353);
+    p = fma_s(p, s, -0.14285714274661848);
+    p = fma_s(p, s, 0.19999999999980458);
+    p = fma_s(p, s, -0.33333333333333476);
+    return fma(z * s, p, z);
+}
 __device__ inline double atan2_pos(double y, double x) {
     constexpr double k = 0.41421356237309503;  // tan(pi/8)
     const double ax = fabs(x);
@@ -256,18 +270,16 @@ __device__ inline double atan2_pos(double y, double x) {
     const double num = fma(pc, y, -(qc * ax));
     const double den = fma(qc, y, pc * ax);
     const double r0 = qc * fma(-pc, 0.7853981633974483, 1.5707963267948966);
-    const double z = fdiv_pos(num, den), s = z * z;
-    double p = fma_s(0.023022964535612277, s, -0.045054138438556275);
-    p = fma_s(p, s, 0.05743860627393907);
-    p = fma_s(p, s, -0.0665101622857059);
-    p = fma_s(p, s, 0.07691210259772996);
-    p = fma_s(p, s, -0.09090862908839843);
-    p = fma_s(p, s, 0.11111110041613353);
-    p = fma_s(p, s, -0.14285714274661848);
-    p = fma_s(p, s, 0.19999999999980458);
-    p = fma_s(p, s, -0.33333333333333476);
-    const double a = r0 + fma(z * s, p, z);
+    const double a = r0 + atan_core(fdiv_pos(num, den));
     return x < 0 ? 3.141592653589793 - a : a;
+}
+// atan2_pos with a wave-uniform fast path: when every active lane is in the first octant (x > 0,
+// y <= tan(pi/8) x -- the spherical triangles of all but the nearest lights), z = y / x directly,
+// without the octant selects.  Bit-identical to atan2_pos there (num = y, den = x, r0 = 0 exactly).
+__device__ inline double atan2_pos_wave(double y, double x) {
+    constexpr double k = 0.41421356237309503;
+    if (__ballot(!(x > 0.0 && y <= k * x)) == 0) return atan_core(fdiv_pos(y, x));
+    return atan2_pos(y, x);
 }
 
 // Weight of one light triangle for the prep kernel (Mylight.cpp:360-413): the same quantity as
@@ -340,7 +352,7 @@ __device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, dou
 __device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, bool* ok) {
     const d3 A = funit(sub(p0, x1)), B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
     const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
-    const double sA = 2.0 * atan2_pos(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
+    const double sA = 2.0 * atan2_pos_wave(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
     const double w = sA * lsum;
     const bool good = (ab < 1.0) & (bc < 1.0) & (ca < 1.0) & (sA > 0) & (w >= 0) & (w <= __DBL_MAX__);
     *ok = good;
