@@ -826,6 +826,38 @@ __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Totals of four 64-lane batches a, b, c, d (gfx950 permlane swaps + one row reduction instead of
+// four full wave scans): returns, in lanes 15 / 31 / 47 / 63, the totals of a / b / c / d.
+//   permlane32_swap(a, c), (b, d): lanes 0-31 of a + c hold a's pair sums (lane l, l+32), lanes
+//   32-63 c's; likewise b + d.  permlane16_swap(p, q) then gathers row r (16 lanes) of p + q =
+//   batch r's sums of four lanes; a row_shr 1/2/4/8 scan leaves each row's total in its lane 15.
+__device__ inline void swap32(double& x, double& y) {
+    const unsigned long long bx = __double_as_longlong(x), by = __double_as_longlong(y);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)bx, (unsigned)by, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(bx >> 32), (unsigned)(by >> 32), false, false);
+    x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+__device__ inline void swap16(double& x, double& y) {
+    const unsigned long long bx = __double_as_longlong(x), by = __double_as_longlong(y);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)bx, (unsigned)by, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(bx >> 32), (unsigned)(by >> 32), false, false);
+    x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+__device__ inline double batch_totals4(double a, double b, double c, double d) {
+    swap32(a, c);
+    swap32(b, d);
+    double p = a + c, q = b + d;
+    swap16(p, q);
+    double r = p + q;
+    r += dpp_shr<0x111>(r);  // row_shr:1
+    r += dpp_shr<0x112>(r);  // row_shr:2
+    r += dpp_shr<0x114>(r);  // row_shr:4
+    r += dpp_shr<0x118>(r);  // row_shr:8
+    return r;
+}
+
 struct PrepLight {
     d3 p0, p1, p2, nl;
     double lsum;
@@ -1359,18 +1391,26 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         }
         }
         wave_lds_sync();
-        // phase B: dense fp64 batches of 64 consecutive candidates
-        for (nb = 0; 64 * nb < ncand; nb++) {
-            const int k = 64 * nb + lane;
-            const bool act = k < ncand;
-            bool ok;
-            double w = prep_weight_buf(rw, act ? (int)lst[k] : 0, x1, &ok);
-            ok = ok && act;
-            w = act ? w : 0.0;
-            if (kBuild && act) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
-            const double sc = wave_incl_scan(w, lane);
-            survivors += __popcll(__ballot(ok));
-            if (lane == 63) bt[nb] = sc;
+        // phase B: dense fp64 batches of 64 consecutive candidates, four at a time (batch_totals4)
+        nb = (ncand + 63) >> 6;
+        for (int b0 = 0; b0 < nb; b0 += 4) {
+            double w4[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                w4[i] = 0.0;
+                if (b0 + i < nb) {  // wave-uniform
+                    const int k = 64 * (b0 + i) + lane;
+                    const bool act = k < ncand;
+                    bool ok;
+                    const double w = prep_weight_buf(rw, act ? (int)lst[k] : 0, x1, &ok);  // 0 if culled
+                    ok = ok && act;
+                    if (kBuild && act) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
+                    w4[i] = act ? w : 0.0;
+                    survivors += __popcll(__ballot(ok));
+                }
+            }
+            const double t = batch_totals4(w4[0], w4[1], w4[2], w4[3]);
+            if ((lane & 15) == 15 && b0 + (lane >> 4) < nb) bt[b0 + (lane >> 4)] = t;
         }
         wave_lds_sync();
         full_acc++;
