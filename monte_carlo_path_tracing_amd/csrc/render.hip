@@ -42,7 +42,7 @@ using namespace mcpt;
 // lights (index >= N_L) have nl = 0, d = 1e30 (light-side culled).  128 B = two s_load_dwordx16.
 struct LightPair {
     float2 nl[3];
-    float2 d;
+    float2 d;      // nl . p0 + 1e-8 of both lights
     float2 p[9];
     float pad[6];
 };
@@ -1213,6 +1213,11 @@ __device__ inline float min_abs_raw(float a, float b) {
     asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+__device__ inline float min3_abs_raw(float a, float b, float c) {  // min(a, |b|, |c|)
+    float r;
+    asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ inline unsigned shift_in(unsigned w, uint64_t carry) {
     unsigned r;
     uint64_t co;
@@ -1226,6 +1231,7 @@ struct CullLane {
     v2f xx, yy, zz, nxx, nyy, nzz, ncn;
     __device__ inline void eval(const LightPair& L, v2f* s, v2f* t) const {
         const v2f nlx{L.nl[0].x, L.nl[0].y}, nly{L.nl[1].x, L.nl[1].y}, nlz{L.nl[2].x, L.nl[2].y};
+        // (the subtraction stays separate: a packed FMA reads at most one scalar operand)
         *s = __builtin_elementwise_fma(xx, nlx, __builtin_elementwise_fma(yy, nly, zz * nlz)) - v2f{L.d.x, L.d.y};
 #pragma unroll
         for (int k = 0; k < 3; k++) {
@@ -1267,7 +1273,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
         for (int h = 0; h < 2; h++) {
             const LightPair* __restrict__ Th = T + 32 * c + 16 * h;
             unsigned w = 0, c1w = 0;
-            uint64_t anyam = 0;
+            float amin = __builtin_inff();  // min over the 32 lights of min(|s|, |min(s, max t)|)
 #pragma unroll 2
             for (int q = 0; q < 16; q++) {
                 v2f s1, t[3];
@@ -1277,12 +1283,12 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
                     const float sv = s1[e];
                     const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
                     // ambiguous lanes (a value within err of the threshold) have s >= -err and a clear bit here
-                    anyam |= __ballot(min_abs_raw(sv, mn) <= err);
+                    amin = min3_abs_raw(amin, sv, mn);
                     c1w += __popcll(__ballot(sv < -err) & actm);
                     w = shift_in(w, __ballot(mn > err));
                 }
             }
-            if (anyam & actm) {  // rare: the reference's exact fp64 stages for the ambiguous (node, light) pairs
+            if (__ballot(amin <= err) & actm) {  // rare: the reference's exact fp64 stages for the ambiguous (node, light) pairs
                 for (int q = 0; q < 16; q++) {
                     v2f s1, t[3];
                     cl.eval(Th[q], &s1, t);
@@ -2189,7 +2195,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
         for (int h = 0; h < 2; h++) {
             const int l = (int)(2 * q) + h;
             if (l >= s.NL) {
-                dd[h] = 1e30f;
+                dd[h] = 1e30f;  // padding: always culled by the light-side test
                 continue;
             }
             const float4 v[3] = {lv[3 * l], lv[3 * l + 1], lv[3 * l + 2]};
