@@ -1198,6 +1198,12 @@ inline int cull_splits(int n, int nchunks) {
 // decisions are the reference's (err as in node_f; the threshold is folded into d and cn).
 // raw v_max3_f32 / v_min_f32 (the builtins canonicalise operands that came out of packed ops
 // first; NaN handling is irrelevant here: a NaN light value never reaches the cull)
+// candidate words in tiles of 8 nodes: word (node, chunk) at (node / 8) [chunk] [node % 8], so the
+// lane-per-node cull writes whole 64-B segments (8 lanes each) and k_prep_pk2's per-node reads of
+// the 8 nodes of a tile (claimed by neighbouring waves at about the same time) hit the same lines
+__device__ inline size_t mask_index(int node, int chunk, int nchunks) {
+    return ((size_t)(node >> 3) * nchunks + chunk) * 8 + (node & 7);
+}
 __device__ inline float max3_raw(float a, float b, float c) {
     float r;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -1312,7 +1318,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
             c1 += c1w;
             word[h] = __builtin_bitreverse32(w);
         }
-        if (act) masks[(size_t)node * nchunks + c] = ((uint64_t)word[1] << 32) | word[0];
+        if (act) masks[mask_index(node, c, nchunks)] = ((uint64_t)word[1] << 32) | word[0];
     }
     // padding lights (index >= N_L, d = 1e30) were counted as light-side culled by every active lane
     if (ce == nchunks) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
@@ -1357,7 +1363,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
         if (kMaskIn) {  // phase A done by k_prep_cull: rebuild the list from the candidate words
             for (int c0 = 0; c0 < nchunks; c0 += 64) {  // one vector load of up to 64 words, then readlanes
-                const unsigned long long mv = c0 + lane < nchunks ? masks[(size_t)node * nchunks + c0 + lane] : 0ull;
+                const unsigned long long mv = c0 + lane < nchunks ? masks[mask_index(node, c0 + lane, nchunks)] : 0ull;
                 const int cend = min(64, nchunks - c0);
                 for (int q = 0; q < cend; q++) {
                     const uint64_t m = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(mv >> 32), q) << 32) |
@@ -2393,7 +2399,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
     if (o->mode != MCPT_MODE_BRDF && D.d.NL > kSmallNL) {
-        if ((rc = ensure(D.masks, (size_t)std::max(cap, npx) * nchunks * 8))) return rc;
+        if ((rc = ensure(D.masks, (size_t)((std::max(cap, npx) + 7) / 8 * 8) * nchunks * 8))) return rc;
         masks = (uint64_t*)D.masks.p;
     }
     // root-point cache (see PrepCache): built here when the call has >= 2 samples per pixel and the
@@ -2789,7 +2795,7 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
     void *dp, *dn, *du, *dw, *dc, *dk, *dm;
-    HIP_OK(hipMalloc(&dm, 8ull * n * prep_chunks(D->d.NL)));  // the render path's split prep (variant 14)
+    HIP_OK(hipMalloc(&dm, 8ull * ((n + 7) / 8 * 8) * prep_chunks(D->d.NL)));  // candidate words of the split prep (variant 17)
     HIP_OK(hipMalloc(&dp, 24ull * n));
     HIP_OK(hipMalloc(&dn, 24ull * n));
     HIP_OK(hipMalloc(&du, 8ull * n));
@@ -2824,7 +2830,7 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
     void *dp, *dn, *du, *dw, *dk, *dm;
-    HIP_OK(hipMalloc(&dm, 8ull * n * prep_chunks(D->d.NL)));
+    HIP_OK(hipMalloc(&dm, 8ull * ((n + 7) / 8 * 8) * prep_chunks(D->d.NL)));
     HIP_OK(hipMalloc(&dp, 24ull * n));
     HIP_OK(hipMalloc(&dn, 24ull * n));
     HIP_OK(hipMalloc(&du, 8ull * n));
