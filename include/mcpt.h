@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 10200 /* 1.2.0 */
+#define MCPT_VERSION 10300 /* 1.3.0 */
 
 enum {
     MCPT_OK = 0,
@@ -37,6 +37,13 @@ enum {
 
 /* shade_with_mis main.cpp:402 / shade_with_brdf :348 / shade :269 (the one main() calls, :575) */
 enum { MCPT_MODE_MIS = 0, MCPT_MODE_BRDF = 1, MCPT_MODE_SHADE = 2 };
+
+/* closest-hit acceleration: the BVH (default; the true closest hit) or the reference's own uniform
+ * grid with its in-cell acceptance rule (Myobj.cpp:78-162, 334-622), crack included -- hit for hit
+ * the reference's traversal, for parity studies (much slower). */
+enum { MCPT_ACCEL_BVH = 0, MCPT_ACCEL_GRID = 1 };
+/* mcpt_closest_hit flags */
+enum { MCPT_HIT_LIGHT_ONLY = 1, MCPT_HIT_GRID = 2 };
 
 typedef struct mcpt_scene mcpt_scene;
 
@@ -80,7 +87,8 @@ typedef struct {
                                  * (0 = auto, 4 Mi nodes) */
     int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2) */
     int32_t device;         /* HIP device ordinal (-1 = current) */
-    int32_t reserved;
+    int32_t accel;          /* MCPT_ACCEL_BVH / MCPT_ACCEL_GRID (grid over the scene and this camera's
+                             * eye with n0 = 100000, main.cpp:501-504; rebuilt when the eye changes) */
     mcpt_progress_fn progress; /* optional (NULL = none) */
     void* progress_user;
 } mcpt_render_opts;
@@ -131,11 +139,19 @@ int mcpt_render(mcpt_scene* scene, const mcpt_camera* cam, const mcpt_render_opt
 int mcpt_render_device(mcpt_scene* scene, const mcpt_camera* cam, const mcpt_render_opts* opts,
                        double* dev_out_rgb, mcpt_stats* stats);
 
+/* Myobj::cal_scene_boundingbox(eye) + Myobj::meshing(n0) (Myobj.cpp:78-162): build the scene's
+ * uniform grid (box of every vertex and `eye`; cell edge = largest extent / n0^(1/3)) for
+ * MCPT_HIT_GRID queries.  Renders with MCPT_ACCEL_GRID build their own for their camera. */
+int mcpt_scene_meshing(mcpt_scene* scene, const double eye[3], int32_t n0);
+/* the current grid: box_and_cell = (xmin, xmax, ymin, ymax, zmin, zmax, cell edge), cells per axis */
+int mcpt_scene_grid_info(const mcpt_scene* scene, double* box_and_cell, int32_t* cells);
+
 /* Myobj::closet_ray_intersect (Myobj.cpp:334) / closet_ray_intersect_light_triangle (:476) for a
  * batch of n rays (host arrays): ro/rd n*3, exclude n (origin facet, -1 none) ->
- * facet (or -1) and t, beta, gamma (n*3). */
+ * facet (or -1) and t, beta, gamma (n*3).  flags: MCPT_HIT_LIGHT_ONLY (the light-only query),
+ * MCPT_HIT_GRID (the reference's grid of mcpt_scene_meshing instead of the BVH). */
 int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const double* rd, const int32_t* exclude,
-                     int32_t light_only, int32_t* facet, double* tbg);
+                     int32_t flags, int32_t* facet, double* tbg);
 /* Mylight::prepared_for_lights_spherical_triangle_sampling (Mylight.cpp:322) at n shading points
  * (x1, normal) -> weights_sum, survivor count, and the FACET of the light triangle picked by the
  * counter-RNG rule for uniform u[k] (first survivor with cumulative weight >= u*weights_sum;

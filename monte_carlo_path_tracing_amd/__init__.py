@@ -16,13 +16,15 @@ import os
 import numpy as np
 
 __all__ = ["Scene", "Camera", "render", "render_device", "closest_hit", "light_prep", "primary_hits",
-           "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "MODE_SHADE", "Stats", "MCPTError", "LIB_PATH", "lib"]
+           "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "MODE_SHADE", "ACCEL_BVH", "ACCEL_GRID", "Stats", "MCPTError", "LIB_PATH", "lib"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmcpt_hip.so")
 MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2  # shade_with_mis / shade_with_brdf / shade (main.cpp:402/348/269)
+ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
+HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
 DEFAULT_SEED = 20240430
-MCPT_VERSION = 10200  # include/mcpt.h MCPT_VERSION this mirror is written against
+MCPT_VERSION = 10300  # include/mcpt.h MCPT_VERSION this mirror is written against
 
 
 class MCPTError(RuntimeError):
@@ -50,7 +52,7 @@ class Camera(C.Structure):
 class RenderOpts(C.Structure):
     _fields_ = [("spp", C.c_int32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32), ("mode", C.c_int32),
                 ("seed", C.c_uint64), ("samples_per_launch", C.c_int32), ("queue_factor", C.c_int32),
-                ("device", C.c_int32), ("reserved", C.c_int32), ("progress", C.c_void_p),
+                ("device", C.c_int32), ("accel", C.c_int32), ("progress", C.c_void_p),
                 ("progress_user", C.c_void_p)]
 
 
@@ -73,7 +75,8 @@ _lib = None
 
 # every symbol include/mcpt.h declares (tests check the .so exports them all)
 EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_create", "mcpt_scene_destroy",
-           "mcpt_scene_counts", "mcpt_scene_arrays", "mcpt_scene_camera", "mcpt_render", "mcpt_render_device",
+           "mcpt_scene_counts", "mcpt_scene_arrays", "mcpt_scene_camera", "mcpt_scene_meshing", "mcpt_scene_grid_info",
+           "mcpt_render", "mcpt_render_device",
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_debug_prep_bench", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp"]
 
@@ -108,6 +111,8 @@ def lib():
         L.mcpt_scene_counts.argtypes = [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]
         L.mcpt_scene_arrays.argtypes = [P, fp, fp, ip, fp, ip, dp, dp]
         L.mcpt_scene_camera.argtypes = [P, C.POINTER(Camera)]
+        L.mcpt_scene_meshing.argtypes = [P, dp, I]
+        L.mcpt_scene_grid_info.argtypes = [P, dp, ip]
         L.mcpt_render.argtypes = [P, C.POINTER(Camera), C.POINTER(RenderOpts), dp, C.POINTER(Stats)]
         L.mcpt_render_device.argtypes = [P, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p, C.POINTER(Stats)]
         L.mcpt_closest_hit.argtypes = [P, I, dp, dp, ip, I, ip, dp]
@@ -161,15 +166,30 @@ class Scene:
         return dict(positions=pos, normals=nrm, material_id=mat, materials=mtl, light_facet=lf[:NL],
                     light_radiance=lr[:NL], unique_normal=un)
 
+    def meshing(self, eye, n0=100000):
+        """Myobj::cal_scene_boundingbox(eye) + Myobj::meshing(n0) (Myobj.cpp:78-162): the reference's
+        uniform grid, for closest_hit(..., grid=True)."""
+        _check(lib().mcpt_scene_meshing(self.h, _d(eye, (3,)), int(n0)))
+
+    def grid_info(self):
+        """((xmin, xmax, ymin, ymax, zmin, zmax, cell edge), cells per axis) of the current grid"""
+        box, cells = np.zeros(7), np.zeros(3, np.int32)
+        _check(lib().mcpt_scene_grid_info(self.h, box, cells))
+        return box, cells
+
     def camera(self):
         c = Camera()
         _check(lib().mcpt_scene_camera(self.h, C.byref(c)))
         return c
 
 
-def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress=None):
+def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress=None, accel="bvh"):
     """progress(done, total) -> truthy to cancel; the ctypes thunk is kept on the returned struct."""
     o = RenderOpts()
+    a = {"bvh": ACCEL_BVH, "grid": ACCEL_GRID}.get(accel, -1) if isinstance(accel, str) else int(accel)
+    if a not in (ACCEL_BVH, ACCEL_GRID):
+        raise ValueError("accel must be 'bvh' or 'grid'")
+    o.accel = a
     if progress is not None:
         o._thunk = PROGRESS_FN(lambda _u, done, total: 1 if progress(int(done), int(total)) else 0)
         o.progress = C.cast(o._thunk, C.c_void_p)
@@ -188,37 +208,41 @@ def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_facto
 
 
 def render(scene, camera, spp, mode="mis", seed=DEFAULT_SEED, sample_range=None, out=None, device=None,
-           samples_per_launch=0, queue_factor=0, progress=None):
+           samples_per_launch=0, queue_factor=0, progress=None, accel="bvh"):
     """render(scene, camera, spp, mode) -- main.cpp:547-588.  Returns (H x W x 3 fp64 radiance, Stats).
 
     Adds sum_k L_k / spp over samples k in `sample_range` (default all) into `out` (zeros if None).
     progress(samples_dispatched, samples_total), called after every wavefront generation, replaces
-    the reference's per-row progress output; a truthy return cancels (MCPTError, partial sum)."""
+    the reference's per-row progress output; a truthy return cancels (MCPTError, partial sum).
+    accel="grid" traces every ray through the reference's uniform grid (Myobj.cpp:78-162) instead of
+    the BVH: hit-for-hit the reference's traversal, crack included."""
     if out is None:
         out = np.zeros((camera.height, camera.width, 3))
     assert out.dtype == np.float64 and out.flags.c_contiguous and out.shape == (camera.height, camera.width, 3)
     st = Stats()
-    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress)
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel)
     _check(lib().mcpt_render(scene.h, C.byref(camera), C.byref(o), out.reshape(-1), C.byref(st)))
     return out, st
 
 
 def render_device(scene, camera, spp, dev_ptr, mode="mis", seed=DEFAULT_SEED, sample_range=None, device=None,
-                  samples_per_launch=0, queue_factor=0, progress=None):
+                  samples_per_launch=0, queue_factor=0, progress=None, accel="bvh"):
     """Accumulate into a device buffer of H*W*3 doubles (e.g. a torch.float64 CUDA tensor's data_ptr())."""
     st = Stats()
-    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress)
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel)
     _check(lib().mcpt_render_device(scene.h, C.byref(camera), C.byref(o), C.c_void_p(int(dev_ptr)), C.byref(st)))
     return st
 
 
-def closest_hit(scene, ro, rd, exclude=None, light_only=False):
-    """Myobj::closet_ray_intersect (Myobj.cpp:334) / ..._light_triangle (:476) for a batch of rays."""
+def closest_hit(scene, ro, rd, exclude=None, light_only=False, grid=False):
+    """Myobj::closet_ray_intersect (Myobj.cpp:334) / ..._light_triangle (:476) for a batch of rays.
+    grid=True traverses the reference's uniform grid of Scene.meshing (crack included), else the BVH."""
     ro, rd = _d(ro, (-1, 3)), _d(rd, (-1, 3))
     n = ro.shape[0]
     ex = np.full(n, -1, np.int32) if exclude is None else np.ascontiguousarray(exclude, np.int32)
     f, tbg = np.zeros(n, np.int32), np.zeros((n, 3))
-    _check(lib().mcpt_closest_hit(scene.h, n, ro, rd, ex, int(bool(light_only)), f, tbg))
+    flags = (HIT_LIGHT_ONLY if light_only else 0) | (HIT_GRID if grid else 0)
+    _check(lib().mcpt_closest_hit(scene.h, n, ro, rd, ex, flags, f, tbg))
     return f, tbg
 
 

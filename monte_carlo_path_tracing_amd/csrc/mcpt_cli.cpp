@@ -6,6 +6,8 @@
 //
 //   mcpt_render --scene scenes/veach-mis/veach-mis [--width 1280 --height 720] [--spp 10]
 //               [--mode mis|brdf|shade] [--seed 20240430] [--out test.bmp] [--hdr out.pfm] [--progress]
+//               [--grid]
+//   --grid traverses the reference's uniform grid (Myobj.cpp:78-162, n0 = 100000) instead of the BVH.
 //   --progress prints the share of camera samples dispatched (the reference prints per-row progress
 //   and updates its EasyX window, main.cpp:539-592) through mcpt_render_opts.progress.
 #include <chrono>
@@ -31,7 +33,7 @@ int print_progress(void* user, uint64_t done, uint64_t total) {
 }
 
 // render(scene, camera, spp, mode): main.cpp:547-588 lifted into a function.
-int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, bool progress,
+int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, bool progress, bool grid,
            std::vector<double>& hdr, mcpt_stats* st) {
     hdr.assign(3ull * cam.width * cam.height, 0.0);
     mcpt_render_opts o{};
@@ -39,6 +41,7 @@ int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_
     o.mode = mode;
     o.seed = seed;
     o.device = -1;
+    o.accel = grid ? MCPT_ACCEL_GRID : MCPT_ACCEL_BVH;
     int last = -10;
     if (progress) {
         o.progress = print_progress;
@@ -67,7 +70,7 @@ int main(int argc, char** argv) {
     int W = 1280, H = 720, spp = 10, mode = MCPT_MODE_MIS;
     double dist_scale = 2.0;
     uint64_t seed = 20240430;
-    bool xml_cam = false, progress = false;
+    bool xml_cam = false, progress = false, grid = false;
     for (int a = 1; a < argc; a++) {
         auto next = [&]() -> const char* {
             if (a + 1 >= argc) {
@@ -96,6 +99,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[a], "--dist-scale")) dist_scale = std::atof(next());
         else if (!std::strcmp(argv[a], "--xml-camera")) xml_cam = true;
         else if (!std::strcmp(argv[a], "--progress")) progress = true;
+        else if (!std::strcmp(argv[a], "--grid")) grid = true;
         else {
             std::fprintf(stderr, "unknown option %s\n", argv[a]);
             return 2;
@@ -123,7 +127,7 @@ int main(int argc, char** argv) {
     std::vector<double> hdr;
     mcpt_stats st{};
     const auto t0 = std::chrono::steady_clock::now();
-    if (render(scene, cam, spp, mode, seed, progress, hdr, &st) != MCPT_OK) {
+    if (render(scene, cam, spp, mode, seed, progress, grid, hdr, &st) != MCPT_OK) {
         std::fprintf(stderr, "render failed: %s\n", mcpt_last_error());
         return 1;
     }

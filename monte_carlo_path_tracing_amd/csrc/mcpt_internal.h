@@ -63,6 +63,19 @@ struct BvhNode4 {
 // four children); leaves and leaf slots are shared with the binary tree
 std::vector<BvhNode4> collapse_bvh4(const Bvh& b);
 
+// grid.cpp -- the reference's uniform grid (Myobj.cpp:78-162) for the MCPT_ACCEL_GRID mode
+struct Grid {
+    bool ok = false;
+    double eye[3] = {0, 0, 0};  // camera point the bounding box was built with
+    int n0 = 0;
+    double mn[3], mx[3];        // bounding box of every vertex and the eye
+    double d = 0, inv_d = 0;    // cell edge and its reciprocal
+    int lim[3], gd[3];          // last cell index per axis; cells per axis (lim + 1)
+    std::vector<int32_t> cell_start;  // CSR over cells (x-major, then y, then z)
+    std::vector<int32_t> cell_tri;    // facets per cell, ascending facet id
+};
+Grid build_grid(const HostScene& s, const double eye[3], int n0);
+
 void set_error(const char* fmt, ...);
 
 }  // namespace mcpt

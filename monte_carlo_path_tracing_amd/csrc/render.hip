@@ -70,6 +70,11 @@ struct DScene {
     const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves)
     const BvhNode4* lbvh4;
     const float4* lleaf_v;
+    // reference uniform grid (MCPT_ACCEL_GRID; null until mcpt_scene_meshing / a grid render)
+    const int* g_start;       // CSR cell -> facets
+    const int* g_tri;
+    double g_mn[3], g_inv_d;
+    int g_lim[3], g_gd[3];
 };
 
 struct CamFrame {
@@ -481,6 +486,81 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     return best;
 }
 
+// x86 cvttsd2si semantics for (int)floor(x) of the reference (out of range -> INT_MIN)
+__device__ inline int icvt(double f) { return (f >= -2147483648.0 && f < 2147483648.0) ? (int)f : (int)0x80000000u; }
+__device__ inline int ifloor(double x) { return icvt(floor(x)); }
+// Myobj::closet_ray_intersect (Myobj.cpp:334-474) and closet_ray_intersect_light_triangle (:476-622)
+// on the reference's uniform grid, in its arithmetic: a 3D-DDA from the cell holding the origin
+// (no clipping to the box: an origin outside it, or rounding to cell -1 on the box's min face, is a
+// miss -- the reference's "crack"); in each cell every listed facet except the origin facet gets
+// the fp64 Cramer test, and a hit counts only if its point lies in the current cell; the first
+// cell with a counted hit returns its nearest (first listed on ties).  light_only skips non-light
+// facets and steps every axis whose crossing ties the nearest within 1e-8 (:576-604).
+__device__ inline Hit grid_trace(const DScene& S, d3 ro, d3 rd, int exclude, bool light_only) {
+    Hit best{-1, DBL_MAX, 0, 0};
+    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
+    const d3 mn = mk3(S.g_mn[0], S.g_mn[1], S.g_mn[2]);
+    const d3 x0 = mul(sub(ro, mn), S.g_inv_d);
+    const double xyz0[3] = {x0.x, x0.y, x0.z}, dir[3] = {rd.x, rd.y, rd.z};
+    int xyz[3], sign[3], nxyz[3];
+    double ts[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        xyz[i] = ifloor(xyz0[i]);
+        sign[i] = dir[i] < 0 ? -1 : 1;
+        if (fabs(dir[i]) < MCPT_EPS) sign[i] = 0;
+        if (sign[i]) {
+            if (fabs(floor(xyz0[i]) - xyz0[i]) < MCPT_EPS) nxyz[i] = xyz[i] + sign[i];
+            else nxyz[i] = sign[i] > 0 ? icvt(ceil(xyz0[i])) : ifloor(xyz0[i]);
+            ts[i] = (nxyz[i] - xyz0[i]) / dir[i];
+        } else {
+            nxyz[i] = -1;
+            ts[i] = DBL_MAX;
+        }
+    }
+    for (;;) {
+        for (int i = 0; i < 3; i++)
+            if (xyz[i] < 0 || xyz[i] > S.g_lim[i]) return best;
+        const size_t c = ((size_t)xyz[0] * S.g_gd[1] + xyz[1]) * S.g_gd[2] + xyz[2];
+        const int q1 = S.g_start[c + 1];
+        for (int q = S.g_start[c]; q < q1; q++) {
+            const int f = S.g_tri[q];
+            if (light_only && S.tri_light[f] < 0) continue;
+            if (f == exclude) continue;
+            const TriHit h = tri_hit(f3(S.tri_v[3 * f]), f3(S.tri_v[3 * f + 1]), f3(S.tri_v[3 * f + 2]), ro, rd);
+            if (!h.hit) continue;
+            const d3 cp = mul(sub(add(ro, mul(rd, h.t)), mn), S.g_inv_d);
+            if (ifloor(cp.x) != xyz[0] || ifloor(cp.y) != xyz[1] || ifloor(cp.z) != xyz[2]) continue;
+            if (h.t < best.t) best = Hit{f, h.t, h.beta, h.gamma};
+        }
+        if (best.f >= 0) return best;
+        if (!light_only) {
+            double t = DBL_MAX;
+            int ind = -1;
+            for (int i = 0; i < 3; i++)
+                if (sign[i] != 0 && ts[i] < t) {
+                    ind = i;
+                    t = ts[i];
+                }
+            if (ind < 0) return best;
+            xyz[ind] += sign[ind];
+            nxyz[ind] += sign[ind];
+            ts[ind] = (nxyz[ind] - xyz0[ind]) / dir[ind];
+        } else {
+            double t = DBL_MAX;
+            for (int i = 0; i < 3; i++)
+                if (ts[i] < t) t = ts[i];
+            if (t == DBL_MAX) return best;
+            for (int i = 0; i < 3; i++)
+                if (fabs(t - ts[i]) < MCPT_EPS) {
+                    xyz[i] += sign[i];
+                    nxyz[i] += sign[i];
+                    ts[i] = (nxyz[i] - xyz0[i]) / dir[i];
+                }
+        }
+    }
+}
+
 // ============================================================================================
 // wavefront queue (SoA)
 // ============================================================================================
@@ -640,6 +720,7 @@ __device__ inline void node_entry(const Params& P, bool active, int f, double be
 // ============================================================================================
 // kernels
 // ============================================================================================
+template <bool kGrid>
 __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam, int* hit_f, double* hit_tbg) {
     __shared__ int stack[kRayLds * kTraceBlock];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -647,7 +728,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
     if (idx >= npx) return;
     const int i = idx / cam.W, j = idx % cam.W;
     const d3 dir = cam_dir(cam, i, j);
-    Hit h = trace4_ww<kRayLds>(S.bvh4, S.leaf_v, cam.eye, dir, -1, stack + threadIdx.x, kTraceBlock);
+    const Hit h = kGrid ? grid_trace(S, cam.eye, dir, -1, false)
+                        : trace4_ww<kRayLds>(S.bvh4, S.leaf_v, cam.eye, dir, -1, stack + threadIdx.x, kTraceBlock);
     hit_f[idx] = h.f;
     hit_tbg[3 * idx] = h.f >= 0 ? h.t : 0.0;
     hit_tbg[3 * idx + 1] = h.f >= 0 ? h.beta : 0.0;
@@ -1467,7 +1549,7 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
                                                    unsigned long long* stats, int nchunks, PrepCache C) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (blockDim.x >> 6);
-    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));  // wave-uniform: scalar loads and SALU hashing
     unsigned long long cached = 0;
     // static assignment: a root costs ~the same everywhere, and a shared work counter would
     // serialise on its one address at this node rate
@@ -1728,7 +1810,7 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 
 // closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
 // queue's shading points, excluding the origin facet
-template <bool kWhileWhile>
+template <bool kWhileWhile, bool kGrid = false>
 __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set) {
     __shared__ int stack[kRayLds * kRayBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1743,7 +1825,9 @@ __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, 
         const d3 rd = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
         const float4* leafv = set == 2 ? S.lleaf_v : S.leaf_v;  // uniform per block
         Hit h;
-        if (kWhileWhile)
+        if (kGrid)
+            h = grid_trace(S, ro, rd, cur.f[i], set == 2);
+        else if (kWhileWhile)
             h = trace4_ww<kRayLds>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
         else
             h = trace_ww<kRayLds>(set == 2 ? S.lbvh : S.bvh, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
@@ -2038,13 +2122,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
 }
 
 // batch closest hit (test / FFI entry mcpt_closest_hit)
+template <bool kGrid>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_batch(DScene S, int n, const double* ro, const double* rd,
                                                              const int* ex, int light_only, int* f_out,
                                                              double* tbg) {
     __shared__ int stack[kRayLds * kTraceBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Hit h = trace4_ww<kRayLds>(light_only ? S.lbvh4 : S.bvh4, light_only ? S.lleaf_v : S.leaf_v, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]),
+    const Hit h = kGrid ? grid_trace(S, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]), mk3(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]),
+                                     ex[i], light_only != 0)
+                        : trace4_ww<kRayLds>(light_only ? S.lbvh4 : S.bvh4, light_only ? S.lleaf_v : S.leaf_v, mk3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]),
                   mk3(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]), ex[i], stack + threadIdx.x, kTraceBlock);
     f_out[i] = h.f;
     tbg[3 * i] = h.f >= 0 ? h.t : 0.0;
@@ -2078,6 +2165,8 @@ struct DeviceState {
     hipStream_t stream = nullptr;
     // reusable work buffers
     DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14], aux[8], cache_bt, cache_lst, cache_info, cache_w, masks;
+    DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
+    int grid_version = 0;
     unsigned* pinned_count = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr;
 };
@@ -2087,6 +2176,8 @@ struct DeviceState {
 struct mcpt_scene {
     HostScene host;
     Bvh bvh, lbvh;
+    Grid grid;             // Myobj::cal_scene_boundingbox(eye) + meshing(n0) (mcpt_scene_meshing)
+    int grid_version = 0;  // bumped by every rebuild; devices re-upload on mismatch
     std::vector<std::unique_ptr<DeviceState>> devs;
     std::mutex mu;
 };
@@ -2341,6 +2432,31 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     return hipGetLastError();
 }
 
+// builds the scene's uniform grid for (eye, n0) unless it already is, and brings D's copy up to date
+int use_grid(mcpt_scene* sc, DeviceState& D, const double eye[3], int n0) {
+    Grid& g = sc->grid;
+    if (!g.ok || g.n0 != n0 || g.eye[0] != eye[0] || g.eye[1] != eye[1] || g.eye[2] != eye[2]) {
+        g = build_grid(sc->host, eye, n0);
+        sc->grid_version++;
+    }
+    if (D.grid_version != sc->grid_version) {
+        int rc;
+        if ((rc = ensure(D.g_start, g.cell_start.size() * 4)) || (rc = ensure(D.g_tri, g.cell_tri.size() * 4))) return rc;
+        HIP_OK(hipMemcpy(D.g_start.p, g.cell_start.data(), g.cell_start.size() * 4, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(D.g_tri.p, g.cell_tri.data(), g.cell_tri.size() * 4, hipMemcpyHostToDevice));
+        D.d.g_start = (const int*)D.g_start.p;
+        D.d.g_tri = (const int*)D.g_tri.p;
+        for (int i = 0; i < 3; i++) {
+            D.d.g_mn[i] = g.mn[i];
+            D.d.g_lim[i] = g.lim[i];
+            D.d.g_gd[i] = g.gd[i];
+        }
+        D.d.g_inv_d = g.inv_d;
+        D.grid_version = sc->grid_version;
+    }
+    return MCPT_OK;
+}
+
 // the wavefront render into a device framebuffer already resident on D's device
 int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o,
                      double* dfb, mcpt_stats* stats) {
@@ -2348,9 +2464,18 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int W = cam->width, H = cam->height, npx = W * H;
     const int s0 = (o->sample_begin == 0 && o->sample_end == 0) ? 0 : o->sample_begin;
     const int s1 = (o->sample_begin == 0 && o->sample_end == 0) ? o->spp : o->sample_end;
-    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF && o->mode != MCPT_MODE_SHADE)) {
-        set_error("invalid render options (spp %d, range [%d,%d), mode %d)", o->spp, s0, s1, o->mode);
+    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF && o->mode != MCPT_MODE_SHADE) ||
+        (o->accel != MCPT_ACCEL_BVH && o->accel != MCPT_ACCEL_GRID)) {
+        set_error("invalid render options (spp %d, range [%d,%d), mode %d, accel %d)", o->spp, s0, s1, o->mode, o->accel);
         return MCPT_E_INVALID;
+    }
+    // MCPT_ACCEL_GRID: the reference's uniform grid over the scene and this camera's eye, n0 =
+    // 100000 (main.cpp:501-504), built here unless the scene already holds that grid
+    const bool grid = o->accel == MCPT_ACCEL_GRID;
+    if (grid) {
+        const double eye[3] = {cf.eye.x, cf.eye.y, cf.eye.z};
+        int rg;
+        if ((rg = use_grid(sc, D, eye, 100000))) return rg;
     }
     // Path regeneration (wavefront with refill): before every generation the current queue is
     // topped up with fresh camera samples (roots) to `target` nodes, so every prep/extend launch
@@ -2375,9 +2500,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // keeps the single kernel (one ray per node; measured faster).  A/B switches:
     static const bool fused_env = getenv("MCPT_FUSED_EXTEND") != nullptr;
     static const bool ifif = getenv("MCPT_TRACE_BVH2") != nullptr;  // A/B: binary-tree trace_ww instead of trace4_ww
-#define K_MIS_RAYS (ifif ? k_mis_rays<false> : k_mis_rays<true>)
+#define K_MIS_RAYS (grid ? k_mis_rays<true, true> : ifif ? k_mis_rays<false> : k_mis_rays<true>)
     static const bool split_brdf = getenv("MCPT_SPLIT_BRDF") != nullptr;
-    const bool fused = fused_env || (o->mode == MCPT_MODE_BRDF && !split_brdf);
+    const bool fused = !grid && (fused_env || (o->mode == MCPT_MODE_BRDF && !split_brdf));  // the grid runs split
     Aux aux{};
     if (!fused && (rc = alloc_aux(D.aux, cap, aux))) return rc;
     hipStream_t st = D.stream;
@@ -2424,8 +2549,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // timed region (seconds, HIP events) starts at the primary-hit kernel
     HIP_OK(hipMemsetAsync(D.stats.p, 0, 64, st));
     HIP_OK(hipEventRecord(D.ev0, st));
-    hipLaunchKernelGGL(k_primary, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, D.d, cf,
-                       (int*)D.hit_f.p, (double*)D.hit_tbg.p);
+    hipLaunchKernelGGL(grid ? k_primary<true> : k_primary<false>, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock),
+                       0, st, D.d, cf, (int*)D.hit_f.p, (double*)D.hit_tbg.p);
     HIP_OK(hipGetLastError());
     if (pc.use) {
         HIP_OK(hipMemsetAsync(qb.count, 0, 4, st));
@@ -2749,9 +2874,38 @@ int mcpt_render(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* 
     return MCPT_OK;
 }
 
+int mcpt_scene_meshing(mcpt_scene* sc, const double eye[3], int32_t n0) {
+    if (!sc || !eye || n0 <= 0 || !std::isfinite(eye[0]) || !std::isfinite(eye[1]) || !std::isfinite(eye[2])) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(sc->mu);
+    sc->grid = build_grid(sc->host, eye, n0);
+    sc->grid_version++;
+    return MCPT_OK;
+}
+
+int mcpt_scene_grid_info(const mcpt_scene* sc, double* box_and_cell, int32_t* cells) {
+    if (!sc || !sc->grid.ok) {
+        set_error(sc ? "no grid (call mcpt_scene_meshing first)" : "null scene");
+        return MCPT_E_INVALID;
+    }
+    const Grid& g = sc->grid;
+    if (box_and_cell) {
+        for (int i = 0; i < 3; i++) {
+            box_and_cell[2 * i] = g.mn[i];
+            box_and_cell[2 * i + 1] = g.mx[i];
+        }
+        box_and_cell[6] = g.d;
+    }
+    if (cells)
+        for (int i = 0; i < 3; i++) cells[i] = g.gd[i];
+    return MCPT_OK;
+}
+
 int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* rd, const int32_t* ex,
-                     int32_t light_only, int32_t* facet, double* tbg) {
-    if (!sc || n < 0 || (n && (!ro || !rd || !ex || !facet || !tbg))) {
+                     int32_t flags, int32_t* facet, double* tbg) {
+    if (!sc || n < 0 || (n && (!ro || !rd || !ex || !facet || !tbg)) || (flags & ~(MCPT_HIT_LIGHT_ONLY | MCPT_HIT_GRID))) {
         set_error("invalid argument");
         return MCPT_E_INVALID;
     }
@@ -2760,6 +2914,15 @@ int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* 
     DeviceState* D;
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
+    const bool grid = (flags & MCPT_HIT_GRID) != 0;
+    if (grid) {
+        if (!sc->grid.ok) {
+            set_error("MCPT_HIT_GRID: no grid (call mcpt_scene_meshing first)");
+            return MCPT_E_INVALID;
+        }
+        if ((rc = use_grid(sc, *D, sc->grid.eye, sc->grid.n0))) return rc;
+    }
+    const int light_only = (flags & MCPT_HIT_LIGHT_ONLY) != 0;
     void *dro, *drd, *dex, *df, *dt;
     HIP_OK(hipMalloc(&dro, 24ull * n));
     HIP_OK(hipMalloc(&drd, 24ull * n));
@@ -2769,7 +2932,7 @@ int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* 
     HIP_OK(hipMemcpy(dro, ro, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(drd, rd, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(dex, ex, 4ull * n, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_trace_batch, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d, n,
+    hipLaunchKernelGGL(grid ? k_trace_batch<true> : k_trace_batch<false>, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d, n,
                        (const double*)dro, (const double*)drd, (const int*)dex, light_only, (int*)df, (double*)dt);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
@@ -2873,7 +3036,7 @@ int mcpt_primary_hits(mcpt_scene* sc, const mcpt_camera* cam, int32_t* facet, do
     if ((rc = get_device_state(sc, -1, &D))) return rc;
     const int npx = cam->width * cam->height;
     if ((rc = ensure(D->hit_f, 4ull * npx)) || (rc = ensure(D->hit_tbg, 24ull * npx))) return rc;
-    hipLaunchKernelGGL(k_primary, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d,
+    hipLaunchKernelGGL(k_primary<false>, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d,
                        cam_setup(*cam), (int*)D->hit_f.p, (double*)D->hit_tbg.p);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
