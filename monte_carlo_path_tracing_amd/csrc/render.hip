@@ -1549,7 +1549,7 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
                                                    unsigned long long* stats, int nchunks, PrepCache C) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (blockDim.x >> 6);
-    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));  // wave-uniform: scalar loads and SALU hashing
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     unsigned long long cached = 0;
     // static assignment: a root costs ~the same everywhere, and a shared work counter would
     // serialise on its one address at this node rate
