@@ -1181,6 +1181,25 @@ __device__ inline int lane_rank(uint64_t m) {  // set bits of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
+// lst[base + rank] = idx for the lanes whose bit is set in m (rank = set bits of m below the lane),
+// with exec = m for the store instead of a per-lane bit test: 2 v_mbcnt + 1 v_lshl_add per word.
+// exec is restored before the block ends; the LDS store is ordered with the kernel's other LDS
+// accesses (in-order per wave; the caller's wave_lds_sync follows the rebuild).
+__device__ inline void append_masked(uint64_t m, unsigned lo, unsigned hi, unsigned base_bytes, unsigned idx) {
+    uint64_t saved;
+    unsigned t;
+    asm volatile(
+        "s_and_saveexec_b64 %[sv], %[m]\n\t"
+        "v_mbcnt_lo_u32_b32 %[t], %[lo], 0\n\t"
+        "v_mbcnt_hi_u32_b32 %[t], %[hi], %[t]\n\t"
+        "v_lshl_add_u32 %[t], %[t], 1, %[b]\n\t"
+        "ds_write_b16 %[t], %[x]\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [sv] "=&s"(saved), [t] "=&v"(t)
+        : [m] "s"(m), [lo] "s"(lo), [hi] "s"(hi), [b] "s"(base_bytes), [x] "v"(idx)
+        : "memory");
+}
+
 // Root-point cache.  Every camera sample of a pixel starts at the same shading point (the
 // reference re-traces the identical primary ray per sample, main.cpp:572), so the light prep of a
 // root node (x1, n) -- batch totals and candidate list -- is a function of the pixel alone; only the
@@ -1443,15 +1462,19 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                               : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
         };
         int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
-        if (kMaskIn) {  // phase A done by k_prep_cull: rebuild the list from the candidate words
+        if (kMaskIn) {  // phase A done by k_prep_cull_lanes: rebuild the list from the candidate words
+            const unsigned lds_lst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lst);  // LDS offset (low half of the flat address)
             for (int c0 = 0; c0 < nchunks; c0 += 64) {  // one vector load of up to 64 words, then readlanes
                 const unsigned long long mv = c0 + lane < nchunks ? masks[mask_index(node, c0 + lane, nchunks)] : 0ull;
-                const int cend = min(64, nchunks - c0);
+                const int cend = __builtin_amdgcn_readfirstlane(min(64, nchunks - c0));
+                unsigned idx = (unsigned)(c0 * 64 + lane);
                 for (int q = 0; q < cend; q++) {
-                    const uint64_t m = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(mv >> 32), q) << 32) |
-                                       (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mv, q);
-                    if ((m >> lane) & 1) lst[ncand + lane_rank(m)] = (unsigned short)((c0 + q) * 64 + lane);
+                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(mv >> 32), q);
+                    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mv, q);
+                    const uint64_t m = ((uint64_t)hi << 32) | lo;
+                    append_masked(m, lo, hi, lds_lst + 2u * (unsigned)ncand, idx);
                     ncand += __popcll(m);
+                    idx += 64;
                 }
             }
         } else {
