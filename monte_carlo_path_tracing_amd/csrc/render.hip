@@ -1593,13 +1593,30 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
             vraw[k] = lane < nchunks ? C.bt[(size_t)px[k] * nchunks + lane] : 0.0;
             inf[k] = C.info[px[k]];
         }
+        // the roots' pick uniforms (dim 1), one root per lane 0..kPickNodes-1: the 64-bit hash chain
+        // runs once for all of them instead of once per root on every lane
+        double ul;
+        {
+            const int kk = lane & (kPickNodes - 1);
+            int pxs = px[0], sms = smp[0];
+            uint64_t nds = nid[0];
+#pragma unroll
+            for (int k = 1; k < kPickNodes; k++) {
+                pxs = kk == k ? px[k] : pxs;
+                sms = kk == k ? smp[k] : sms;
+                nds = kk == k ? nid[k] : nds;
+            }
+            ul = counter_u(counter_key(seed, (uint64_t)pxs, (uint64_t)sms, nds), 1);
+        }
         double wsum[kPickNodes], base[kPickNodes], target[kPickNodes];
         int kb[kPickNodes];
 #pragma unroll
         for (int k = 0; k < kPickNodes; k++) {
             const int nb = inf[k].x;
             const double* bt = C.bt + (size_t)px[k] * nchunks;
-            const double u = counter_u(counter_key(seed, (uint64_t)px[k], (uint64_t)smp[k], nid[k]), 1);
+            const double u = __longlong_as_double(
+                ((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(ul) >> 32), k) << 32) |
+                (unsigned)__builtin_amdgcn_readlane((int)__double_as_longlong(ul), k));
             wsum[k] = 0;
             kb[k] = -1;
             base[k] = 0;
