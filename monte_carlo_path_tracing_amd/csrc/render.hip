@@ -1,16 +1,24 @@
 // MI355X (gfx950) wavefront path tracer for the reference's per-pixel radiance loop
-// (main.cpp:547-588 -> shade_with_mis main.cpp:402-494 / shade_with_brdf :348-399).
+// (main.cpp:547-588 -> shade_with_mis main.cpp:402-494 / shade_with_brdf :348-399 / shade :269-344).
 //
-// The recursion is flattened into generations of a persistent SoA node queue in HBM:
+// The recursion is flattened into generations of a persistent SoA node queue in HBM (DESIGN.md §4):
 //
-//   k_primary   lane per pixel : camera ray (main.cpp:547-564) + BVH closest hit, once per frame
-//   k_roots     lane per root  : node-entry checks of the root (back-face, emitter, RR) -> queue
-//   k_prep      WAVE per node  : Mylight::prepared_for_lights_spherical_triangle_sampling over all
-//                                light triangles (64 lanes = 64 light triangles, fp64), wave
-//                                prefix sums -> weights_sum and the inverse-CDF pick (MIS only)
-//   k_extend_*  lane per node  : Arvo light sample, Phong BRDF sample, up to 3 BVH traversals,
-//                                MIS weights, and the entry checks of the <= 2 children, which are
-//                                appended to the next generation's queue (wave-aggregated atomics)
+//   k_primary          lane per pixel : camera ray (main.cpp:547-564) + closest hit, once per call
+//   k_roots            lane per root  : node-entry checks of a camera sample's root (back-face,
+//                                       emitter, RR) -> queue (path regeneration)
+//   k_root_points      lane per pixel : root shading points for the per-pixel root-point cache
+//   k_prep_cull_lanes  lane per node  : light prep phase A -- the light-side and tangent-plane culls
+//                                       of Mylight.cpp:340-357 against every light (light table
+//                                       in scalar registers) -> candidate words
+//   k_prep_pk2         WAVE per node  : phase B -- fp64 spherical-triangle weights of the candidates
+//                                       (Mylight.cpp:360-413) in dense 64-wide batches -> weights_sum
+//                                       and the inverse-CDF pick; in build mode fills the cache
+//   k_prep_pick        WAVE per root  : the pick of a root from the root-point cache
+//   k_prep / k_prep_lane              : the same prep for huge / tiny light sets
+//   k_mis_gen / k_shade_gen / k_brdf_gen, k_mis_rays (BVH or the reference grid), k_*_combine:
+//                                       light + BRDF samples, their closest hits, MIS weights and the
+//                                       children's entry checks -> next generation's queue
+//   k_extend_brdf      lane per node  : the BRDF-only vertex in one kernel
 //
 // A node's value is the sum over its subtree's emitter hits of (throughput x emit); contributions
 // are accumulated straight into an fp64 framebuffer with hardware fp64 atomics.
@@ -64,9 +72,7 @@ struct DScene {
     const float* lt_d;        // NL: float(nl . p0)
     const double2* lt_w;      // NL*5: p0, p1, p2 (fp64), RadianceRGB::sum()
     const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
-    const BvhNode* bvh;       // all facets
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
-    const BvhNode* lbvh;      // light facets only
     const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves)
     const BvhNode4* lbvh4;
     const float4* lleaf_v;
@@ -120,7 +126,7 @@ __device__ inline d3 cam_dir(const CamFrame& f, int i, int j) {  // main.cpp:563
 // ============================================================================================
 constexpr int kStack = 48;
 constexpr int kRayBlock = 256;
-constexpr int kRayLds = 16;  // LDS stack entries per lane of trace_s / trace_ww (16 KB per 256 lanes)
+constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB per 256 lanes)
 constexpr int kTraceBlock = 128;
 
 struct Hit {
@@ -128,263 +134,20 @@ struct Hit {
     double t, beta, gamma;
 };
 
-__device__ inline Hit trace(const BvhNode* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
-                            int exclude, int* __restrict__ stack, int stride) {
-    Hit best{-1, DBL_MAX, 0, 0};
-    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
-    const float ox = (float)ro.x, oy = (float)ro.y, oz = (float)ro.z;
-    auto inv = [](double d) {
-        float f = (float)d;
-        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
-        return 1.0f / f;
-    };
-    const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
-    float tlimit = FLT_MAX;
-    int sp = 0;
-    int node = 0;
-    while (true) {
-        const BvhNode nd = nodes[node];
-        float tn[2];
-        bool hitc[2];
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            float tx0 = (nd.lo[k][0] - ox) * ix, tx1 = (nd.hi[k][0] - ox) * ix;
-            float ty0 = (nd.lo[k][1] - oy) * iy, ty1 = (nd.hi[k][1] - oy) * iy;
-            float tz0 = (nd.lo[k][2] - oz) * iz, tz1 = (nd.hi[k][2] - oz) * iz;
-            float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-            float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
-            hitc[k] = t0 <= t1 * 1.00001f + 1e-6f;
-            tn[k] = t0;
-        }
-        int next[2];
-        int nn = 0;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            if (!hitc[k]) continue;
-            const int c = nd.child[k];
-            if (c >= 0) {
-                next[nn++] = c;
-                continue;
-            }
-            const int first = ~c, cnt = nd.count[k];
-            for (int q = first; q < first + cnt; q++) {
-                const float4 a = leafv[3 * q], b = leafv[3 * q + 1], cc = leafv[3 * q + 2];
-                const int fac = __float_as_int(a.w);
-                if (fac == exclude) continue;
-                TriHit h = tri_hit(f3(a), f3(b), f3(cc), ro, rd);
-                if (h.hit && (h.t < best.t || (h.t == best.t && fac < best.f))) {
-                    best.f = fac;
-                    best.t = h.t;
-                    best.beta = h.beta;
-                    best.gamma = h.gamma;
-                    tlimit = (float)h.t * 1.0001f + 1e-5f;
-                }
-            }
-        }
-        if (nn == 2) {
-            int nearc = next[0], farc = next[1];
-            if (tn[1] < tn[0]) {
-                nearc = next[1];
-                farc = next[0];
-            }
-            if (sp < kStack) stack[(sp++) * stride] = farc;
-            node = nearc;
-        } else if (nn == 1) {
-            node = next[0];
-        } else {
-            if (sp == 0) break;
-            node = stack[(--sp) * stride];
-        }
-    }
-    return best;
-}
-
-// trace() for the split pipeline's ray kernels: a short LDS stack of kLds entries per lane with a
-// private (scratch) overflow up to kStack, slab tests as one FMA per plane (origin * inverse
-// precomputed; the boxes' conservative margins absorb the extra rounding), and a sign pre-test
-// that rejects beta < 0, gamma < 0 and t < 0 before the three fp64 divisions of the reference's
-// Cramer rule (a nonzero quotient has the sign of its operands; the divisions of the surviving
-// candidates are exactly tri_hit's, so accepted hits are bit-identical).
-template <int kLds>
-__device__ inline Hit trace_s(const BvhNode* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
-                              int exclude, int* __restrict__ lds, int stride) {
-    Hit best{-1, DBL_MAX, 0, 0};
-    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
-    int spill[kStack - kLds];
-    auto inv = [](double d) {
-        float f = (float)d;
-        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
-        return 1.0f / f;
-    };
-    const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
-    const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
-    float tlimit = FLT_MAX;
-    int sp = 0;
-    int node = 0;
-    while (true) {
-        const BvhNode nd = nodes[node];
-        float tn[2];
-        bool hitc[2];
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const float tx0 = fmaf(nd.lo[k][0], ix, -oix), tx1 = fmaf(nd.hi[k][0], ix, -oix);
-            const float ty0 = fmaf(nd.lo[k][1], iy, -oiy), ty1 = fmaf(nd.hi[k][1], iy, -oiy);
-            const float tz0 = fmaf(nd.lo[k][2], iz, -oiz), tz1 = fmaf(nd.hi[k][2], iz, -oiz);
-            const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-            const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
-            hitc[k] = t0 <= t1 * 1.00001f + 1e-6f;
-            tn[k] = t0;
-        }
-        int next[2];
-        int nn = 0;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            if (!hitc[k]) continue;
-            const int c = nd.child[k];
-            if (c >= 0) {
-                next[nn++] = c;
-                continue;
-            }
-            const int first = ~c, cnt = nd.count[k];
-            for (int q = first; q < first + cnt; q++) {
-                const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
-                const int fac = __float_as_int(a4.w);
-                if (fac == exclude) continue;
-                const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
-                const double detA = det3(ab, ac, rd);
-                if (fabs(detA) < MCPT_EPS) continue;
-                const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
-                const bool neg = detA < 0;
-                if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
-                    continue;  // beta, gamma or t < 0
-                const double beta = nb / detA, gamma = ng / detA, t = nt / detA;
-                if (beta < 0 || gamma < 0 || beta + gamma > 1 || t < 0 || fabs(t) < MCPT_EPS) continue;
-                if (t < best.t || (t == best.t && fac < best.f)) {
-                    best.f = fac;
-                    best.t = t;
-                    best.beta = beta;
-                    best.gamma = gamma;
-                    tlimit = (float)t * 1.0001f + 1e-5f;
-                }
-            }
-        }
-        if (nn == 2) {
-            int nearc = next[0], farc = next[1];
-            if (tn[1] < tn[0]) {
-                nearc = next[1];
-                farc = next[0];
-            }
-            if (sp < kLds) lds[sp * stride] = farc;
-            else if (sp < kStack) spill[sp - kLds] = farc;
-            sp = sp < kStack ? sp + 1 : sp;
-            node = nearc;
-        } else if (nn == 1) {
-            node = next[0];
-        } else {
-            if (sp == 0) break;
-            --sp;
-            node = sp < kLds ? lds[sp * stride] : spill[sp - kLds];
-        }
-    }
-    return best;
-}
-
-// trace_s reorganised as Aila & Laine's "while-while" loop: a lane descends through internal nodes
-// until it holds a leaf (postponed), and the wave tests triangles only once every active lane has
-// one (or ran out of nodes), so the fp64 triangle tests run with few idle lanes.  Leaves travel on
-// the stack as ~((first << 3) | count); arithmetic and results are trace_s's.
-template <int kLds>
-__device__ inline Hit trace_ww(const BvhNode* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
-                               int exclude, int* __restrict__ lds, int stride) {
-    constexpr int kDone = 0x7fffffff;  // popped from an empty stack
-    Hit best{-1, DBL_MAX, 0, 0};
-    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
-    int spill[kStack - kLds];
-    auto inv = [](double d) {
-        float f = (float)d;
-        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
-        return 1.0f / f;
-    };
-    const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
-    const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
-    float tlimit = FLT_MAX;
-    int sp = 0;
-    auto push = [&](int v) {
-        if (sp < kLds) lds[sp * stride] = v;
-        else if (sp < kStack) spill[sp - kLds] = v;
-        sp = sp < kStack ? sp + 1 : sp;
-    };
-    auto pop = [&]() -> int {
-        if (sp == 0) return kDone;
-        --sp;
-        return sp < kLds ? lds[sp * stride] : spill[sp - kLds];
-    };
-    int node = 0;   // >= 0 internal node (or kDone), < 0 packed leaf
-    int leaf = 0;   // < 0: a postponed leaf
-    while (node != kDone || leaf < 0) {
-        while (node >= 0 && node != kDone) {
-            const BvhNode nd = nodes[node];
-            float tn[2];
-            bool hc[2];
-            int code[2];
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const float tx0 = fmaf(nd.lo[k][0], ix, -oix), tx1 = fmaf(nd.hi[k][0], ix, -oix);
-                const float ty0 = fmaf(nd.lo[k][1], iy, -oiy), ty1 = fmaf(nd.hi[k][1], iy, -oiy);
-                const float tz0 = fmaf(nd.lo[k][2], iz, -oiz), tz1 = fmaf(nd.hi[k][2], iz, -oiz);
-                const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
-                hc[k] = t0 <= t1 * 1.00001f + 1e-6f;
-                tn[k] = t0;
-                const int c = nd.child[k];
-                code[k] = c >= 0 ? c : ~(((~c) << 3) | nd.count[k]);
-            }
-            if (!hc[0] && !hc[1]) {
-                node = pop();
-            } else {
-                const bool first0 = hc[0] && (!hc[1] || tn[0] <= tn[1]);
-                node = first0 ? code[0] : code[1];
-                if (hc[0] && hc[1]) push(first0 ? code[1] : code[0]);
-            }
-            if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
-                leaf = node;
-                node = pop();
-            }
-            if (!__any(leaf >= 0)) break;  // every lane holds a leaf
-        }
-        while (leaf < 0) {
-            const int packed = ~leaf, first = packed >> 3, cnt = packed & 7;
-            for (int q = first; q < first + cnt; q++) {
-                const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
-                const int fac = __float_as_int(a4.w);
-                if (fac == exclude) continue;
-                const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
-                const double detA = det3(ab, ac, rd);
-                if (fabs(detA) < MCPT_EPS) continue;
-                const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
-                const bool neg = detA < 0;
-                if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
-                    continue;
-                const double beta = nb / detA, gamma = ng / detA, t = nt / detA;
-                if (beta < 0 || gamma < 0 || beta + gamma > 1 || t < 0 || fabs(t) < MCPT_EPS) continue;
-                if (t < best.t || (t == best.t && fac < best.f)) {
-                    best.f = fac;
-                    best.t = t;
-                    best.beta = beta;
-                    best.gamma = gamma;
-                    tlimit = (float)t * 1.0001f + 1e-5f;
-                }
-            }
-            leaf = node;
-            if (node < 0) node = pop();
-        }
-    }
-    return best;
-}
-
-// trace_ww over the 4-wide tree: four slab tests per node visit, hits ordered near-to-far with
-// a 5-comparator network, the nearest followed and the rest pushed far-first.  Same candidate
-// set semantics (every triangle in a hit leaf gets the exact fp64 test), so results equal trace_s.
+// Closest hit over the 4-wide BVH (Myobj::closet_ray_intersect semantics without the grid):
+//  * Aila & Laine's "while-while" loop: a lane descends through inner nodes until it holds a leaf
+//    (postponed), and the wave tests triangles only once every active lane has one (or ran out of
+//    nodes), so the fp64 triangle tests run with few idle lanes; leaves travel on the stack as
+//    ~((first << 3) | count);
+//  * four slab tests per node visit as one FMA per plane (origin * inverse precomputed; the boxes'
+//    conservative margins absorb the extra rounding), hits ordered near-to-far by a 5-comparator
+//    network, the nearest followed and the rest pushed far-first;
+//  * a short LDS stack of kLds entries per lane with a private (scratch) overflow up to kStack;
+//  * every triangle of a hit leaf gets the reference's fp64 Cramer test (Myobj.cpp:165-192) behind
+//    a sign pre-test that rejects beta < 0, gamma < 0 and t < 0 before the three divisions (a
+//    nonzero quotient has the sign of its operands; the divisions of the surviving candidates are
+//    exactly tri_hit's, so accepted hits are bit-identical); origin facet excluded, t > 1e-8, ties
+//    to the lower facet id.
 template <int kLds>
 __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
                                 int exclude, int* __restrict__ lds, int stride) {
@@ -1692,95 +1455,10 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
     if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
 }
 
-// one MIS node (main.cpp:440-493), lane per node; children go through node_entry.
-__global__ __launch_bounds__(kTraceBlock) void k_extend_mis(Params P, Queue cur, int n, Queue nxt) {
-    __shared__ int stack[kStack * kTraceBlock];
-    int* st = stack + threadIdx.x;
-    const DScene& S = P.S;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = i < n;
-    const int ii = active ? i : 0;
-    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
-    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
-    const d3 wo = mk3(cur.wo[3 * ii], cur.wo[3 * ii + 1], cur.wo[3 * ii + 2]);
-    const d3 tp = mk3(cur.tp[3 * ii], cur.tp[3 * ii + 1], cur.tp[3 * ii + 2]);
-    const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
-    const uint64_t node = cur.node[ii];
-    const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
-    const float* m = S.mtl + 7 * S.tri_mat[f];
-    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
-    const double sh = m[6];
-    const double wsum = cur.wsum[ii];
-    const int pick = cur.pick[ii];
-
-    // ---- light branch (main.cpp:443-466) ----
-    bool c1 = false;
-    Hit h1{-1, 0, 0, 0};
-    d3 wl = mk3(0, 0, 0), tp1 = mk3(0, 0, 0);
-    if (active) {
-        d3 coord;
-        double lprob = 1;
-        if (pick >= 0) {
-            const double4 ln = S.lt_n[pick];
-            SphTri sph;
-            light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph,
-                       true);
-            const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
-            TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
-            coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:475-481)
-            lprob = S.light_sum[pick] / wsum;
-        } else {
-            coord = add(mul(N, -1), p);  // Mylight.cpp:427-430
-        }
-        wl = normalized(sub(coord, p));
-        if (dot(wl, N) > 0) {
-            h1 = trace(S.bvh, S.leaf_v, p, wl, f, st, kTraceBlock);
-            if (h1.f >= 0) {
-                const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
-                const double pp = phong_pdf(N, wl, wo, kd, ks, sh);
-                tp1 = mul(hmul(tp, b), dot(wl, N) / (lprob + pp) / MCPT_P_RR);
-                c1 = true;
-            }
-        }
-    }
-    // ---- BRDF branch (main.cpp:469-493) ----
-    bool c2 = false;
-    Hit h2{-1, 0, 0, 0};
-    d3 wi = mk3(0, 0, 0), tp2 = mk3(0, 0, 0);
-    unsigned nrays = 0, nlrays = 0;
-    if (active) {
-        nrays += (dot(wl, N) > 0);
-        double pdf;
-        wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
-        if (!(dot(wi, N) < 0)) {
-            nrays++;
-            h2 = trace(S.bvh, S.leaf_v, p, wi, f, st, kTraceBlock);
-            if (h2.f >= 0) {
-                const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
-                double lpdf = 0;
-                nlrays++;
-                Hit hl = trace(S.lbvh, S.lleaf_v, p, wi, f, st, kTraceBlock);
-                if (hl.f >= 0 && !(fabs(wsum) < MCPT_EPS)) {
-                    const int li = S.tri_light[hl.f];
-                    const PrepLight L = load_light(S, li);
-                    double wl_unused;
-                    if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) && light_weight(L.p0, L.p1, L.p2, L.lsum, p, &wl_unused))
-                        lpdf = S.light_sum[li] / wsum;  // fresh-state eval (Mylight.cpp:484-493)
-                }
-                tp2 = mul(hmul(tp, b), dot(wi, N) / (pdf + lpdf) / MCPT_P_RR);
-                c2 = true;
-            }
-        }
-    }
-    node_entry(P, c1, h1.f, h1.beta, h1.gamma, mul(wl, -1), tp1, pixel, sample, 2 * node, nxt);
-    node_entry(P, c2, h2.f, h2.beta, h2.gamma, mul(wi, -1), tp2, pixel, sample, 2 * node + 1, nxt);
-    block_count(P.stats + 2, active ? nrays : 0u, P.stats + 3, active ? nlrays : 0u);
-}
-
 // ---- MIS node split into three kernels (ray generation / traversal / combination) -------------
-// k_extend_mis does everything per lane with three inlined traversals (152 VGPRs, 3 waves/SIMD).
-// Split, the traversal kernel runs at high occupancy on a short LDS stack, and the shading
-// kernels carry no traversal state.  Per node in `Aux` (capacity = queue capacity):
+// (one MIS node per lane with three inlined traversals measured 152 VGPRs, 3 waves/SIMD.)  Split,
+// the traversal kernel runs at high occupancy on a short LDS stack, and the shading kernels carry
+// no traversal state.  Per node in `Aux` (capacity = queue capacity):
 //   d1, d2   light / BRDF directions (3 doubles each)
 //   w1       tp * f(wl) * cos / (p_light + p_phong) / 0.6  -- the light child's throughput
 //   w2       tp * f(wi); c2 = (pdf, cos) of the BRDF sample -- the BRDF child's throughput needs
@@ -1850,7 +1528,7 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 
 // closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
 // queue's shading points, excluding the origin facet
-template <bool kWhileWhile, bool kGrid = false>
+template <bool kGrid>
 __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set) {
     __shared__ int stack[kRayLds * kRayBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1867,10 +1545,8 @@ __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, 
         Hit h;
         if (kGrid)
             h = grid_trace(S, ro, rd, cur.f[i], set == 2);
-        else if (kWhileWhile)
-            h = trace4_ww<kRayLds>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
         else
-            h = trace_ww<kRayLds>(set == 2 ? S.lbvh : S.bvh, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
+            h = trace4_ww<kRayLds>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
@@ -2040,87 +1716,6 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
     block_count(P.stats + 2, (active && (fl & 2)) ? 1u : 0u);
-}
-
-// one shade() node (main.cpp:295-343), lane per node: the direct-light estimate is splatted into
-// the framebuffer here; RR, then at most one child (a Phong-sampled bounce that hits a non-emitter,
-// main.cpp:335) through node_entry.  The light point comes from the prep kernel's pick -- the
-// non-staged sampler select_a_point_from_lights_spherical_triangle (Mylight.cpp:163-318) has the
-// same culls, weights and pick as the staged pair used by MIS.
-__global__ __launch_bounds__(kTraceBlock) void k_extend_shade(Params P, Queue cur, int n, Queue nxt) {
-    __shared__ int stack[kStack * kTraceBlock];
-    int* st = stack + threadIdx.x;
-    const DScene& S = P.S;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = i < n;
-    const int ii = active ? i : 0;
-    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
-    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
-    const d3 wo = mk3(cur.wo[3 * ii], cur.wo[3 * ii + 1], cur.wo[3 * ii + 2]);
-    const d3 tp = mk3(cur.tp[3 * ii], cur.tp[3 * ii + 1], cur.tp[3 * ii + 2]);
-    const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
-    const uint64_t node = cur.node[ii];
-    const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
-    const float* m = S.mtl + 7 * S.tri_mat[f];
-    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
-    const double sh = m[6];
-    const double wsum = cur.wsum[ii];
-    const int pick = cur.pick[ii];
-    bool c = false;
-    Hit h{-1, 0, 0, 0};
-    d3 wi = mk3(0, 0, 0), tpc = mk3(0, 0, 0);
-    unsigned nrays = 0;
-    if (active) {
-        // ---- direct light (main.cpp:295-316) ----
-        d3 coord, n1 = N;
-        double lprob = 1;
-        if (pick >= 0) {
-            const double4 ln = S.lt_n[pick];
-            SphTri sph;
-            light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph,
-                       true);
-            const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
-            TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
-            coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:311-317)
-            lprob = S.light_sum[pick] / wsum;
-            n1 = mk3(ln.x, ln.y, ln.z);
-        } else {
-            // empty set: the dummy point x1 - n (Mylight.cpp:263-266); wl = -N fails wl.N > 0, so the
-            // dummy facet's normal is never read
-            coord = add(mul(N, -1), p);
-        }
-        const d3 wl = normalized(sub(coord, p));
-        if (dot(wl, N) > 0 && dot(mul(wl, -1), n1) > 0) {
-            nrays++;
-            const Hit hs = trace(S.bvh, S.leaf_v, p, wl, f, st, kTraceBlock);
-            if (pick >= 0 && hs.f >= 0 && hs.f == S.light_facet[pick]) {
-                const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
-                const d3 d = sub(coord, p);
-                const d3 I = mk3(S.light_rad[3 * pick], S.light_rad[3 * pick + 1], S.light_rad[3 * pick + 2]);
-                const d3 Ld = mul(hmul(I, b), dot(wl, N) * dot(mul(wl, -1), n1) / dot(d, d) / lprob);
-                double* px = P.fb + 3 * (size_t)pixel;
-                unsafeAtomicAdd(px + 0, tp.x * Ld.x * P.inv_spp);
-                unsafeAtomicAdd(px + 1, tp.y * Ld.y * P.inv_spp);
-                unsafeAtomicAdd(px + 2, tp.z * Ld.z * P.inv_spp);
-            }
-        }
-        // ---- indirect (main.cpp:318-343) ----
-        if (!(counter_u(key, 0) > MCPT_P_RR)) {
-            double pdf;
-            wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
-            if (!(dot(wi, N) < 0)) {
-                nrays++;
-                h = trace(S.bvh, S.leaf_v, p, wi, f, st, kTraceBlock);
-                if (h.f >= 0 && S.tri_light[h.f] < 0) {
-                    const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
-                    tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
-                    c = true;
-                }
-            }
-        }
-    }
-    node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
-    block_count(P.stats + 2, active ? nrays : 0u);
 }
 
 // one BRDF-only path vertex (main.cpp:385-396)
@@ -2351,9 +1946,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, lpk, &d.lt_pk))) return rc;
     if ((rc = upload(*D, ld, &d.lt_d))) return rc;
     if ((rc = upload(*D, lw, &d.lt_w))) return rc;
-    if ((rc = upload(*D, sc->bvh.nodes, &d.bvh))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
-    if ((rc = upload(*D, sc->lbvh.nodes, &d.lbvh))) return rc;
     if ((rc = upload(*D, collapse_bvh4(sc->bvh), &d.bvh4))) return rc;
     if ((rc = upload(*D, collapse_bvh4(sc->lbvh), &d.lbvh4))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
@@ -2538,11 +2131,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     if ((rc = alloc_queue(D.qa, cap, qa)) || (rc = alloc_queue(D.qb, cap, qb))) return rc;
     // extension kernels: MIS and shade split into gen / rays / combine (measured faster), BRDF-only
     // keeps the single kernel (one ray per node; measured faster).  A/B switches:
-    static const bool fused_env = getenv("MCPT_FUSED_EXTEND") != nullptr;
-    static const bool ifif = getenv("MCPT_TRACE_BVH2") != nullptr;  // A/B: binary-tree trace_ww instead of trace4_ww
-#define K_MIS_RAYS (grid ? k_mis_rays<true, true> : ifif ? k_mis_rays<false> : k_mis_rays<true>)
+#define K_MIS_RAYS (grid ? k_mis_rays<true> : k_mis_rays<false>)
     static const bool split_brdf = getenv("MCPT_SPLIT_BRDF") != nullptr;
-    const bool fused = !grid && (fused_env || (o->mode == MCPT_MODE_BRDF && !split_brdf));  // the grid runs split
+    const bool fused = !grid && o->mode == MCPT_MODE_BRDF && !split_brdf;  // BRDF-only: k_extend_brdf (the grid runs split)
     Aux aux{};
     if (!fused && (rc = alloc_aux(D.aux, cap, aux))) return rc;
     hipStream_t st = D.stream;
@@ -2695,13 +2286,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 1), dim3(kRayBlock), 0, st, D.d, *cur,
                                ni, aux, 1);
             hipLaunchKernelGGL(k_brdf_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
-        } else if (o->mode == MCPT_MODE_MIS)
-            hipLaunchKernelGGL(k_extend_mis, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st, P,
-                               *cur, ni, *nxt);
-        else if (o->mode == MCPT_MODE_SHADE)
-            hipLaunchKernelGGL(k_extend_shade, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
-                               P, *cur, ni, *nxt);
-        else
+        } else
             hipLaunchKernelGGL(k_extend_brdf, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
                                P, *cur, ni, *nxt);
         HIP_OK(hipGetLastError());
