@@ -2318,8 +2318,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->generations = gens;
         stats->shading_nodes = nodes_total;
 
-        // variant 8 counts its full-prep nodes (hs[7]) and cached roots (hs[0]); the older variants
-        // run every node in full
+        // k_prep_pk2 counts its full-prep nodes (hs[7]) and k_prep_pick the cached roots (hs[0]);
+        // k_prep / k_prep_lane (huge / tiny light sets) run every node in full
         const uint64_t full = hs[7] ? hs[7] : (o->mode != MCPT_MODE_BRDF ? nodes_total : 0);
         stats->prep_full_nodes = full;
         stats->prep_cached_nodes = hs[0];
