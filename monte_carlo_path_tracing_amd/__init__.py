@@ -19,7 +19,7 @@ __all__ = ["Scene", "Camera", "render", "render_device", "closest_hit", "light_p
            "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "MODE_SHADE", "ACCEL_BVH", "ACCEL_GRID", "Stats", "MCPTError", "LIB_PATH", "lib"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmcpt_hip.so")
+LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(HERE, "libmcpt_hip.so")  # override: A/B of two builds
 MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2  # shade_with_mis / shade_with_brdf / shade (main.cpp:402/348/269)
 ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
 HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
