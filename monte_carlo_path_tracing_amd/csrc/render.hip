@@ -125,6 +125,7 @@ __device__ inline d3 cam_dir(const CamFrame& f, int i, int j) {  // main.cpp:563
 // triangle test on every candidate.  Stack in LDS, [depth][thread] layout (conflict-free).
 // ============================================================================================
 constexpr int kStack = 48;
+constexpr int kLeafBits = 5;  // leaf code ~((first slot << kLeafBits) | count)
 constexpr int kRayBlock = 256;
 constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB per 256 lanes)
 constexpr int kTraceBlock = 128;
@@ -138,7 +139,7 @@ struct Hit {
 //  * Aila & Laine's "while-while" loop: a lane descends through inner nodes until it holds a leaf
 //    (postponed), and the wave tests triangles only once every active lane has one (or ran out of
 //    nodes), so the fp64 triangle tests run with few idle lanes; leaves travel on the stack as
-//    ~((first << 3) | count);
+//    ~((first << kLeafBits) | count) (kLeafBits = 5: SAH leaves hold up to 16 triangles);
 //  * four slab tests per node visit as one FMA per plane (origin * inverse precomputed; the boxes'
 //    conservative margins absorb the extra rounding), hits ordered near-to-far by a 5-comparator
 //    network, the nearest followed and the rest pushed far-first;
@@ -183,10 +184,10 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                          lz = *reinterpret_cast<const float4*>(nd->lo[2]);
             const float4 hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
                          hz = *reinterpret_cast<const float4*>(nd->hi[2]);
-            const int4 ch = *reinterpret_cast<const int4*>(nd->child), cn = *reinterpret_cast<const int4*>(nd->count);
+            const int4 ch = *reinterpret_cast<const int4*>(nd->child);
             const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, lys[4] = {ly.x, ly.y, ly.z, ly.w}, lzs[4] = {lz.x, lz.y, lz.z, lz.w};
             const float hxs[4] = {hx.x, hx.y, hx.z, hx.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
-            const int chs[4] = {ch.x, ch.y, ch.z, ch.w}, cns[4] = {cn.x, cn.y, cn.z, cn.w};
+            const int chs[4] = {ch.x, ch.y, ch.z, ch.w};
             float t[4];
             int code[4];
 #pragma unroll
@@ -198,7 +199,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                 const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
                 const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
                 t[k] = h ? t0 : FLT_MAX;
-                code[k] = !h ? kDone : chs[k] >= 0 ? chs[k] : ~(((~chs[k]) << 3) | cns[k]);
+                code[k] = h ? chs[k] : kDone;  // leaves come pre-packed (pack_leaf_codes)
             }
             // sort (t, code) ascending; misses (FLT_MAX, kDone) sink to the end
             auto cs = [&](int a, int b) {
@@ -220,7 +221,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
             if (!__any(leaf >= 0)) break;
         }
         while (leaf < 0) {
-            const int packed = ~leaf, first = packed >> 3, cnt = packed & 7;
+            const int packed = ~leaf, first = packed >> kLeafBits, cnt = packed & ((1 << kLeafBits) - 1);
             for (int q = first; q < first + cnt; q++) {
                 const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
                 const int fac = __float_as_int(a4.w);
@@ -1838,6 +1839,22 @@ int upload(DeviceState& D, const std::vector<T>& v, const T** out) {
     return MCPT_OK;
 }
 
+// leaf children as the traversal stack code ~((first leaf slot << 3) | count), so a node visit needs
+// no count load or decode (trace4_ww)
+int pack_leaf_codes(std::vector<BvhNode4>& nodes) {
+    for (BvhNode4& n : nodes)
+        for (int k = 0; k < 4; k++)
+            if (n.child[k] < 0) {
+                const int first = ~n.child[k];
+                if (n.count[k] >= (1 << kLeafBits) || first >= (1 << (31 - kLeafBits))) {
+                    set_error("BVH leaf (%d triangles at slot %d) does not fit the traversal's leaf code", n.count[k], first);
+                    return MCPT_E_SCENE;
+                }
+                n.child[k] = ~((first << kLeafBits) | n.count[k]);
+            }
+    return MCPT_OK;
+}
+
 std::vector<float4> leaf_vertices(const HostScene& s, const Bvh& b) {
     std::vector<float4> v(3 * std::max<size_t>(b.leaf_facets.size(), 1));
     for (size_t q = 0; q < b.leaf_facets.size(); q++) {
@@ -1947,8 +1964,10 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, ld, &d.lt_d))) return rc;
     if ((rc = upload(*D, lw, &d.lt_w))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
-    if ((rc = upload(*D, collapse_bvh4(sc->bvh), &d.bvh4))) return rc;
-    if ((rc = upload(*D, collapse_bvh4(sc->lbvh), &d.lbvh4))) return rc;
+    std::vector<BvhNode4> b4 = collapse_bvh4(sc->bvh), lb4 = collapse_bvh4(sc->lbvh);
+    if ((rc = pack_leaf_codes(b4)) || (rc = pack_leaf_codes(lb4))) return rc;
+    if ((rc = upload(*D, b4, &d.bvh4))) return rc;
+    if ((rc = upload(*D, lb4, &d.lbvh4))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc(&D->pinned_count, 64));
