@@ -221,16 +221,19 @@ __device__ inline double fma_s(double a, double b, double c) {
     return r;
 }
 
-// a / |a| by the hardware rsqrt estimate plus one third-order Newton step (the refinement ocml's
-// rsqrt uses, without its zero/inf class fix-ups: a zero vector gives NaN either way, which every
-// caller culls)
-__device__ inline d3 funit(d3 a) {
-    const double s = fdot(a, a);
+// 1/sqrt(s) by the hardware rsqrt estimate plus one third-order Newton step (the refinement
+// ocml's rsqrt uses, without its zero/inf class fix-ups: a zero vector gives NaN either way, which
+// every caller culls)
+__device__ inline double frsq(double s) {
     const double y = __builtin_amdgcn_rsq(s);
     const double e = fma(-s * y, y, 1.0);  // 1 - s y^2
     double h;  // e * 0.375 + 0.5, the 0.375 from an SGPR (see fma_s)
     asm("v_fma_f64 %0, %1, %2, 0.5" : "=v"(h) : "v"(e), "s"(0.375));
-    const double r = fma(y * e, h, y);
+    return fma(y * e, h, y);
+}
+// a / |a|
+__device__ inline d3 funit(d3 a) {
+    const double r = frsq(fdot(a, a));
     return d3{a.x * r, a.y * r, a.z * r};
 }
 // num / den for den > 0 (finite): hardware reciprocal estimate plus one third-order step
@@ -247,17 +250,26 @@ __device__ inline double clamp1(double x) { return fmax(-1.0, fmin(1.0, x)); }
 // ocml's ~100.  Octant reduction: y <= k|x|: z = y/|x|; |x| <= k y: z = -|x|/y (+pi/2);
 // otherwise z = (y-|x|)/(y+|x|) (+pi/4); then pi - r for x < 0.
 // atan(z) for |z| <= tan(pi/8): z + z^3 P(z^2)
+// The Horner chain is ONE asm block: between two separate asm statements the compiler's hazard
+// recognizer cannot see the instructions and pads each boundary with an s_nop (8 per call); a
+// dependent v_fma_f64 chain needs no software wait states on gfx950.
 __device__ inline double atan_core(double z) {
     const double s = z * z;
-    double p = fma_s(0.023022964535612277, s, -0.045054138438556275);
-    p = fma_s(p, s, 0.05743860627393907);
-    p = fma_s(p, s, -0.0665101622857059);
-    p = fma_s(p, s, 0.07691210259772996);
-    p = fma_s(p, s, -0.09090862908839843);
-    p = fma_s(p, s, 0.11111110041613353);
-    p = fma_s(p, s, -0.14285714274661848);
-    p = fma_s(p, s, 0.19999999999980458);
-    p = fma_s(p, s, -0.33333333333333476);
+    double p;
+    asm("v_fma_f64 %0, %2, %1, %3\n\t"
+        "v_fma_f64 %0, %0, %1, %4\n\t"
+        "v_fma_f64 %0, %0, %1, %5\n\t"
+        "v_fma_f64 %0, %0, %1, %6\n\t"
+        "v_fma_f64 %0, %0, %1, %7\n\t"
+        "v_fma_f64 %0, %0, %1, %8\n\t"
+        "v_fma_f64 %0, %0, %1, %9\n\t"
+        "v_fma_f64 %0, %0, %1, %10\n\t"
+        "v_fma_f64 %0, %0, %1, %11"
+        : "=&v"(p)
+        : "v"(s), "v"(0.023022964535612277), "s"(-0.045054138438556275), "s"(0.05743860627393907),
+          "s"(-0.0665101622857059), "s"(0.07691210259772996), "s"(-0.09090862908839843),
+          "s"(0.11111110041613353), "s"(-0.14285714274661848), "s"(0.19999999999980458),
+          "s"(-0.33333333333333476));
     return fma(z * s, p, z);
 }
 __device__ inline double atan2_pos(double y, double x) {
@@ -282,81 +294,80 @@ __device__ inline double atan2_pos_wave(double y, double x) {
     return atan2_pos(y, x);
 }
 
-// Weight of one light triangle for the prep kernel (Mylight.cpp:360-413): the same quantity as
-// light_full's w without the parts only Arvo's sampler needs (orientation, alpha, c).  The edge
-// culls a,b,c < 1e-8 are kept (as clamp(cos) >= 1); the vertex-angle culls alpha,beta,gamma < 1e-8
-// mark a degenerate (zero-area) spherical triangle, which here is sA <= 0.  Returns false if culled.
-__device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, double* w_out);
-
 // Stage 3 (Mylight.cpp:360-413) in fp64 with fewer instructions than the reference's literal
 // formulation; identical up to rounding (DESIGN.md "light prep numerics"):
-//  * unit vectors by rsqrt instead of sqrt + 3 divisions; the B/C orientation test on the
-//    un-normalised edge vectors (normalising by positive lengths cannot change the sign);
-//  * the edge-length culls a,b,c < 1e-8 rad as clamp(cos) >= 1: in fp64, acos(x) < 1e-8 iff x
-//    rounds to 1 (acos of the largest double below 1 is 1.49e-8), so no acos is needed for them;
-//  * the vertex-angle culls alpha, beta, gamma < 1e-8 (a degenerate, zero-area spherical
-//    triangle) as sA <= 0 -- identical to light_weight, so the prep kernel and this function agree
-//    on every survivor;
+//  * unit vectors A, B, C by rsqrt instead of sqrt + 3 divisions;
 //  * the spherical excess sA = alpha + beta + gamma - pi by the Van Oosterom-Strackee identity
-//    sA = 2 atan2(|A.(BxC)|, 1 + A.B + B.C + C.A) (one atan2 instead of three acos, and free of the
-//    cancellation of alpha+beta+gamma-pi for small triangles);
-//  * alpha (needed only by Arvo's sampling of the picked triangle) and c only when want_alpha_c.
+//    sA = 2 atan2(|A.(B x C)|, 1 + A.B + B.C + C.A) (one atan2 instead of six acos, and free of
+//    the cancellation of alpha+beta+gamma-pi for small triangles);
+//  * the edge-length culls a,b,c < 1e-8 rad as cos >= 1 (NaN included): in fp64, acos(x) < 1e-8
+//    iff x rounds to 1 (acos of the largest double below 1 is 1.49e-8), so no acos is needed;
+//  * the vertex-angle culls alpha, beta, gamma < 1e-8 (a degenerate, zero-area spherical
+//    triangle) as sA <= 0.
+// Every consumer (the prep batches, the small-N_L lane prep, the pdf's survival test in
+// k_mis_combine and the picked triangle's Arvo setup in k_mis_gen / k_shade_gen) goes through
+// sph_excess on the same unswapped vectors, so they agree bit for bit on survival and sA.
+struct SphEx {
+    d3 A, B, C;     // unit vectors towards p0, p1, p2 (reference vertex order)
+    double ab;      // A.B
+    double sA;
+    bool edges_ok;  // A.B, B.C, C.A < 1
+};
+__device__ inline SphEx sph_excess(d3 a, d3 b, d3 c) {
+    SphEx e;
+    e.A = funit(a);
+    e.B = funit(b);
+    e.C = funit(c);
+    const double ab = fdot(e.A, e.B), bc = fdot(e.B, e.C), ca = fdot(e.C, e.A);
+    e.ab = ab;
+    e.edges_ok = (ab < 1.0) & (bc < 1.0) & (ca < 1.0);
+    e.sA = 2.0 * atan2_pos_wave(fabs(fdot(e.A, fcross(e.B, e.C))), 1.0 + ab + bc + ca);
+    return e;
+}
+
+// Weight of one light triangle (Mylight.cpp:360-413) without branches: every lane evaluates
+// straight through and the culls become one predicate.  Returns w, or 0 if culled (*ok = false).
+__device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, bool* ok) {
+    const SphEx e = sph_excess(sub(p0, x1), sub(p1, x1), sub(p2, x1));
+    const double w = e.sA * lsum;
+    const bool good = e.edges_ok & (e.sA > 0) & (w >= 0) & (w <= __DBL_MAX__);
+    *ok = good;
+    return good ? w : 0.0;
+}
+__device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, double* w_out) {
+    bool ok;
+    *w_out = light_weight_bf(p0, p1, p2, lsum, x1, &ok);
+    return ok;
+}
+
+// The picked triangle's spherical triangle for Arvo's sampler: the same survival and sA as
+// light_weight_bf, plus unit vectors in the reference's orientation (B, C swapped so that the
+// triangle winds counter-clockwise about n, Mylight.cpp:366-371; the test runs on the
+// un-normalised edge vectors, normalising by positive lengths cannot change its sign), alpha
+// (the angle at A between the great arcs AB and AC, Mylight.cpp:385) and c = acos(A.B).
 // Returns true if the triangle survives; fills o.
-__device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, d3 n, SphTri* o, bool want_c) {
-    // want_c: also compute alpha and c = acos(A.B) (Arvo sampling of the picked triangle)
-    const d3 A = funit(sub(p0, x1));
-    d3 B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
+__device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, d3 n, SphTri* o) {
+    const SphEx e = sph_excess(sub(p0, x1), sub(p1, x1), sub(p2, x1));
+    const double w = e.sA * lsum;
+    if (!(e.edges_ok & (e.sA > 0) & (w >= 0) & (w <= __DBL_MAX__))) return false;
+    const d3 A = e.A;
+    d3 B = e.B, C = e.C;
+    double ab = e.ab;
     if (fdot(fcross(sub(C, A), sub(B, A)), n) < 0) {
         const d3 t = B;
         B = C;
         C = t;
+        ab = fdot(A, B);
     }
-    const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
-    if (clamp1(bc) >= 1.0 || clamp1(ca) >= 1.0 || clamp1(ab) >= 1.0) return false;
-    const double sA = 2.0 * atan2_pos(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
-    if (!(sA > 0)) return false;  // degenerate: the vertex-angle culls (see light_weight)
-    const double w = sA * lsum;
-    if (w < 0 || isinf(w) || isnan(w)) return false;
-    if (o) {
-        o->A = A;
-        o->B = B;
-        o->C = C;
-        o->alpha = 0.0;
-        o->c = 0.0;
-        if (want_c) {  // alpha = angle at A between the great arcs AB and AC (Mylight.cpp:385)
-            const d3 u1 = fcross(B, A), u2 = fcross(A, C);
-            o->alpha = acos(clamp1(-(fdot(u1, u2) * rsqrt(fdot(u1, u1)) * rsqrt(fdot(u2, u2)))));
-            o->c = acos(clamp1(ab));
-        }
-        o->sA = sA;
-        o->w = w;
-    }
+    o->A = A;
+    o->B = B;
+    o->C = C;
+    const d3 u1 = fcross(B, A), u2 = fcross(A, C);
+    o->alpha = acos(clamp1(-(fdot(u1, u2) * rsqrt(fdot(u1, u1)) * rsqrt(fdot(u2, u2)))));
+    o->c = acos(clamp1(ab));
+    o->sA = e.sA;
+    o->w = w;
     return true;
-}
-
-__device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, double* w_out) {
-    const d3 A = funit(sub(p0, x1)), B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
-    const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
-    if (clamp1(bc) >= 1.0 || clamp1(ca) >= 1.0 || clamp1(ab) >= 1.0) return false;
-    const double sA = 2.0 * atan2_pos(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
-    if (!(sA > 0)) return false;
-    const double w = sA * lsum;
-    if (w < 0 || isinf(w) || isnan(w)) return false;
-    *w_out = w;
-    return true;
-}
-
-// light_weight without branches, for the prep kernel's dense batches: vertices in fp64, every
-// lane evaluates straight through and the culls become one predicate at the end.  clamp1(x) >= 1
-// (light_full's edge culls) is !(x < 1), NaN included.  Returns w, or 0 if culled (*ok = false).
-__device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, bool* ok) {
-    const d3 A = funit(sub(p0, x1)), B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
-    const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
-    const double sA = 2.0 * atan2_pos_wave(fabs(fdot(A, fcross(B, C))), 1.0 + ab + bc + ca);
-    const double w = sA * lsum;
-    const bool good = (ab < 1.0) & (bc < 1.0) & (ca < 1.0) & (sA > 0) & (w >= 0) & (w <= __DBL_MAX__);
-    *ok = good;
-    return good ? w : 0.0;
 }
 
 // Arvo SampleTriangle (Mylight.cpp:453-461)

@@ -557,6 +557,10 @@ __device__ inline unsigned long long wave_sum_u64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+__device__ inline int wave_sum_int(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
 __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                    const double* __restrict__ qn, const int* __restrict__ qpixel,
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
@@ -930,13 +934,24 @@ __device__ inline float4 u4f(v4u v) {
 __device__ inline double u2d(unsigned lo, unsigned hi) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+// structured (idxen) buffer load: address = base + vindex * stride (from the descriptor) + offset,
+// so a light index from the candidate list needs no VALU address arithmetic (hipcc has no builtin
+// for the struct form; this binds the LLVM intrinsic by name)
+__device__ v4u struct_load_b128(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+constexpr int kLtW = 80;  // bytes per light record in lt_w (the descriptor's stride)
+// the light-record descriptor for k_prep_pk2 / prep_select: stride kLtW, the whole padded table
+// plus the sentinel records (lt_w has nl_pad + kSentinelPad records)
+constexpr int kSentinelPad = 64;
+__device__ inline __amdgpu_buffer_rsrc_t light_record_rsrc(const DScene& S, int ngroups4) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_w, kLtW, (ngroups4 * 256 + kSentinelPad) * kLtW, kBufFlags);
+}
 __device__ inline double prep_weight_buf(__amdgpu_buffer_rsrc_t rw, int li, d3 x1, bool* ok) {
-    const int o = li * 80;
-    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, 0);
-    const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 16, 0, 0);
-    const v4u c = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 32, 0, 0);
-    const v4u d = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 48, 0, 0);
-    const v4u e = __builtin_amdgcn_raw_buffer_load_b128(rw, o + 64, 0, 0);
+    const v4u a = struct_load_b128(rw, li, 0, 0, 0);
+    const v4u b = struct_load_b128(rw, li, 16, 0, 0);
+    const v4u c = struct_load_b128(rw, li, 32, 0, 0);
+    const v4u d = struct_load_b128(rw, li, 48, 0, 0);
+    const v4u e = struct_load_b128(rw, li, 64, 0, 0);
     return light_weight_bf(mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y)),
                            mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
                            mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1, ok);
@@ -961,7 +976,7 @@ __device__ inline void append_masked(uint64_t m, unsigned lo, unsigned hi, unsig
         "s_mov_b64 exec, %[sv]"
         : [sv] "=&s"(saved), [t] "=&v"(t)
         : [m] "s"(m), [lo] "s"(lo), [hi] "s"(hi), [b] "s"(base_bytes), [x] "v"(idx)
-        : "memory");
+        : "memory", "scc");  // s_and_saveexec writes SCC
 }
 
 // Root-point cache.  Every camera sample of a pixel starts at the same shading point (the
@@ -1190,6 +1205,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
 
+constexpr int kMaskBatch = 8;  // candidate words per batch of scalar loads (k_prep_pk2)
 template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
@@ -1207,8 +1223,12 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
     const int ngroups4 = (nchunks + 3) / 4;
     const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, ngroups4 * 4 * 3072, kBufFlags);
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, ngroups4 * 4 * 256, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_w, 0, ngroups4 * 4 * 5120, kBufFlags);
-    unsigned long long surv_acc = 0, cand_acc = 0, c1_acc = 0, full_acc = 0;
+    const __amdgpu_buffer_rsrc_t rw = light_record_rsrc(S, ngroups4);
+    // list padding: the entries [ncand, 64 nb) of the last batch name a sentinel record past the
+    // table, which the full stage always culls, so a batch needs no k < ncand test
+    const unsigned short sentinel = (unsigned short)(ngroups4 * 256);
+    unsigned long long cand_acc = 0, c1_acc = 0, full_acc = 0, pad_acc = 0;
+    unsigned bad_acc = 0;  // per lane: culled lanes of phase B, padding included
     int grab = 0, left = 0;
     while (true) {
         if (left == 0) {
@@ -1227,16 +1247,21 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         };
         int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
         if (kMaskIn) {  // phase A done by k_prep_cull_lanes: rebuild the list from the candidate words
+            // The node's words are wave-uniform: scalar loads (8 in flight) put each straight into
+            // SGPRs, so a word costs 3 VALU (2 v_mbcnt + 1 v_lshl_add) + 1 v_add for the index
+            // instead of 2 v_readlane more.  Words past nchunks are read (the scratch is padded by
+            // one tile) and zeroed by a scalar select.
             const unsigned lds_lst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lst);  // LDS offset (low half of the flat address)
-            for (int c0 = 0; c0 < nchunks; c0 += 64) {  // one vector load of up to 64 words, then readlanes
-                const unsigned long long mv = c0 + lane < nchunks ? masks[mask_index(node, c0 + lane, nchunks)] : 0ull;
-                const int cend = __builtin_amdgcn_readfirstlane(min(64, nchunks - c0));
-                unsigned idx = (unsigned)(c0 * 64 + lane);
-                for (int q = 0; q < cend; q++) {
-                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(mv >> 32), q);
-                    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mv, q);
-                    const uint64_t m = ((uint64_t)hi << 32) | lo;
-                    append_masked(m, lo, hi, lds_lst + 2u * (unsigned)ncand, idx);
+            const uint64_t* __restrict__ mrow = masks + mask_index(node, 0, nchunks);
+            unsigned idx = (unsigned)lane;
+            for (int c0 = 0; c0 < nchunks; c0 += kMaskBatch) {
+                uint64_t mw[kMaskBatch];
+#pragma unroll
+                for (int q = 0; q < kMaskBatch; q++) mw[q] = mrow[(size_t)(c0 + q) * 8];
+#pragma unroll
+                for (int q = 0; q < kMaskBatch; q++) {
+                    const uint64_t m = c0 + q < nchunks ? mw[q] : 0ull;
+                    append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_lst + 2u * (unsigned)ncand, idx);
                     ncand += __popcll(m);
                     idx += 64;
                 }
@@ -1271,9 +1296,14 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             }
         }
         }
-        wave_lds_sync();
-        // phase B: dense fp64 batches of 64 consecutive candidates, four at a time (batch_totals4)
         nb = (ncand + 63) >> 6;
+        if (ncand + lane < 64 * nb) lst[ncand + lane] = sentinel;  // pad the last batch
+        wave_lds_sync();
+        // phase B: dense fp64 batches of 64 consecutive candidates, four at a time (batch_totals4).
+        // Culled lanes (the full stage's rare culls and the sentinel padding) are counted by a
+        // branch on the exec mask that is almost never taken except for the padding, instead of a
+        // ballot per batch; survivors = ncand - (culled lanes - padding).
+        int nbad = 0;
         for (int b0 = 0; b0 < nb; b0 += 4) {
             double w4[4];
 #pragma unroll
@@ -1281,21 +1311,22 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                 w4[i] = 0.0;
                 if (b0 + i < nb) {  // wave-uniform
                     const int k = 64 * (b0 + i) + lane;
-                    const bool act = k < ncand;
                     bool ok;
-                    const double w = prep_weight_buf(rw, act ? (int)lst[k] : 0, x1, &ok);  // 0 if culled
-                    ok = ok && act;
-                    if (kBuild && act) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
-                    w4[i] = act ? w : 0.0;
-                    survivors += __popcll(__ballot(ok));
+                    const double w = prep_weight_buf(rw, (int)lst[k], x1, &ok);  // 0 if culled
+                    if (kBuild && k < ncand) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
+                    w4[i] = w;
+                    if (!ok) asm volatile("v_add_u32 %0, 1, %0" : "+v"(nbad));  // a real branch (SALU only when no lane is culled)
                 }
             }
             const double t = batch_totals4(w4[0], w4[1], w4[2], w4[3]);
             if ((lane & 15) == 15 && b0 + (lane >> 4) < nb) bt[b0 + (lane >> 4)] = t;
         }
         wave_lds_sync();
+        const int npad = 64 * nb - ncand;
+        if (kBuild || count_out) survivors = ncand - (wave_sum_int(nbad) - npad);
+        bad_acc += nbad;
+        pad_acc += npad;
         full_acc++;
-        surv_acc += survivors;
         cand_acc += ncand;
         c1_acc += culled1;
         if (kBuild) {  // store the entry of this pixel (C.build)
@@ -1315,11 +1346,14 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         }
         wave_lds_sync();
     }
-    if (lane == 0 && stats) {
-        if (surv_acc) atomicAdd(stats + 1, surv_acc);
-        if (cand_acc) atomicAdd(stats + 5, cand_acc);
-        if (c1_acc) atomicAdd(stats + 6, c1_acc);
-        if (full_acc) atomicAdd(stats + 7, full_acc);
+    if (stats) {
+        const unsigned long long surv_acc = cand_acc - (wave_sum_u64(bad_acc) - pad_acc);
+        if (lane == 0) {
+            if (surv_acc) atomicAdd(stats + 1, surv_acc);
+            if (cand_acc) atomicAdd(stats + 5, cand_acc);
+            if (c1_acc) atomicAdd(stats + 6, c1_acc);
+            if (full_acc) atomicAdd(stats + 7, full_acc);
+        }
     }
 }
 
@@ -1494,7 +1528,7 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
     if (pick >= 0) {
         const double4 ln = S.lt_n[pick];
         SphTri sph;
-        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph, true);
+        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph);
         const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
         TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
         coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:475-481)
@@ -1621,7 +1655,7 @@ __global__ __launch_bounds__(256) void k_shade_gen(Params P, Queue cur, int n, A
     if (pick >= 0) {
         const double4 ln = S.lt_n[pick];
         SphTri sph;
-        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph, true);
+        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph);
         const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
         TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
         coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:311-317)
@@ -1921,7 +1955,12 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     const int nl_pad = 256 * ((prep_chunks(s.NL) + 3) / 4);  // whole groups of 4 chunks: the prep kernel reads past N_L unchecked
     std::vector<float4> lpk(3 * nl_pad, make_float4(0, 0, 0, 0));
     std::vector<float> ld(nl_pad, 0.0f);
-    std::vector<double2> lw(5 * nl_pad, make_double2(0, 0));
+    // + kSentinelPad sentinel records (zero vertices, lsum = -1): k_prep_pk2 pads its candidate
+    // batches with index nl_pad; the full stage culls them for any x1, as sA > 0 gives w < 0 and
+    // sA <= 0 or NaN fail directly (a zero lsum could pass with w = 0), and sA stays on the atan
+    // fast path (|y| ~ 0, x ~ 4)
+    std::vector<double2> lw(5 * (nl_pad + kSentinelPad), make_double2(0, 0));
+    for (int l = nl_pad; l < nl_pad + kSentinelPad; l++) lw[5 * (size_t)l + 4] = make_double2(0.0, -1.0);
     for (int l = 0; l < s.NL; l++) {
         const float4 a = lv[3 * l], b = lv[3 * l + 1], c = lv[3 * l + 2];
         lpk[3 * l] = make_float4(a.x, b.x, c.x, a.w);
@@ -2174,7 +2213,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
     if (o->mode != MCPT_MODE_BRDF && D.d.NL > kSmallNL) {
-        if ((rc = ensure(D.masks, (size_t)((std::max(cap, npx) + 7) / 8 * 8) * nchunks * 8))) return rc;
+        // + one tile of padding: k_prep_pk2 reads whole batches of kMaskBatch words past nchunks
+        if ((rc = ensure(D.masks, ((size_t)((std::max(cap, npx) + 7) / 8 * 8) * nchunks + 8 * kMaskBatch) * 8))) return rc;
         masks = (uint64_t*)D.masks.p;
     }
     // root-point cache (see PrepCache): built here when the call has >= 2 samples per pixel and the

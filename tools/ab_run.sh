@@ -1,10 +1,13 @@
 #!/bin/bash
-# On the GPU box: alternate the two builds of tools/ab_build.sh through bench.py (same box, same
-# clocks), ROUNDS times each, printing Msamples/s per run.  Extra args go to bench.py.
+# On the GPU box: alternate the builds ab/lib<V>.so (tools/ab_build.sh makes A = HEAD and B = the
+# working tree; more variants can be dropped into ab/ by hand) through bench.py (same box, same
+# clocks), ROUNDS times each, printing Msamples/s and the light-prep launch time per run.
+# VARIANTS="A B C" selects the builds; extra args go to bench.py.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 ROUNDS=${ROUNDS:-3}
+VARIANTS=${VARIANTS:-A B}
 for r in $(seq "$ROUNDS"); do
-    for v in A B; do
+    for v in $VARIANTS; do
         out=$(MCPT_LIB_PATH=ab/lib$v.so timeout -k 10 200 python bench.py --no-cpu "$@" 2>/dev/null | grep '^{') || exit 1
         echo "$v $(echo "$out" | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["avg_launch_ms"])')"
     done
