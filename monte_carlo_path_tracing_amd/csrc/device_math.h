@@ -221,27 +221,27 @@ __device__ inline double fma_s(double a, double b, double c) {
     return r;
 }
 
-// 1/sqrt(s) by the hardware rsqrt estimate plus one third-order Newton step (the refinement
-// ocml's rsqrt uses, without its zero/inf class fix-ups: a zero vector gives NaN either way, which
-// every caller culls)
+// 1/sqrt(s) by the hardware rsqrt estimate plus one second-order Newton step, y (1 + e/2) with
+// e = 1 - s y^2: relative error ~1.5 e0^2 ~ 1e-14 for the estimate's e0 (weights agree with the
+// third-order refinement to ~1e-13 relative, measured; a third-order step costs one more fp64
+// FMA per vector in the prep's hottest loop).  No zero/inf fix-ups: a zero vector gives NaN,
+// which every caller culls.
 __device__ inline double frsq(double s) {
     const double y = __builtin_amdgcn_rsq(s);
     const double e = fma(-s * y, y, 1.0);  // 1 - s y^2
-    double h;  // e * 0.375 + 0.5, the 0.375 from an SGPR (see fma_s)
-    asm("v_fma_f64 %0, %1, %2, 0.5" : "=v"(h) : "v"(e), "s"(0.375));
-    return fma(y * e, h, y);
+    return fma(y * e, 0.5, y);
 }
 // a / |a|
 __device__ inline d3 funit(d3 a) {
     const double r = frsq(fdot(a, a));
     return d3{a.x * r, a.y * r, a.z * r};
 }
-// num / den for den > 0 (finite): hardware reciprocal estimate plus one third-order step
-// (r (1 + e + e^2), e = 1 - den r), then one rounding in the product (<= ~1.5 ulp)
+// num / den for den > 0 (finite): hardware reciprocal estimate plus one second-order step
+// r (1 + e), e = 1 - den r, then one rounding in the product (~1e-14 relative)
 __device__ inline double fdiv_pos(double num, double den) {
     const double r = __builtin_amdgcn_rcp(den);
     const double e = fma(-den, r, 1.0);
-    return num * fma(r, fma(e, e, e), r);
+    return num * fma(r, e, r);
 }
 __device__ inline double clamp1(double x) { return fmax(-1.0, fmin(1.0, x)); }
 
