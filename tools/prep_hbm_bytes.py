@@ -20,7 +20,8 @@ import os
 
 
 def per_kernel(d, counter):
-    path = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    path = (glob.glob(os.path.join(d, "*counter_collection.csv")) +  # --output-format csv
+            glob.glob(os.path.join(d, "*counter_collection_trace.csv")))[0]  # rocpd2csv of the default db
     tot = collections.defaultdict(float)
     n = collections.Counter()
     for r in csv.DictReader(open(path)):

@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Turns the rocprofv3 CSVs of a GPU run (gpurun_out/) into the committed summaries (profiles/).
 
+Either rocprofv3's CSV output (--output-format csv) or its default rocpd database converted with
+`rocpd2csv -i run_results.db -d DIR` (counters) and `rocpd2summary -i run_results.db -f csv -d DIR`
+(kernel stats) is accepted.
+
     python tools/summarize_profiles.py --tag round1 --stats gpurun_out/prof_r1 \
         --fetch gpurun_out/pmc_r1_fetch --write gpurun_out/pmc_r1_write --sq gpurun_out/pmc_r1_sq \
         --bench gpurun_out/bench_default.log
@@ -25,7 +29,10 @@ def short(name):
 
 
 def counters(d):
-    path = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    # rocprofv3 --output-format csv writes *counter_collection.csv; rocpd2csv (from the default
+    # rocpd database output) writes out_counter_collection_trace.csv with the same columns
+    path = (glob.glob(os.path.join(d, "*counter_collection.csv")) +
+            glob.glob(os.path.join(d, "*counter_collection_trace.csv")))[0]
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
@@ -46,8 +53,14 @@ def main():
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    stats_csv = glob.glob(os.path.join(a.stats, "*kernel_stats.csv"))[0]
-    rows = list(csv.DictReader(open(stats_csv)))
+    stats = glob.glob(os.path.join(a.stats, "*kernel_stats.csv"))
+    if stats:
+        rows = list(csv.DictReader(open(stats[0])))
+    else:  # rocpd2summary -f csv: *_kernels_summary.csv, durations in columns "... (Nsec)"
+        rows = [{"Name": r["Name"], "Calls": r["Calls"], "TotalDurationNs": r["Duration (Nsec)"],
+                 "AverageNs": r["Average (Nsec)"], "Percentage": r["Percent (Inc)"],
+                 "MinNs": r["Min (Nsec)"], "MaxNs": r["Max (Nsec)"]}
+                for r in csv.DictReader(open(glob.glob(os.path.join(a.stats, "*kernels_summary.csv"))[0]))]
     with open(os.path.join(out, "%s_kernel_stats.csv" % a.tag), "w") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "calls", "total_ms", "avg_us", "percent", "min_us", "max_us"])
