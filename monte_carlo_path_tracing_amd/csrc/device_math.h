@@ -310,7 +310,7 @@ __device__ inline double atan2_pos_wave(double y, double x) {
 struct SphEx {
     d3 A, B, C;     // unit vectors towards p0, p1, p2 (reference vertex order)
     double ab;      // A.B
-    double sA;
+    double half;    // sA / 2
     bool edges_ok;  // A.B, B.C, C.A < 1
 };
 __device__ inline SphEx sph_excess(d3 a, d3 b, d3 c) {
@@ -321,35 +321,38 @@ __device__ inline SphEx sph_excess(d3 a, d3 b, d3 c) {
     const double ab = fdot(e.A, e.B), bc = fdot(e.B, e.C), ca = fdot(e.C, e.A);
     e.ab = ab;
     e.edges_ok = (ab < 1.0) & (bc < 1.0) & (ca < 1.0);
-    e.sA = 2.0 * atan2_pos_wave(fabs(fdot(e.A, fcross(e.B, e.C))), 1.0 + ab + bc + ca);
+    e.half = atan2_pos_wave(fabs(fdot(e.A, fcross(e.B, e.C))), 1.0 + ab + bc + ca);
     return e;
 }
 
 // Weight of one light triangle (Mylight.cpp:360-413) without branches: every lane evaluates
-// straight through and the culls become one predicate.  Returns w, or 0 if culled (*ok = false).
-__device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, bool* ok) {
+// straight through and the culls become one predicate.  lsum2 = 2 RadianceRGB::sum(), so
+// w = (sA/2) lsum2 rounds exactly like the reference's sA * sum (scaling by 2 is exact) without
+// the doubling of sA; 0 <= w <= DBL_MAX is one v_cmp_class (-0, +0, +denormal, +normal).
+// Returns w, or 0 if culled (*ok = false).
+__device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, bool* ok) {
     const SphEx e = sph_excess(sub(p0, x1), sub(p1, x1), sub(p2, x1));
-    const double w = e.sA * lsum;
-    const bool good = e.edges_ok & (e.sA > 0) & (w >= 0) & (w <= __DBL_MAX__);
+    const double w = e.half * lsum2;
+    const bool good = e.edges_ok & (e.half > 0) & __builtin_amdgcn_class(w, 0x1e0);
     *ok = good;
     return good ? w : 0.0;
 }
-__device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, double* w_out) {
+__device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, double* w_out) {
     bool ok;
-    *w_out = light_weight_bf(p0, p1, p2, lsum, x1, &ok);
+    *w_out = light_weight_bf(p0, p1, p2, lsum2, x1, &ok);
     return ok;
 }
 
 // The picked triangle's spherical triangle for Arvo's sampler: the same survival and sA as
-// light_weight_bf, plus unit vectors in the reference's orientation (B, C swapped so that the
+// light_weight_bf (lsum2 = 2 RadianceRGB::sum()), plus unit vectors in the reference's orientation (B, C swapped so that the
 // triangle winds counter-clockwise about n, Mylight.cpp:366-371; the test runs on the
 // un-normalised edge vectors, normalising by positive lengths cannot change its sign), alpha
 // (the angle at A between the great arcs AB and AC, Mylight.cpp:385) and c = acos(A.B).
 // Returns true if the triangle survives; fills o.
-__device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, d3 n, SphTri* o) {
+__device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, d3 n, SphTri* o) {
     const SphEx e = sph_excess(sub(p0, x1), sub(p1, x1), sub(p2, x1));
-    const double w = e.sA * lsum;
-    if (!(e.edges_ok & (e.sA > 0) & (w >= 0) & (w <= __DBL_MAX__))) return false;
+    const double w = e.half * lsum2;
+    if (!(e.edges_ok & (e.half > 0) & __builtin_amdgcn_class(w, 0x1e0))) return false;
     const d3 A = e.A;
     d3 B = e.B, C = e.C;
     double ab = e.ab;
@@ -365,7 +368,7 @@ __device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum, d3 x1, d3 n,
     const d3 u1 = fcross(B, A), u2 = fcross(A, C);
     o->alpha = acos(clamp1(-(fdot(u1, u2) * rsqrt(fdot(u1, u1)) * rsqrt(fdot(u2, u2)))));
     o->c = acos(clamp1(ab));
-    o->sA = e.sA;
+    o->sA = 2.0 * e.half;
     o->w = w;
     return true;
 }

@@ -70,7 +70,7 @@ struct DScene {
     const double4* lt_n;      // NL: unique normal xyz, w = RadianceRGB::sum()
     const float4* lt_pk;      // NL*3: (p0.x, p1.x, p2.x, nl.x), (.. .y), (.. .z) -- packed cheap stages
     const float* lt_d;        // NL: float(nl . p0)
-    const double2* lt_w;      // NL*5: p0, p1, p2 (fp64), RadianceRGB::sum()
+    const double2* lt_w;      // NL*5: p0, p1, p2 (fp64), 2 RadianceRGB::sum()
     const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
     const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves)
@@ -710,11 +710,11 @@ __device__ inline double batch_totals4(double a, double b, double c, double d) {
 
 struct PrepLight {
     d3 p0, p1, p2, nl;
-    double lsum;
+    double lsum2;  // 2 RadianceRGB::sum()
 };
 __device__ inline PrepLight load_light(const DScene& S, int li) {
     const double4 ln = S.lt_n[li];
-    return PrepLight{f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]), mk3(ln.x, ln.y, ln.z), ln.w};
+    return PrepLight{f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]), mk3(ln.x, ln.y, ln.z), 2.0 * ln.w};
 }
 // The cheap stages evaluated in fp32 with a rigorous rounding-error bound `err`, falling back to
 // the exact fp64 reference arithmetic only when a value lies within err of the 1e-8 threshold:
@@ -804,7 +804,7 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
                 bool ok = false;
                 if (act) {
                     const PrepLight L = load_light(S, lj);
-                    ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
+                    ok = light_weight(L.p0, L.p1, L.p2, L.lsum2, x1, &w);
                     if (!ok) w = 0;
                 }
                 const double sc = wave_incl_scan(w, lane);
@@ -872,7 +872,7 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
             bool ok = false;
             if (act) {
                 const PrepLight L = load_light(S, lj);
-                ok = light_weight(L.p0, L.p1, L.p2, L.lsum, x1, &w);
+                ok = light_weight(L.p0, L.p1, L.p2, L.lsum2, x1, &w);
                 if (!ok) w = 0;
             }
             const double sc = wave_incl_scan(w, lane);
@@ -1459,27 +1459,34 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
             }
         }
         double wc[kPickNodes];
-        int lj[kPickNodes];
 #pragma unroll
         for (int k = 0; k < kPickNodes; k++) {
             const int j = 64 * kb[k] + lane;
             const bool act = kb[k] >= 0 && j < inf[k].y;
             wc[k] = act ? C.w[(size_t)px[k] * C.lstride + j] : -1.0;
-            lj[k] = act ? (int)C.lst[(size_t)px[k] * C.lstride + j] : 0;
         }
+        // the picked lane's light index only (one uniform load per root, issued for all roots
+        // before waiting) instead of the batch's 64 list entries
+        int pls[kPickNodes];
 #pragma unroll
         for (int k = 0; k < kPickNodes; k++) {
-            int pick = -1;
+            pls[k] = -1;
             if (kb[k] >= 0) {
                 const bool ok = wc[k] >= 0;
                 const double sc = wave_incl_scan(ok ? wc[k] : 0.0, lane);
                 const uint64_t candm = __ballot(ok && (base[k] + sc >= target[k]));
                 const uint64_t okm = __ballot(ok);
-                int pl = -1;
-                if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-                else if (okm) pl = 63 - __clzll((long long)okm);
-                if (pl >= 0) pick = __shfl(lj[k], pl);
+                if (candm) pls[k] = __ffsll((unsigned long long)candm) - 1;
+                else if (okm) pls[k] = 63 - __clzll((long long)okm);
             }
+        }
+        int pk[kPickNodes];
+#pragma unroll
+        for (int k = 0; k < kPickNodes; k++)
+            pk[k] = pls[k] >= 0 ? (int)C.lst[(size_t)px[k] * C.lstride + 64 * kb[k] + pls[k]] : -1;
+#pragma unroll
+        for (int k = 0; k < kPickNodes; k++) {
+            const int pick = pk[k];
             if (lane == 0 && n0 + k < n) {
                 wsum_out[n0 + k] = wsum[k];
                 pick_out[n0 + k] = pick;
@@ -1528,7 +1535,7 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
     if (pick >= 0) {
         const double4 ln = S.lt_n[pick];
         SphTri sph;
-        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph);
+        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), 2.0 * ln.w, p, N, &sph);
         const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
         TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
         coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:475-481)
@@ -1615,7 +1622,7 @@ __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n,
             const int li = S.tri_light[lf];
             const PrepLight L = load_light(S, li);
             double wl_unused;
-            if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) && light_weight(L.p0, L.p1, L.p2, L.lsum, p, &wl_unused))
+            if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) && light_weight(L.p0, L.p1, L.p2, L.lsum2, p, &wl_unused))
                 lpdf = S.light_sum[li] / cur.wsum[ii];  // fresh-state eval (Mylight.cpp:484-493)
         }
         tp2 = mul(mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]), A.c2[2 * ii + 1] / (A.c2[2 * ii] + lpdf) / MCPT_P_RR);
@@ -1655,7 +1662,7 @@ __global__ __launch_bounds__(256) void k_shade_gen(Params P, Queue cur, int n, A
     if (pick >= 0) {
         const double4 ln = S.lt_n[pick];
         SphTri sph;
-        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), ln.w, p, N, &sph);
+        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), 2.0 * ln.w, p, N, &sph);
         const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
         TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
         coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:311-317)
@@ -1955,7 +1962,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     const int nl_pad = 256 * ((prep_chunks(s.NL) + 3) / 4);  // whole groups of 4 chunks: the prep kernel reads past N_L unchecked
     std::vector<float4> lpk(3 * nl_pad, make_float4(0, 0, 0, 0));
     std::vector<float> ld(nl_pad, 0.0f);
-    // + kSentinelPad sentinel records (zero vertices, lsum = -1): k_prep_pk2 pads its candidate
+    // + kSentinelPad sentinel records (zero vertices, lsum2 = -1): k_prep_pk2 pads its candidate
     // batches with index nl_pad; the full stage culls them for any x1, as sA > 0 gives w < 0 and
     // sA <= 0 or NaN fail directly (a zero lsum could pass with w = 0), and sA stays on the atan
     // fast path (|y| ~ 0, x ~ 4)
@@ -1971,7 +1978,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
         lw[5 * l + 1] = make_double2(a.z, b.x);
         lw[5 * l + 2] = make_double2(b.y, b.z);
         lw[5 * l + 3] = make_double2(c.x, c.y);
-        lw[5 * l + 4] = make_double2(c.z, ln[l].w);
+        lw[5 * l + 4] = make_double2(c.z, 2.0 * ln[l].w);
     }
     std::vector<LightPair> lpr(32 * (size_t)std::max(prep_chunks(s.NL), 1));
     for (size_t q = 0; q < lpr.size(); q++) {
