@@ -154,7 +154,7 @@ def main():
     for k in range(args.steps):
         s0 = (k * world + rank) * S
         st = mcpt.render_device(scene, cam, frame_spp, fb.data_ptr(), mode=args.mode, seed=args.seed,
-                                sample_range=(s0, s0 + S), device=local)
+                                sample_range=(s0, s0 + S), device=local, flags=mcpt.RENDER_NO_BACKFACE_STATS)
         for key, v in st.as_dict().items():
             totals[key] = totals.get(key, 0) + v
         if rank == 0 and time.perf_counter() - tlog > 30:
@@ -171,6 +171,22 @@ def main():
         elapsed = float(t.item())
     samples = float(W * H) * frame_spp
     value = samples / elapsed / 1e6
+    # The timed steps skip the light-side cull statistic (mcpt_render_opts.flags; one compare per
+    # (node, light) in the hot loop).  The roofline's flop count needs it: replay the same steps
+    # (same seed and sample ranges, so the same nodes) untimed into the scratch buffer with the
+    # statistic on, and check that the work the two runs counted is identical.
+    if args.mode != "brdf":
+        rep = {}
+        for k in range(args.steps):
+            s0 = (k * world + rank) * S
+            st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
+                                    sample_range=(s0, s0 + S), device=local)
+            for key, v in st.as_dict().items():
+                rep[key] = rep.get(key, 0) + v
+        for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes"):
+            assert rep.get(key) == totals.get(key), (key, rep.get(key), totals.get(key))
+        totals["light_evals_culled_backface"] = rep["light_evals_culled_backface"]
+        totals["light_evals_culled_plane"] = rep["light_evals_culled_plane"]
 
     log("rank %d totals: %s" % (rank, json.dumps({k: v for k, v in totals.items()})))
     if rank != 0:

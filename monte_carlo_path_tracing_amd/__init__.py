@@ -24,7 +24,7 @@ MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2  # shade_with_mis / shade_with_brdf / 
 ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
 HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
 DEFAULT_SEED = 20240430
-MCPT_VERSION = 10300  # include/mcpt.h MCPT_VERSION this mirror is written against
+MCPT_VERSION = 10400  # include/mcpt.h MCPT_VERSION this mirror is written against
 
 
 class MCPTError(RuntimeError):
@@ -53,7 +53,8 @@ class RenderOpts(C.Structure):
     _fields_ = [("spp", C.c_int32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32), ("mode", C.c_int32),
                 ("seed", C.c_uint64), ("samples_per_launch", C.c_int32), ("queue_factor", C.c_int32),
                 ("device", C.c_int32), ("accel", C.c_int32), ("progress", C.c_void_p),
-                ("progress_user", C.c_void_p)]
+                ("progress_user", C.c_void_p), ("flags", C.c_int32)]
+RENDER_NO_BACKFACE_STATS = 1  # mcpt_render_opts.flags (include/mcpt.h)
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_uint64)
@@ -183,9 +184,11 @@ class Scene:
         return c
 
 
-def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress=None, accel="bvh"):
+def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress=None, accel="bvh",
+          flags=0):
     """progress(done, total) -> truthy to cancel; the ctypes thunk is kept on the returned struct."""
     o = RenderOpts()
+    o.flags = int(flags)
     a = {"bvh": ACCEL_BVH, "grid": ACCEL_GRID}.get(accel, -1) if isinstance(accel, str) else int(accel)
     if a not in (ACCEL_BVH, ACCEL_GRID):
         raise ValueError("accel must be 'bvh' or 'grid'")
@@ -226,10 +229,11 @@ def render(scene, camera, spp, mode="mis", seed=DEFAULT_SEED, sample_range=None,
 
 
 def render_device(scene, camera, spp, dev_ptr, mode="mis", seed=DEFAULT_SEED, sample_range=None, device=None,
-                  samples_per_launch=0, queue_factor=0, progress=None, accel="bvh"):
-    """Accumulate into a device buffer of H*W*3 doubles (e.g. a torch.float64 CUDA tensor's data_ptr())."""
+                  samples_per_launch=0, queue_factor=0, progress=None, accel="bvh", flags=0):
+    """Accumulate into a device buffer of H*W*3 doubles (e.g. a torch.float64 CUDA tensor's data_ptr()).
+    flags: RENDER_NO_BACKFACE_STATS skips the light-side cull statistic (mcpt_render_opts.flags)."""
     st = Stats()
-    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel)
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel, flags)
     _check(lib().mcpt_render_device(scene.h, C.byref(camera), C.byref(o), C.c_void_p(int(dev_ptr)), C.byref(st)))
     return st
 

@@ -1128,6 +1128,7 @@ struct CullLane {
     }
 };
 
+template <bool kCountC1>
 __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
                                                          const double* __restrict__ qn, uint64_t* __restrict__ masks,
                                                          int nchunks, unsigned long long* stats) {
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
                     const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
                     // ambiguous lanes (a value within err of the threshold) have s >= -err and a clear bit here
                     amin = min3_abs_raw(amin, sv, mn);
-                    c1w += __popcll(__ballot(sv < -err) & actm);
+                    if (kCountC1) c1w += __popcll(__ballot(sv < -err) & actm);  // statistic only
                     w = shift_in(w, __ballot(mn > err));
                 }
             }
@@ -1191,7 +1192,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
                                                    mk3(pc(6), pc(7), pc(8)), mk3(ln.x, ln.y, ln.z), x1, nn);
                             if (st == 0) w |= 1u << (31 - (2 * q + e));
                         }
-                        c1w += __popcll(__ballot(st == 1));  // uniform: every lane of the wave
+                        if (kCountC1) c1w += __popcll(__ballot(st == 1));  // uniform: every lane of the wave
                     }
                 }
             }
@@ -1201,7 +1202,7 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
         if (act) masks[mask_index(node, c, nchunks)] = ((uint64_t)word[1] << 32) | word[0];
     }
     // padding lights (index >= N_L, d = 1e30) were counted as light-side culled by every active lane
-    if (ce == nchunks) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
+    if (kCountC1 && ce == nchunks) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
 
@@ -2090,7 +2091,7 @@ constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
-                       const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr) {
+                       const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr, bool count_c1 = true) {
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
@@ -2112,8 +2113,12 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
         hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
-        hipLaunchKernelGGL(k_prep_cull_lanes, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d, n, qp,
-                           qn, masks, nchunks, stats);
+        if (count_c1 || !stats)
+            hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d,
+                               n, qp, qn, masks, nchunks, stats);
+        else
+            hipLaunchKernelGGL(k_prep_cull_lanes<false>, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d,
+                               n, qp, qn, masks, nchunks, stats);
         if (cache.build)
             hipLaunchKernelGGL((k_prep_pk2<5, true, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
                                qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
@@ -2215,6 +2220,11 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
         return MCPT_E_SCENE;
     }
+    if (o->flags & ~MCPT_RENDER_NO_BACKFACE_STATS) {
+        set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
+        return MCPT_E_INVALID;
+    }
+    const bool count_c1 = !(o->flags & MCPT_RENDER_NO_BACKFACE_STATS);
     double prep_ms = 0;
     uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0;
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
@@ -2261,7 +2271,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
             HIP_OK(launch_prep(masks ? 17 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks));
+                               nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks, count_c1));
             HIP_OK(hipEventRecord(D.evp1, st));
             HIP_OK(hipEventSynchronize(D.evp1));
             float ms = 0;
@@ -2315,7 +2325,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 if (nc > 0) {
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks));
+                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks,
+                                       count_c1));
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
@@ -2329,7 +2340,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             } else {
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks));
+                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks,
+                                   count_c1));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 timed = true;
             }

@@ -200,6 +200,27 @@ def test_render_device_buffer_with_torch(scene):
     assert st.camera_samples == 64 * 48 * 4
 
 
+def test_no_backface_stats_flag(scene):
+    """mcpt_render_opts.flags = MCPT_RENDER_NO_BACKFACE_STATS (bench.py's timed steps): the same
+    image and work; only the light-side cull statistic is folded into the plane-cull count."""
+    torch = pytest.importorskip("torch")
+    cam = mcpt.Camera.reference(64, 48)
+    dev = torch.cuda.current_device()
+    fa = torch.zeros((48, 64, 3), dtype=torch.float64, device="cuda")
+    fb = torch.zeros_like(fa)
+    a = mcpt.render_device(scene, cam, 8, fa.data_ptr(), seed=SEED, device=dev).as_dict()
+    b = mcpt.render_device(scene, cam, 8, fb.data_ptr(), seed=SEED, device=dev,
+                           flags=mcpt.RENDER_NO_BACKFACE_STATS).as_dict()
+    torch.cuda.synchronize()
+    assert rel_l2(fb.cpu().numpy(), fa.cpu().numpy()) < 1e-12  # fp64 atomic accumulation order only
+    assert a["light_evals_culled_backface"] > 0 and b["light_evals_culled_backface"] == 0
+    assert b["light_evals_culled_plane"] == a["light_evals_culled_plane"] + a["light_evals_culled_backface"]
+    for k in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays"):
+        assert a[k] == b[k], k
+    with pytest.raises(mcpt.MCPTError, match="flags"):
+        mcpt.render_device(scene, cam, 8, fb.data_ptr(), seed=SEED, device=dev, flags=2)
+
+
 def test_progress_callback_and_cancel(scene):
     """mcpt_render_opts.progress (the reference's per-row progress, main.cpp:539-592): monotone
     reports ending at the call's total; a truthy return cancels with an error."""

@@ -48,8 +48,9 @@ def main():
     for line in open(a.log):
         if line.startswith("rank 0 totals:"):
             tot = json.loads(line.split(":", 1)[1])
-    # totals cover the timed steps; the profile also saw the warmup steps (same work per step)
-    nodes = tot["prep_full_nodes"] * (a.steps + a.warmup) / a.steps
+    # totals cover the timed steps; the profile also saw the warmup steps and bench.py's untimed
+    # replay of the timed steps (the cull statistic pass, MIS/shade) -- same work per step
+    nodes = tot["prep_full_nodes"] * (2 * a.steps + a.warmup) / a.steps
     kernels = [k for k in fetch if k.startswith("k_prep_cull_lanes") or k.startswith("k_prep_pk2")]
     fb = sum(2 * fetch[k] for k in kernels)
     wb = sum(write.get(k, 0.0) for k in kernels)
@@ -63,7 +64,8 @@ def main():
         "full_prep_nodes": int(nodes),
         "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 64-B tally of 128-B requests) and --pmc WRITE_SIZE in "
                   "separate passes over `bench.py --steps %d --warmup %d --no-cpu`; bytes of both kernels over all "
-                  "dispatches / full-prep nodes (timed-step count scaled to the profiled steps); tools/prep_hbm_bytes.py"
+                  "dispatches / full-prep nodes (timed-step count scaled to the profiled steps: warmup + timed + replay); "
+                  "tools/prep_hbm_bytes.py"
                   % (a.steps, a.warmup),
     }
     with open(a.out, "w") as f:
