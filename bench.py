@@ -8,9 +8,12 @@ rendered by one mcpt_render_device call (wavefront kernels, fp64 framebuffer res
 Each call computes everything it uses, including its root-point light-prep cache (DESIGN.md §4.4);
 nothing is carried from one step to the next except the framebuffer.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling by sample-range sharding -- rank r renders
-global samples [(k*G + r)*S, (k*G + r + 1)*S) in step k -- and ONE RCCL reduce of the framebuffer
-inside the timed region (monte_carlo_path_tracing_amd/shard.py).
+Multi-GPU (torchrun, one process per GPU): weak scaling by sample-range sharding.  Every rank joins
+the library's own RCCL communicator (mcpt_comm: rank 0's ncclUniqueId is broadcast over
+torch.distributed, then mcpt_comm_init_rank); step k is the job [k*G*S, (k+1)*G*S) of global sample
+indices, which the library splits into one S-sample shard per rank and ends with ONE ncclReduce(sum)
+of the fp64 framebuffers into rank 0 (include/mcpt.h, mcpt_render_opts.comm).  torch.distributed
+only provides the barrier and the max-over-ranks timing.
 
 Also reported: the roofline of the dominant kernel (k_prep: fp64 VALU-bound light prep), the
 CPU baseline (the C oracle on a bounded stratified pixel subset, rank 0, N=1 only) and the
@@ -121,11 +124,15 @@ def main():
     import torch.distributed as dist
 
     import monte_carlo_path_tracing_amd as mcpt
-    from monte_carlo_path_tracing_amd.shard import reduce_framebuffers
 
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # the library's RCCL communicator (one rank per process); a 1-rank communicator at N=1
+    uid = [mcpt.Comm.unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    comm = mcpt.Comm(world, rank, uid[0], device=local)
 
     def barrier():
         if world > 1:
@@ -143,25 +150,23 @@ def main():
     fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
     scratch = torch.zeros_like(fb)
 
-    for k in range(args.warmup):  # warmup renders go to a scratch buffer
-        mcpt.render_device(scene, cam, S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
-                           sample_range=(0, S), device=local)
+    flags = mcpt.RENDER_NO_BACKFACE_STATS
+    for k in range(args.warmup):  # warmup renders (same kernels and flags as the timed steps) go to scratch
+        mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
+                           sample_range=(0, world * S), comm=comm, flags=flags)
     totals = {}
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tlog = t0
-    for k in range(args.steps):
-        s0 = (k * world + rank) * S
+    for k in range(args.steps):  # the job of step k: [k*G*S, (k+1)*G*S), S samples per rank, 1 reduce
         st = mcpt.render_device(scene, cam, frame_spp, fb.data_ptr(), mode=args.mode, seed=args.seed,
-                                sample_range=(s0, s0 + S), device=local, flags=mcpt.RENDER_NO_BACKFACE_STATS)
+                                sample_range=(k * world * S, (k + 1) * world * S), comm=comm, flags=flags)
         for key, v in st.as_dict().items():
             totals[key] = totals.get(key, 0) + v
         if rank == 0 and time.perf_counter() - tlog > 30:
             tlog = time.perf_counter()
             log("step %d/%d, %.1f s" % (k + 1, args.steps, tlog - t0))
-    if world > 1:
-        reduce_framebuffers(fb, dist, dst=0)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -178,9 +183,8 @@ def main():
     if args.mode != "brdf":
         rep = {}
         for k in range(args.steps):
-            s0 = (k * world + rank) * S
             st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
-                                    sample_range=(s0, s0 + S), device=local)
+                                    sample_range=(k * world * S, (k + 1) * world * S), comm=comm)
             for key, v in st.as_dict().items():
                 rep[key] = rep.get(key, 0) + v
         for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes"):
@@ -238,7 +242,7 @@ def main():
         "config": {"workload": "%s %s %dx%d" % ("veach-mis" if args.scene == "veach" else "cornell-1M", args.mode.upper(), W, H),
                    "width": W, "height": H,
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
-                   "parallelism": "sample-shard x%d + 1 RCCL reduce" % world},
+                   "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "l2_vs_cpu": l2,

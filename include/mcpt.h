@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 10400 /* 1.4.0 */
+#define MCPT_VERSION 20000 /* 2.0.0: mcpt_render_opts carries struct_size (checked first), a device list
+                               * and a multi-process communicator; debug entry points moved to mcpt_debug.h */
 
 enum {
     MCPT_OK = 0,
@@ -31,7 +32,7 @@ enum {
     MCPT_E_IO = -2,       /* file not found / parse error */
     MCPT_E_SCENE = -3,    /* scene violates the reference's assumptions (e.g. facet without material) */
     MCPT_E_DEVICE = -4,   /* HIP error */
-    MCPT_E_OVERFLOW = -5, /* wavefront queue overflow (raise mcpt_render_opts.queue_factor) */
+    MCPT_E_OVERFLOW = -5, /* reserved (since 2.0 a generation larger than the queue is processed in slices) */
     MCPT_E_CANCELLED = -6, /* the progress callback asked to stop */
 };
 
@@ -76,27 +77,57 @@ typedef struct {
  * the framebuffer then holds a partial sum). */
 typedef int (*mcpt_progress_fn)(void* user, uint64_t samples_dispatched, uint64_t samples_total);
 
+/* Multi-process communicator (one process per GPU, e.g. torchrun): rank 0 creates an id with
+ * mcpt_comm_unique_id, the caller broadcasts its MCPT_COMM_ID_BYTES bytes (any channel), every rank
+ * calls mcpt_comm_init_rank (RCCL ncclCommInitRank on `device`; collective over all ranks).  The
+ * library owns the RCCL communicator. */
+typedef struct mcpt_comm mcpt_comm;
+#define MCPT_COMM_ID_BYTES 128
+
 typedef struct {
+    uint32_t struct_size;   /* sizeof(mcpt_render_opts) of the caller's header (mcpt_render_opts_init sets
+                             * it); checked before any other field -- a mismatch is MCPT_E_INVALID */
     int32_t spp;            /* samples per pixel of the whole frame (the 1/spp weight) */
     int32_t sample_begin;   /* render global sample indices [sample_begin, sample_end) */
-    int32_t sample_end;     /*   (sharding across GPUs/calls; 0,0 = all) */
+    int32_t sample_end;     /*   (0,0 = all); with devices / comm this is the JOB's range, split below */
     int32_t mode;           /* MCPT_MODE_MIS / MCPT_MODE_BRDF / MCPT_MODE_SHADE */
     uint64_t seed;          /* counter-RNG seed (reference default 20240430 in bench/tests) */
     int32_t samples_per_launch; /* wavefront working set: the node queue is refilled with camera samples
                                  * up to samples_per_launch x width x height nodes per generation
                                  * (0 = auto, 4 Mi nodes) */
-    int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2) */
-    int32_t device;         /* HIP device ordinal (-1 = current) */
+    int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2); a generation with
+                             * more nodes than the children buffer can take is processed in slices, the
+                             * rest parked on a spill stack in HBM (never an overflow error) */
+    int32_t device;         /* HIP device ordinal (-1 = current); ignored when num_devices > 0 */
     int32_t accel;          /* MCPT_ACCEL_BVH / MCPT_ACCEL_GRID (grid over the scene and this camera's
                              * eye with n0 = 100000, main.cpp:501-504; rebuilt when the eye changes) */
-    mcpt_progress_fn progress; /* optional (NULL = none) */
+    mcpt_progress_fn progress; /* optional (NULL = none); with several devices it is called from the
+                                * devices' worker threads, serialised by the library */
     void* progress_user;
     int32_t flags;          /* MCPT_RENDER_* bits (0 = defaults) */
+    /* One process, several GPUs: num_devices > 0 splits [sample_begin, sample_end)
+     * into num_devices contiguous, balanced shards, shard k rendered on devices[k] (a device may be
+     * listed more than once: its shards run one after another into that device's buffer), one host
+     * thread and stream per distinct device, no exchange while rendering; then ONE RCCL
+     * ncclReduce(sum) over the distinct devices (ncclCommInitAll, cached per scene handle) into the
+     * root devices[0].  mcpt_render: the result lands in out_rgb; mcpt_render_device: dev_out_rgb
+     * lives on devices[0].  The image equals the single-device render up to fp64 summation order. */
+    int32_t num_devices;
+    const int32_t* devices;
+    /* One process per GPU: this process renders rank's share of [sample_begin, sample_end) on the
+     * communicator's device and the call ends with ONE ncclReduce(sum, root rank 0): the whole job's
+     * sum is ADDED to rank 0's buffer; other ranks' buffers are left unchanged (their shard goes
+     * through a library buffer).  Every rank must make the same call.  Exclusive with devices. */
+    mcpt_comm* comm;
 } mcpt_render_opts;
-/* mcpt_render_opts.flags: skip the light-side cull statistic (mcpt_stats.light_evals_culled_backface
- * stays 0 and _culled_plane then holds both cheap-stage culls) -- one compare per (node, light) less
- * in the light cull; images and all other statistics are unchanged */
+/* mcpt_render_opts.flags: skip the light-side cull statistic in the hot loop of the split light cull;
+ * mcpt_stats.light_evals_culled_backface then reads 0 and _culled_plane holds both cheap-stage culls
+ * (every prep variant reports it that way).  Images and all other statistics are unchanged. */
 enum { MCPT_RENDER_NO_BACKFACE_STATS = 1 };
+
+/* zero-fills *opts and sets struct_size, device = -1, seed = 20240430, spp = 10 (main.cpp:567),
+ * mode = MCPT_MODE_MIS */
+void mcpt_render_opts_init(mcpt_render_opts* opts);
 
 typedef struct {
     double seconds;         /* device time of the render (HIP events) */
@@ -115,7 +146,12 @@ typedef struct {
     uint64_t prep_full_nodes;   /* prep nodes that ran the O(N_L) stages (incl. root-cache builds) */
     uint64_t prep_cached_nodes; /* root nodes served by the per-pixel root-point cache (pick only) */
     uint64_t prep_cache_points; /* root points whose prep built the cache (included in prep_full_nodes) */
+    uint64_t spilled_nodes; /* nodes parked on the spill stack (generations larger than the queue) */
+    double reduce_seconds;  /* the RCCL reduce of a multi-device / multi-rank call (0 otherwise) */
+    int32_t devices_used;   /* distinct devices (or 1 per rank) that rendered */
 } mcpt_stats;
+/* With several devices, `seconds` is the wall time of the whole call (shards + reduce), counts are
+ * summed over devices and prep_seconds is summed device time. */
 
 int mcpt_version(void);
 const char* mcpt_last_error(void);
@@ -136,11 +172,14 @@ int mcpt_scene_camera(const mcpt_scene* scene, mcpt_camera* cam);
 
 /* main.cpp:547-588: render samples [sample_begin, sample_end) of an spp-sample frame and ADD
  * sum_k L_k * (1/spp) into out_rgb (caller-owned host buffer, height*width*3 doubles, row 0 =
- * top image row).  Devices: opts->device. */
+ * top image row).  Devices: opts->device, or opts->devices / opts->comm (see mcpt_render_opts). */
 int mcpt_render(mcpt_scene* scene, const mcpt_camera* cam, const mcpt_render_opts* opts, double* out_rgb,
                 mcpt_stats* stats);
-/* same, accumulating into a DEVICE buffer (height*width*3 doubles on opts->device), without any
- * host round trip -- the form used with torch.distributed / RCCL reduce. */
+/* same, accumulating into a DEVICE buffer (height*width*3 doubles on opts->device, devices[0] or the
+ * comm's device), without any host round trip.  The buffer must be coarse-grained device memory
+ * (hipMalloc, or the torch caching allocator): the framebuffer is updated with hardware fp64
+ * atomics, which do not work on fine-grained / managed (hipMallocManaged, hipHostMalloc) memory --
+ * such buffers are rejected with MCPT_E_INVALID. */
 int mcpt_render_device(mcpt_scene* scene, const mcpt_camera* cam, const mcpt_render_opts* opts,
                        double* dev_out_rgb, mcpt_stats* stats);
 
@@ -163,15 +202,6 @@ int mcpt_closest_hit(mcpt_scene* scene, int32_t n, const double* ro, const doubl
  * -1 if empty or weights_sum < 1e-8). */
 int mcpt_light_prep(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                     double* weights_sum, int32_t* count, int32_t* pick);
-/* diagnostics: run the light-prep kernel variant `variant` `iters` times on the n points and report
- * the mean device time per launch; outputs as mcpt_light_prep (pick = facet).  Variants: -1 auto
- * (9 if N_L <= 64, else 17, else 0 when the candidate list does not fit in LDS); 0 k_prep (per-wave
- * LDS candidate queue, any N_L); 8 k_prep_pk2 (packed-fp32 cheap stages, stored LDS candidate list,
- * branch-free fp64 batches, lane-parallel batch search in one kernel); 9 k_prep_lane (lane per
- * node, small light sets); 17 k_prep_cull_lanes (lane per node, light table in scalar registers)
- * + k_prep_pk2's fp64 phase (the renderer's form).  Other values: MCPT_E_HIP (invalid value). */
-int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
-                          int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 /* primary-hit map of main.cpp:563-572 for a camera: facet (or -1), t, beta, gamma per pixel */
 int mcpt_primary_hits(mcpt_scene* scene, const mcpt_camera* cam, int32_t* facet, double* tbg);
 
@@ -180,6 +210,13 @@ int mcpt_primary_hits(mcpt_scene* scene, const mcpt_camera* cam, int32_t* facet,
 int mcpt_tone_map(const double* rgb, int32_t width, int32_t height, double max_radiance, double gamma,
                   uint8_t* out_rgb8);
 int mcpt_write_bmp(const char* path, const uint8_t* rgb8, int32_t width, int32_t height);
+
+/* Multi-process communicator (see mcpt_comm above): ncclGetUniqueId / ncclCommInitRank /
+ * ncclCommDestroy.  device -1 = the current device. */
+int mcpt_comm_unique_id(uint8_t id[MCPT_COMM_ID_BYTES]);
+int mcpt_comm_init_rank(int32_t nranks, int32_t rank, const uint8_t id[MCPT_COMM_ID_BYTES], int32_t device,
+                        mcpt_comm** out);
+void mcpt_comm_destroy(mcpt_comm* comm);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,30 @@
+/* mcpt_debug.h -- diagnostics and A/B switches of libmcpt_hip.so.  NOT part of the drop-in boundary
+ * (include/mcpt.h): kernel-variant timing and render switches used by tools/ for same-box A/B
+ * experiments.  No reference interface corresponds to these. */
+#ifndef MCPT_DEBUG_H
+#define MCPT_DEBUG_H
+#include "mcpt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* mcpt_render_opts.flags bits for A/B experiments (the library accepts them; images are unchanged):
+ * MCPT_DEBUG_SPLIT_BRDF runs BRDF-only renders as gen / rays / combine kernels instead of the fused
+ * k_extend_brdf; MCPT_DEBUG_NO_ROOT_CACHE disables the per-pixel root-point light-prep cache. */
+enum { MCPT_DEBUG_SPLIT_BRDF = 1 << 16, MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17 };
+
+/* diagnostics: run the light-prep kernel variant `variant` `iters` times on the n points and report
+ * the mean device time per launch; outputs like those of mcpt_light_prep, pick = facet.  Variants: -1 auto
+ * (9 if N_L <= 64, else 17, else 0 when the candidate list does not fit in LDS); 0 k_prep (per-wave
+ * LDS candidate queue, any N_L); 8 k_prep_pk2 (packed-fp32 cheap stages, stored LDS candidate list,
+ * branch-free fp64 batches, lane-parallel batch search in one kernel); 9 k_prep_lane (lane per
+ * node, small light sets); 17 k_prep_cull_lanes (lane per node, light table in scalar registers)
+ * + k_prep_pk2's fp64 phase (the renderer's form).  Other values: MCPT_E_DEVICE (invalid value). */
+int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
+                          int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

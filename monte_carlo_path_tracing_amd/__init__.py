@@ -15,7 +15,7 @@ import os
 
 import numpy as np
 
-__all__ = ["Scene", "Camera", "render", "render_device", "closest_hit", "light_prep", "primary_hits",
+__all__ = ["Scene", "Camera", "Comm", "render", "render_device", "closest_hit", "light_prep", "primary_hits",
            "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "MODE_SHADE", "ACCEL_BVH", "ACCEL_GRID", "Stats", "MCPTError", "LIB_PATH", "lib"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -24,7 +24,8 @@ MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2  # shade_with_mis / shade_with_brdf / 
 ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
 HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
 DEFAULT_SEED = 20240430
-MCPT_VERSION = 10400  # include/mcpt.h MCPT_VERSION this mirror is written against
+MCPT_VERSION = 20000  # include/mcpt.h MCPT_VERSION this mirror is written against
+COMM_ID_BYTES = 128  # MCPT_COMM_ID_BYTES
 
 
 class MCPTError(RuntimeError):
@@ -50,11 +51,14 @@ class Camera(C.Structure):
 
 
 class RenderOpts(C.Structure):
-    _fields_ = [("spp", C.c_int32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32), ("mode", C.c_int32),
+    _fields_ = [("struct_size", C.c_uint32), ("spp", C.c_int32), ("sample_begin", C.c_int32),
+                ("sample_end", C.c_int32), ("mode", C.c_int32),
                 ("seed", C.c_uint64), ("samples_per_launch", C.c_int32), ("queue_factor", C.c_int32),
                 ("device", C.c_int32), ("accel", C.c_int32), ("progress", C.c_void_p),
-                ("progress_user", C.c_void_p), ("flags", C.c_int32)]
+                ("progress_user", C.c_void_p), ("flags", C.c_int32), ("num_devices", C.c_int32),
+                ("devices", C.POINTER(C.c_int32)), ("comm", C.c_void_p)]
 RENDER_NO_BACKFACE_STATS = 1  # mcpt_render_opts.flags (include/mcpt.h)
+DEBUG_SPLIT_BRDF, DEBUG_NO_ROOT_CACHE = 1 << 16, 1 << 17  # include/mcpt_debug.h A/B switches
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_uint64)
@@ -66,7 +70,8 @@ class Stats(C.Structure):
                 ("generations", C.c_uint64), ("prep_seconds", C.c_double), ("prep_launches", C.c_uint64),
                 ("light_evals_total", C.c_uint64), ("light_evals_culled_backface", C.c_uint64),
                 ("light_evals_culled_plane", C.c_uint64), ("light_evals_candidates", C.c_uint64),
-                ("prep_full_nodes", C.c_uint64), ("prep_cached_nodes", C.c_uint64), ("prep_cache_points", C.c_uint64)]
+                ("prep_full_nodes", C.c_uint64), ("prep_cached_nodes", C.c_uint64), ("prep_cache_points", C.c_uint64),
+                ("spilled_nodes", C.c_uint64), ("reduce_seconds", C.c_double), ("devices_used", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -77,9 +82,10 @@ _lib = None
 # every symbol include/mcpt.h declares (tests check the .so exports them all)
 EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_create", "mcpt_scene_destroy",
            "mcpt_scene_counts", "mcpt_scene_arrays", "mcpt_scene_camera", "mcpt_scene_meshing", "mcpt_scene_grid_info",
-           "mcpt_render", "mcpt_render_device",
-           "mcpt_closest_hit", "mcpt_light_prep", "mcpt_debug_prep_bench", "mcpt_primary_hits", "mcpt_tone_map",
-           "mcpt_write_bmp"]
+           "mcpt_render_opts_init", "mcpt_render", "mcpt_render_device",
+           "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
+           "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
+DEBUG_EXPORTS = ["mcpt_debug_prep_bench"]  # include/mcpt_debug.h
 
 
 def lib():
@@ -114,6 +120,8 @@ def lib():
         L.mcpt_scene_camera.argtypes = [P, C.POINTER(Camera)]
         L.mcpt_scene_meshing.argtypes = [P, dp, I]
         L.mcpt_scene_grid_info.argtypes = [P, dp, ip]
+        L.mcpt_render_opts_init.argtypes = [C.POINTER(RenderOpts)]
+        L.mcpt_render_opts_init.restype = None
         L.mcpt_render.argtypes = [P, C.POINTER(Camera), C.POINTER(RenderOpts), dp, C.POINTER(Stats)]
         L.mcpt_render_device.argtypes = [P, C.POINTER(Camera), C.POINTER(RenderOpts), C.c_void_p, C.POINTER(Stats)]
         L.mcpt_closest_hit.argtypes = [P, I, dp, dp, ip, I, ip, dp]
@@ -122,6 +130,10 @@ def lib():
         L.mcpt_debug_prep_bench.argtypes = [P, I, dp, dp, dp, I, I, C.POINTER(C.c_double), dp, ip]
         L.mcpt_tone_map.argtypes = [dp, I, I, D, D, u8]
         L.mcpt_write_bmp.argtypes = [C.c_char_p, u8, I, I]
+        L.mcpt_comm_unique_id.argtypes = [C.c_char_p]
+        L.mcpt_comm_init_rank.argtypes = [I, I, C.c_char_p, I, C.POINTER(P)]
+        L.mcpt_comm_destroy.argtypes = [P]
+        L.mcpt_comm_destroy.restype = None
         _lib = L
     return _lib
 
@@ -184,11 +196,47 @@ class Scene:
         return c
 
 
+class Comm:
+    """mcpt_comm: this process's rank of a multi-process RCCL communicator owned by the library
+    (one process per GPU).  Rank 0 calls Comm.unique_id(); the caller broadcasts the bytes (e.g.
+    torch.distributed.broadcast_object_list); every rank then constructs Comm(nranks, rank, id, device).
+    Renders with comm=... render this rank's share of the job's sample range and end with ONE
+    ncclReduce(sum) into rank 0's buffer."""
+
+    def __init__(self, nranks, rank, uid, device=-1):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("comm id must be %d bytes" % COMM_ID_BYTES)
+        h = C.c_void_p()
+        _check(lib().mcpt_comm_init_rank(int(nranks), int(rank), bytes(uid), int(device), C.byref(h)))
+        self.h, self.nranks, self.rank = h, int(nranks), int(rank)
+
+    @staticmethod
+    def unique_id():
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        _check(lib().mcpt_comm_unique_id(buf))
+        return buf.raw
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mcpt_comm_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+
 def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress=None, accel="bvh",
-          flags=0):
-    """progress(done, total) -> truthy to cancel; the ctypes thunk is kept on the returned struct."""
+          flags=0, devices=None, comm=None):
+    """progress(done, total) -> truthy to cancel; the ctypes thunk is kept on the returned struct.
+    devices: list of device ordinals (one process, several GPUs); comm: a Comm (one process per GPU)."""
     o = RenderOpts()
+    lib().mcpt_render_opts_init(C.byref(o))
     o.flags = int(flags)
+    if devices is not None:
+        o._devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        o.num_devices = len(devices)
+        o.devices = C.cast(o._devs, C.POINTER(C.c_int32))
+    if comm is not None:
+        o.comm = comm.h
     a = {"bvh": ACCEL_BVH, "grid": ACCEL_GRID}.get(accel, -1) if isinstance(accel, str) else int(accel)
     if a not in (ACCEL_BVH, ACCEL_GRID):
         raise ValueError("accel must be 'bvh' or 'grid'")
@@ -197,6 +245,7 @@ def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_facto
         o._thunk = PROGRESS_FN(lambda _u, done, total: 1 if progress(int(done), int(total)) else 0)
         o.progress = C.cast(o._thunk, C.c_void_p)
     o.spp = int(spp)
+    o.sample_begin = o.sample_end = 0
     m = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE}.get(mode, -1) if isinstance(mode, str) else int(mode)
     if m not in (MODE_MIS, MODE_BRDF, MODE_SHADE):
         raise ValueError("mode must be 'mis', 'brdf' or 'shade'")
@@ -211,29 +260,34 @@ def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_facto
 
 
 def render(scene, camera, spp, mode="mis", seed=DEFAULT_SEED, sample_range=None, out=None, device=None,
-           samples_per_launch=0, queue_factor=0, progress=None, accel="bvh"):
+           samples_per_launch=0, queue_factor=0, progress=None, accel="bvh", devices=None, comm=None, flags=0):
     """render(scene, camera, spp, mode) -- main.cpp:547-588.  Returns (H x W x 3 fp64 radiance, Stats).
 
     Adds sum_k L_k / spp over samples k in `sample_range` (default all) into `out` (zeros if None).
     progress(samples_dispatched, samples_total), called after every wavefront generation, replaces
     the reference's per-row progress output; a truthy return cancels (MCPTError, partial sum).
     accel="grid" traces every ray through the reference's uniform grid (Myobj.cpp:78-162) instead of
-    the BVH: hit-for-hit the reference's traversal, crack included."""
+    the BVH: hit-for-hit the reference's traversal, crack included.
+    devices=[d0, d1, ...] shards the sample range over several GPUs of this process (one thread and
+    stream each; a device may repeat) and sums them with one RCCL reduce; comm=Comm(...) renders this
+    rank's share and reduces to rank 0 (see mcpt_render_opts in include/mcpt.h)."""
     if out is None:
         out = np.zeros((camera.height, camera.width, 3))
     assert out.dtype == np.float64 and out.flags.c_contiguous and out.shape == (camera.height, camera.width, 3)
     st = Stats()
-    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel)
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel, flags,
+              devices, comm)
     _check(lib().mcpt_render(scene.h, C.byref(camera), C.byref(o), out.reshape(-1), C.byref(st)))
     return out, st
 
 
 def render_device(scene, camera, spp, dev_ptr, mode="mis", seed=DEFAULT_SEED, sample_range=None, device=None,
-                  samples_per_launch=0, queue_factor=0, progress=None, accel="bvh", flags=0):
+                  samples_per_launch=0, queue_factor=0, progress=None, accel="bvh", flags=0, devices=None, comm=None):
     """Accumulate into a device buffer of H*W*3 doubles (e.g. a torch.float64 CUDA tensor's data_ptr()).
     flags: RENDER_NO_BACKFACE_STATS skips the light-side cull statistic (mcpt_render_opts.flags)."""
     st = Stats()
-    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel, flags)
+    o = _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress, accel, flags,
+              devices, comm)
     _check(lib().mcpt_render_device(scene.h, C.byref(camera), C.byref(o), C.c_void_p(int(dev_ptr)), C.byref(st)))
     return st
 

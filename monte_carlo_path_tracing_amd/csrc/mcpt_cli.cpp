@@ -6,7 +6,10 @@
 //
 //   mcpt_render --scene scenes/veach-mis/veach-mis [--width 1280 --height 720] [--spp 10]
 //               [--mode mis|brdf|shade] [--seed 20240430] [--out test.bmp] [--hdr out.pfm] [--progress]
-//               [--grid]
+//               [--grid] [--devices 0,1,2,3,4,5,6,7]
+//   --devices renders on several GPUs of this node: the sample range is split into one contiguous shard
+//   per listed device, rendered concurrently, and summed by ONE RCCL reduce into the first device
+//   (mcpt_render_opts.devices; the reference itself is single-threaded, README.md:418).
 //   --grid traverses the reference's uniform grid (Myobj.cpp:78-162, n0 = 100000) instead of the BVH.
 //   --progress prints the share of camera samples dispatched (the reference prints per-row progress
 //   and updates its EasyX window, main.cpp:539-592) through mcpt_render_opts.progress.
@@ -34,14 +37,18 @@ int print_progress(void* user, uint64_t done, uint64_t total) {
 
 // render(scene, camera, spp, mode): main.cpp:547-588 lifted into a function.
 int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, bool progress, bool grid,
-           std::vector<double>& hdr, mcpt_stats* st) {
+           const std::vector<int32_t>& devices, std::vector<double>& hdr, mcpt_stats* st) {
     hdr.assign(3ull * cam.width * cam.height, 0.0);
-    mcpt_render_opts o{};
+    mcpt_render_opts o;
+    mcpt_render_opts_init(&o);
     o.spp = spp;
     o.mode = mode;
     o.seed = seed;
-    o.device = -1;
     o.accel = grid ? MCPT_ACCEL_GRID : MCPT_ACCEL_BVH;
+    if (!devices.empty()) {  // one process, several GPUs: shards + one RCCL reduce
+        o.num_devices = (int32_t)devices.size();
+        o.devices = devices.data();
+    }
     int last = -10;
     if (progress) {
         o.progress = print_progress;
@@ -71,6 +78,7 @@ int main(int argc, char** argv) {
     double dist_scale = 2.0;
     uint64_t seed = 20240430;
     bool xml_cam = false, progress = false, grid = false;
+    std::vector<int32_t> devices;
     for (int a = 1; a < argc; a++) {
         auto next = [&]() -> const char* {
             if (a + 1 >= argc) {
@@ -100,6 +108,17 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[a], "--xml-camera")) xml_cam = true;
         else if (!std::strcmp(argv[a], "--progress")) progress = true;
         else if (!std::strcmp(argv[a], "--grid")) grid = true;
+        else if (!std::strcmp(argv[a], "--devices")) {
+            for (const char* p = next(); *p;) {
+                char* e = nullptr;
+                devices.push_back((int32_t)std::strtol(p, &e, 10));
+                if (e == p) {
+                    std::fprintf(stderr, "bad --devices list\n");
+                    return 2;
+                }
+                p = *e == ',' ? e + 1 : e;
+            }
+        }
         else {
             std::fprintf(stderr, "unknown option %s\n", argv[a]);
             return 2;
@@ -127,13 +146,14 @@ int main(int argc, char** argv) {
     std::vector<double> hdr;
     mcpt_stats st{};
     const auto t0 = std::chrono::steady_clock::now();
-    if (render(scene, cam, spp, mode, seed, progress, grid, hdr, &st) != MCPT_OK) {
+    if (render(scene, cam, spp, mode, seed, progress, grid, devices, hdr, &st) != MCPT_OK) {
         std::fprintf(stderr, "render failed: %s\n", mcpt_last_error());
         return 1;
     }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::printf("%dx%d @ %d spp (%s): %.3f s wall, %.3f s device, %.2f Msamples/s\n", W, H, spp,
-                mode == MCPT_MODE_MIS ? "MIS" : mode == MCPT_MODE_BRDF ? "BRDF" : "shade", sec, st.seconds, st.camera_samples / st.seconds * 1e-6);
+    std::printf("%dx%d @ %d spp (%s): %.3f s wall, %.3f s device, %.2f Msamples/s on %d device(s)\n", W, H, spp,
+                mode == MCPT_MODE_MIS ? "MIS" : mode == MCPT_MODE_BRDF ? "BRDF" : "shade", sec, st.seconds,
+                st.camera_samples / st.seconds * 1e-6, st.devices_used);
     std::vector<uint8_t> rgb8(hdr.size());
     mcpt_tone_map(hdr.data(), W, H, 380.0, 0.25, rgb8.data());  // main.cpp:583
     if (mcpt_write_bmp(out.c_str(), rgb8.data(), W, H) != MCPT_OK) {

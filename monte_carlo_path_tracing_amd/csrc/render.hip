@@ -26,17 +26,22 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
+#include "comm.h"
 #include "device_math.h"
 #include "mcpt.h"
+#include "mcpt_debug.h"
 #include "mcpt_internal.h"
 
 using namespace mcpt;
@@ -522,6 +527,26 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
         }
     }
     node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
+}
+
+// moves nodes [sb, sb + m) of src to [db, db + m) of dst (every field a generation carries into the
+// next: point, normal, wo, throughput, facet, pixel, sample, node id) -- the spill stack's push and
+// pop when a generation is larger than its children buffer can take (render_on_device)
+__global__ __launch_bounds__(256) void k_queue_move(Queue src, int sb, Queue dst, int db, int m) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const size_t s = (size_t)sb + k, d = (size_t)db + k;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        dst.p[3 * d + c] = src.p[3 * s + c];
+        dst.n[3 * d + c] = src.n[3 * s + c];
+        dst.wo[3 * d + c] = src.wo[3 * s + c];
+        dst.tp[3 * d + c] = src.tp[3 * s + c];
+    }
+    dst.f[d] = src.f[s];
+    dst.pixel[d] = src.pixel[s];
+    dst.sample[d] = src.sample[s];
+    dst.node[d] = src.node[s];
 }
 
 // root shading points of the pixels whose primary hit is a front-facing non-emitter (the nodes
@@ -1842,7 +1867,8 @@ struct DeviceState {
     std::vector<void*> allocs;
     hipStream_t stream = nullptr;
     // reusable work buffers
-    DevBuf hit_f, hit_tbg, fb, stats, work, qa[14], qb[14], aux[8], cache_bt, cache_lst, cache_info, cache_w, masks;
+    DevBuf hit_f, hit_tbg, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[8], cache_bt, cache_lst, cache_info, cache_w, masks;
+    int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
     unsigned* pinned_count = nullptr;
@@ -1857,6 +1883,8 @@ struct mcpt_scene {
     Grid grid;             // Myobj::cal_scene_boundingbox(eye) + meshing(n0) (mcpt_scene_meshing)
     int grid_version = 0;  // bumped by every rebuild; devices re-upload on mismatch
     std::vector<std::unique_ptr<DeviceState>> devs;
+    std::vector<int> comm_devices;  // distinct devices of the cached ncclCommInitAll communicators
+    std::vector<void*> comms;
     std::mutex mu;
 };
 
@@ -2202,7 +2230,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // extension kernels: MIS and shade split into gen / rays / combine (measured faster), BRDF-only
     // keeps the single kernel (one ray per node; measured faster).  A/B switches:
 #define K_MIS_RAYS (grid ? k_mis_rays<true> : k_mis_rays<false>)
-    static const bool split_brdf = getenv("MCPT_SPLIT_BRDF") != nullptr;
+    const bool split_brdf = (o->flags & MCPT_DEBUG_SPLIT_BRDF) != 0;
     const bool fused = !grid && o->mode == MCPT_MODE_BRDF && !split_brdf;  // BRDF-only: k_extend_brdf (the grid runs split)
     Aux aux{};
     if (!fused && (rc = alloc_aux(D.aux, cap, aux))) return rc;
@@ -2220,7 +2248,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
         return MCPT_E_SCENE;
     }
-    if (o->flags & ~MCPT_RENDER_NO_BACKFACE_STATS) {
+    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
@@ -2235,12 +2263,17 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         masks = (uint64_t*)D.masks.p;
     }
     // root-point cache (see PrepCache): built here when the call has >= 2 samples per pixel and the
-    // entries fit in a 64 GiB budget of HBM (800x600 with N_L = 3012: 15 GB)
+    // entries fit in the free HBM less a 16 GiB reserve (800x600 with N_L = 3012: 15 GB; 1600x1200:
+    // 60 GB -- sized for the 288 GB of an MI355X)
     PrepCache pc{};
     const int lstride = 64 * nchunks;
     const size_t cache_bytes = (size_t)npx * ((size_t)nchunks * 8 + (size_t)lstride * 10 + 16);
-    static const bool no_cache = getenv("MCPT_NO_ROOT_CACHE") != nullptr;  // A/B switch
-    if (o->mode != MCPT_MODE_BRDF && s1 - s0 >= 2 && cache_bytes <= (64ull << 30) && !no_cache && D.d.NL > kSmallNL &&
+    size_t free_b = 0, total_b = 0;
+    HIP_OK(hipMemGetInfo(&free_b, &total_b));
+    const size_t held = D.cache_bt.bytes + D.cache_lst.bytes + D.cache_info.bytes + D.cache_w.bytes;
+    const size_t budget = free_b + held > (16ull << 30) ? free_b + held - (16ull << 30) : 0;
+    const bool no_cache = (o->flags & MCPT_DEBUG_NO_ROOT_CACHE) != 0;  // A/B switch
+    if (o->mode != MCPT_MODE_BRDF && s1 - s0 >= 2 && cache_bytes <= budget && !no_cache && D.d.NL > kSmallNL &&
         prep_list_wave_bytes(nchunks) * 4 <= kPrepListMaxLds && D.d.NL <= 65535) {
         if ((rc = ensure(D.cache_bt, (size_t)npx * nchunks * 8)) || (rc = ensure(D.cache_lst, (size_t)npx * lstride * 2)) ||
             (rc = ensure(D.cache_info, (size_t)npx * 16)) || (rc = ensure(D.cache_w, (size_t)npx * lstride * 8)))
@@ -2287,6 +2320,43 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     Queue* nxt = &qb;
     HIP_OK(hipMemsetAsync(cur->count, 0, 4, st));
     long long rnext = 0;
+    // Slicing: an MIS node has up to 2 children (shade / BRDF: 1), so a generation of at most `slice`
+    // nodes always fits its children into nxt.  A larger generation (supercritical trees, e.g. occluded
+    // lights: 2 x RR 0.6 = 1.2 children per node) parks its excess on a spill stack in HBM (grown on
+    // demand) and takes it back, last in first out, before fresh roots -- so deep subtrees drain
+    // first and the stack stays bounded by ~depth x slice.  The image does not depend on the order.
+    const int branch = o->mode == MCPT_MODE_MIS ? 2 : 1;
+    const int slice = cap / branch;
+    const int fill = std::min(target, slice);  // refill / pop up to this many nodes per generation
+    Queue qs{};
+    long long spill_n = 0;
+    uint64_t spilled = 0;
+    auto grow_spill = [&](long long need) -> int {
+        if (need <= D.spill_cap && qs.p) return MCPT_OK;
+        if (need > (1ll << 30)) {
+            set_error("spill stack beyond 2^30 nodes");
+            return MCPT_E_DEVICE;
+        }
+        const int ncap = (int)std::min<long long>(std::max<long long>(need, 2ll * D.spill_cap), 1ll << 30);
+        DevBuf nb[14];
+        Queue nq;
+        int r;
+        if ((r = alloc_queue(nb, ncap, nq))) return r;
+        if (spill_n > 0 && qs.p)
+            hipLaunchKernelGGL(k_queue_move, dim3((unsigned)((spill_n + 255) / 256)), dim3(256), 0, st, qs, 0, nq, 0, (int)spill_n);
+        HIP_OK(hipStreamSynchronize(st));
+        for (int k = 0; k < 14; k++) {
+            if (D.qs[k].p) HIP_OK(hipFree(D.qs[k].p));
+            D.qs[k] = nb[k];
+        }
+        D.spill_cap = ncap;
+        qs = nq;
+        return MCPT_OK;
+    };
+    if (D.spill_cap > 0) {  // the stack of an earlier call (empty)
+        int r;
+        if ((r = alloc_queue(D.qs, D.spill_cap, qs))) return r;
+    }
     auto read_count = [&](unsigned* out) -> int {  // cur's node count; fails on a queue overflow
         HIP_OK(hipMemcpyAsync(D.pinned_count, cur->count, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipMemcpyAsync(D.pinned_count + 2, (char*)D.stats.p + 32, 8, hipMemcpyDeviceToHost, st));
@@ -2301,9 +2371,26 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     while (true) {
         unsigned n = 0;
         if ((rc = read_count(&n))) return rc;
+        if (n > (unsigned)slice) {  // push the excess children onto the spill stack
+            const int m = (int)n - slice;
+            if ((rc = grow_spill(spill_n + m))) return rc;
+            hipLaunchKernelGGL(k_queue_move, dim3((m + 255) / 256), dim3(256), 0, st, *cur, slice, qs, (int)spill_n, m);
+            HIP_OK(hipGetLastError());
+            spill_n += m;
+            spilled += (uint64_t)m;
+            n = (unsigned)slice;
+            HIP_OK(hipMemsetD32Async((hipDeviceptr_t)cur->count, (int)n, 1, st));
+        } else if (spill_n > 0 && n < (unsigned)fill) {  // pop spilled children before new roots
+            const int m = (int)std::min<long long>((long long)fill - n, spill_n);
+            spill_n -= m;
+            hipLaunchKernelGGL(k_queue_move, dim3((m + 255) / 256), dim3(256), 0, st, qs, (int)spill_n, *cur, (int)n, m);
+            HIP_OK(hipGetLastError());
+            n += (unsigned)m;
+            HIP_OK(hipMemsetD32Async((hipDeviceptr_t)cur->count, (int)n, 1, st));
+        }
         const unsigned n_children = n;  // [0, n_children) children, [n_children, n) fresh roots
-        if (rnext < R && n < (unsigned)target) {  // refill with roots (appended through node_entry)
-            const int m = (int)std::min<long long>((long long)target - n, R - rnext);
+        if (rnext < R && n < (unsigned)fill) {  // refill with roots (appended through node_entry)
+            const int m = (int)std::min<long long>((long long)fill - n, R - rnext);
             hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
                                (const double*)D.hit_tbg.p, s0, rnext, m, *cur);
             HIP_OK(hipGetLastError());
@@ -2311,7 +2398,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             if ((rc = read_count(&n))) return rc;
         }
         if (n == 0) {
-            if (rnext >= R) break;
+            if (rnext >= R && spill_n == 0) break;
             continue;  // every root of the refill terminated at entry: refill again
         }
         gens++;
@@ -2403,11 +2490,281 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->prep_cached_nodes = hs[0];
         stats->prep_cache_points = cache_points;
         stats->light_evals_total = full * (uint64_t)D.d.NL;
-        stats->light_evals_culled_backface = hs[6];
+        stats->light_evals_culled_backface = count_c1 ? hs[6] : 0;
         stats->light_evals_candidates = hs[5];
-        stats->light_evals_culled_plane = stats->light_evals_total - hs[5] - hs[6];
+        stats->light_evals_culled_plane = stats->light_evals_total - hs[5] - stats->light_evals_culled_backface;
+        stats->spilled_nodes = spilled;
+        stats->reduce_seconds = 0;
+        stats->devices_used = 1;
         stats->prep_seconds = prep_ms * 1e-3;
         stats->prep_launches = prep_launches;
+    }
+    return MCPT_OK;
+}
+
+int check_opts(const mcpt_render_opts* o) {
+    if (o->struct_size != sizeof(mcpt_render_opts)) {
+        set_error("mcpt_render_opts.struct_size is %u, this library expects %zu (use mcpt_render_opts_init / the "
+                  "mcpt.h of MCPT_VERSION %d)", o->struct_size, sizeof(mcpt_render_opts), MCPT_VERSION);
+        return MCPT_E_INVALID;
+    }
+    if (o->num_devices < 0 || (o->num_devices > 0 && !o->devices) || (o->num_devices > 0 && o->comm)) {
+        set_error("invalid device list (num_devices %d, devices %p, comm %p)", o->num_devices, (const void*)o->devices,
+                  (const void*)o->comm);
+        return MCPT_E_INVALID;
+    }
+    if (o->num_devices > 0) {
+        int nd = 0;
+        HIP_OK(hipGetDeviceCount(&nd));
+        for (int k = 0; k < o->num_devices; k++)
+            if (o->devices[k] < 0 || o->devices[k] >= nd) {
+                set_error("devices[%d] = %d: no such device (%d visible)", k, o->devices[k], nd);
+                return MCPT_E_INVALID;
+            }
+    }
+    return MCPT_OK;
+}
+
+// the caller's framebuffer must be device memory of `device` (fp64 hardware atomics are lost on
+// host / managed memory, and a host pointer the runtime does not know would fault the GPU)
+int check_device_buffer(const void* p, int device) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("dev_out_rgb is not coarse-grained device memory (unknown to the HIP runtime)");
+        return MCPT_E_INVALID;
+    }
+    if (a.type != hipMemoryTypeDevice || a.isManaged) {
+        set_error("dev_out_rgb is not coarse-grained device memory (memory type %d, managed %d)", (int)a.type, a.isManaged);
+        return MCPT_E_INVALID;
+    }
+    if (a.device != device) {
+        set_error("dev_out_rgb lives on device %d, the render's root device is %d", a.device, device);
+        return MCPT_E_INVALID;
+    }
+    return MCPT_OK;
+}
+
+// [s0, s1) of the whole job (0,0 = [0, spp))
+void job_range(const mcpt_render_opts* o, int* s0, int* s1) {
+    const bool all = o->sample_begin == 0 && o->sample_end == 0;
+    *s0 = all ? 0 : o->sample_begin;
+    *s1 = all ? o->spp : o->sample_end;
+}
+
+// shard k of n of [s0, s1): contiguous and balanced (sizes differ by at most one sample)
+void shard_range(int s0, int s1, int k, int n, int* a, int* b) {
+    const long long len = (long long)s1 - s0;
+    *a = s0 + (int)(len * k / n);
+    *b = s0 + (int)(len * (k + 1) / n);
+}
+
+void add_stats(mcpt_stats& t, const mcpt_stats& x) {
+    t.camera_samples += x.camera_samples;
+    t.shading_nodes += x.shading_nodes;
+    t.light_evals_survived += x.light_evals_survived;
+    t.rays += x.rays;
+    t.light_rays += x.light_rays;
+    t.generations += x.generations;
+    t.prep_seconds += x.prep_seconds;
+    t.prep_launches += x.prep_launches;
+    t.light_evals_total += x.light_evals_total;
+    t.light_evals_culled_backface += x.light_evals_culled_backface;
+    t.light_evals_culled_plane += x.light_evals_culled_plane;
+    t.light_evals_candidates += x.light_evals_candidates;
+    t.prep_full_nodes += x.prep_full_nodes;
+    t.prep_cached_nodes += x.prep_cached_nodes;
+    t.prep_cache_points += x.prep_cache_points;
+    t.spilled_nodes += x.spilled_nodes;
+}
+
+// progress of a multi-device call: the shards' dispatched counts are summed and the caller's callback
+// is invoked under a lock (it may be called from any device's worker thread); a cancel stops every
+// shard at its next generation
+struct MultiProgress {
+    const mcpt_render_opts* o;
+    uint64_t total = 0;
+    std::mutex mu;
+    std::vector<uint64_t> done;  // per shard
+    std::atomic<bool> cancel{false};
+};
+struct ShardProgress {
+    MultiProgress* m;
+    int shard;
+};
+int multi_progress_cb(void* user, uint64_t dispatched, uint64_t) {
+    ShardProgress* sp = static_cast<ShardProgress*>(user);
+    MultiProgress* m = sp->m;
+    if (m->cancel.load()) return 1;
+    if (!m->o->progress) return 0;
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->done[sp->shard] = dispatched;
+    uint64_t sum = 0;
+    for (uint64_t d : m->done) sum += d;
+    if (m->o->progress(m->o->progress_user, sum, m->total)) m->cancel.store(true);
+    return m->cancel.load() ? 1 : 0;
+}
+
+// One process, several devices (mcpt_render_opts.devices): shards of the sample range rendered
+// concurrently -- one host thread and stream per distinct device, shards on a repeated device run in
+// order into that device's buffer -- then ONE ncclReduce(sum) into the root devices[0].
+// root_out: the root's framebuffer (device memory on devices[0]); host_out (mcpt_render): when
+// non-null, root_out is the library's buffer, loaded from and stored back to host_out.
+int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* root_out,
+                 double* host_out, mcpt_stats* stats) {
+    const int nshards = o->num_devices;
+    std::vector<int> uniq;  // distinct devices in order of first appearance; uniq[0] = root
+    std::vector<int> shard_dev(nshards);
+    for (int k = 0; k < nshards; k++) {
+        const int d = o->devices[k];
+        auto it = std::find(uniq.begin(), uniq.end(), d);
+        shard_dev[k] = (int)(it - uniq.begin());
+        if (it == uniq.end()) uniq.push_back(d);
+    }
+    const int nu = (int)uniq.size();
+    const size_t nfb = 3ull * cam->width * cam->height;
+    std::vector<DeviceState*> Ds(nu);
+    std::vector<double*> fbs(nu);
+    int rc;
+    for (int u = 0; u < nu; u++) {  // device states are created on this thread (sc->devs is not thread-safe)
+        if ((rc = get_device_state(sc, uniq[u], &Ds[u]))) return rc;
+        HIP_OK(hipDeviceSynchronize());  // the caller's buffers may still be written by other streams
+        if (u == 0 && !host_out) {
+            fbs[0] = root_out;
+            continue;
+        }
+        if ((rc = ensure(Ds[u]->fb, nfb * sizeof(double)))) return rc;
+        fbs[u] = (double*)Ds[u]->fb.p;
+        if (u == 0)
+            HIP_OK(hipMemcpyAsync(fbs[0], host_out, nfb * sizeof(double), hipMemcpyHostToDevice, Ds[0]->stream));
+        else
+            HIP_OK(hipMemsetAsync(fbs[u], 0, nfb * sizeof(double), Ds[u]->stream));
+        HIP_OK(hipStreamSynchronize(Ds[u]->stream));
+    }
+    if (sc->comm_devices != uniq) {  // RCCL communicators over exactly these devices (cached)
+        comm_all_destroy(sc->comms);
+        sc->comm_devices.clear();
+        if ((rc = comm_all_init(uniq, sc->comms))) return rc;
+        sc->comm_devices = uniq;
+    }
+    int s0, s1;
+    job_range(o, &s0, &s1);
+    MultiProgress mp;
+    mp.o = o;
+    mp.total = (uint64_t)(s1 - s0) * cam->width * cam->height;
+    mp.done.assign(nshards, 0);
+    std::vector<ShardProgress> sp(nshards);
+    std::vector<mcpt_stats> sst(nshards);
+    std::vector<int> urc(nu, MCPT_OK);
+    std::vector<std::string> uerr(nu);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto worker = [&](int u) {
+        if (hipSetDevice(uniq[u]) != hipSuccess) {
+            urc[u] = MCPT_E_DEVICE;
+            uerr[u] = "hipSetDevice failed";
+            return;
+        }
+        for (int k = 0; k < nshards; k++) {
+            if (shard_dev[k] != u) continue;
+            int a, b;
+            shard_range(s0, s1, k, nshards, &a, &b);
+            if (a == b) continue;  // more shards than samples
+            mcpt_render_opts ok = *o;
+            ok.sample_begin = a;
+            ok.sample_end = b;
+            ok.num_devices = 0;
+            ok.devices = nullptr;
+            ok.device = uniq[u];
+            sp[k] = ShardProgress{&mp, k};
+            ok.progress = multi_progress_cb;
+            ok.progress_user = &sp[k];
+            const int r = render_on_device(sc, *Ds[u], cam, &ok, fbs[u], &sst[k]);
+            if (r) {
+                urc[u] = r;
+                uerr[u] = mcpt_last_error();
+                mp.cancel.store(true);
+                return;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int u = 1; u < nu; u++) th.emplace_back(worker, u);
+    worker(0);
+    for (auto& t : th) t.join();
+    for (int u = 0; u < nu; u++)
+        if (urc[u]) {
+            set_error("device %d: %s", uniq[u], uerr[u].c_str());
+            return urc[u];
+        }
+    const auto t1 = std::chrono::steady_clock::now();
+    std::vector<hipStream_t> streams(nu);
+    for (int u = 0; u < nu; u++) streams[u] = Ds[u]->stream;
+    if ((rc = comm_all_reduce_sum(sc->comms, uniq, fbs, streams, nfb))) return rc;
+    for (int u = 0; u < nu; u++) {
+        HIP_OK(hipSetDevice(uniq[u]));
+        HIP_OK(hipStreamSynchronize(Ds[u]->stream));
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    HIP_OK(hipSetDevice(uniq[0]));
+    if (host_out) {
+        HIP_OK(hipMemcpyAsync(host_out, fbs[0], nfb * sizeof(double), hipMemcpyDeviceToHost, Ds[0]->stream));
+        HIP_OK(hipStreamSynchronize(Ds[0]->stream));
+    }
+    if (stats) {
+        mcpt_stats t{};
+        for (int k = 0; k < nshards; k++) add_stats(t, sst[k]);
+        t.seconds = std::chrono::duration<double>(t2 - t0).count();
+        t.reduce_seconds = std::chrono::duration<double>(t2 - t1).count();
+        t.devices_used = nu;
+        *stats = t;
+    }
+    return MCPT_OK;
+}
+
+// One process per device (mcpt_render_opts.comm): this rank's shard of the job's sample range, then
+// ncclReduce(sum) to rank 0.  Rank 0 accumulates straight into its buffer `out` (the reduce is in
+// place there); other ranks render into a zeroed library buffer, so that only this call's samples
+// are summed and their `out` is left unchanged.
+int render_rank(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o, double* out,
+                mcpt_stats* stats) {
+    int nranks, rank, device;
+    int rc;
+    if ((rc = comm_rank_info(o->comm, &nranks, &rank, &device))) return rc;
+    double* fb = out;
+    if (rank != 0) {
+        const size_t bytes = 3ull * cam->width * cam->height * sizeof(double);
+        if ((rc = ensure(D.rank_fb, bytes))) return rc;
+        fb = (double*)D.rank_fb.p;
+        HIP_OK(hipMemsetAsync(fb, 0, bytes, D.stream));
+    }
+    int s0, s1, a, b;
+    job_range(o, &s0, &s1);
+    shard_range(s0, s1, rank, nranks, &a, &b);
+    mcpt_stats st{};
+    if (a < b) {
+        mcpt_render_opts ok = *o;
+        ok.sample_begin = a;
+        ok.sample_end = b;
+        ok.comm = nullptr;
+        ok.device = device;
+        if ((rc = render_on_device(sc, D, cam, &ok, fb, &st))) return rc;
+    } else {  // an empty shard still validates its options and joins the reduce
+        if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp) {
+            set_error("invalid render options (spp %d, range [%d,%d))", o->spp, s0, s1);
+            return MCPT_E_INVALID;
+        }
+    }
+    HIP_OK(hipEventRecord(D.ev0, D.stream));
+    if ((rc = comm_rank_reduce_sum(o->comm, fb, 3ull * cam->width * cam->height, D.stream))) return rc;
+    HIP_OK(hipEventRecord(D.ev1, D.stream));
+    HIP_OK(hipEventSynchronize(D.ev1));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, D.ev0, D.ev1));
+    if (stats) {
+        *stats = st;
+        stats->seconds += ms * 1e-3;
+        stats->reduce_seconds = ms * 1e-3;
+        stats->devices_used = 1;
     }
     return MCPT_OK;
 }
@@ -2495,16 +2852,16 @@ int mcpt_scene_create(const mcpt_scene_desc* d, mcpt_scene** out) {
 
 void mcpt_scene_destroy(mcpt_scene* sc) {
     if (!sc) return;
+    comm_all_destroy(sc->comms);
     for (auto& D : sc->devs) {
         (void)hipSetDevice(D->device);
         for (void* p : D->allocs) (void)hipFree(p);
-        DevBuf* bufs[] = {&D->hit_f, &D->hit_tbg, &D->fb, &D->stats, &D->work};
+        std::vector<DevBuf*> bufs = {&D->hit_f, &D->hit_tbg, &D->fb, &D->rank_fb, &D->stats, &D->work, &D->cache_bt, &D->cache_lst,
+                                     &D->cache_info, &D->cache_w, &D->masks, &D->g_start, &D->g_tri};
+        for (int k = 0; k < 14; k++) bufs.insert(bufs.end(), {&D->qa[k], &D->qb[k], &D->qs[k]});
+        for (int k = 0; k < 8; k++) bufs.push_back(&D->aux[k]);
         for (DevBuf* b : bufs)
             if (b->p) (void)hipFree(b->p);
-        for (int k = 0; k < 14; k++) {
-            if (D->qa[k].p) (void)hipFree(D->qa[k].p);
-            if (D->qb[k].p) (void)hipFree(D->qb[k].p);
-        }
         if (D->pinned_count) (void)hipHostFree(D->pinned_count);
         if (D->stream) (void)hipStreamDestroy(D->stream);
         hipEvent_t evs[] = {D->ev0, D->ev1, D->evp0, D->evp1};
@@ -2546,19 +2903,40 @@ int mcpt_scene_camera(const mcpt_scene* sc, mcpt_camera* cam) {
     return MCPT_OK;
 }
 
+void mcpt_render_opts_init(mcpt_render_opts* o) {
+    if (!o) return;
+    std::memset((void*)o, 0, sizeof *o);
+    o->struct_size = sizeof *o;
+    o->spp = 10;  // main.cpp:567
+    o->mode = MCPT_MODE_MIS;
+    o->seed = 20240430;
+    o->device = -1;
+}
+
 int mcpt_render_device(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* dev_out,
                        mcpt_stats* stats) {
     if (!sc || !o || !dev_out) {
         set_error("null argument");
         return MCPT_E_INVALID;
     }
-    int rc = validate_camera(cam);
-    if (rc) return rc;
+    int rc;
+    if ((rc = check_opts(o)) || (rc = validate_camera(cam))) return rc;
     std::lock_guard<std::mutex> lk(sc->mu);
+    if (o->num_devices > 0) {
+        if ((rc = check_device_buffer(dev_out, o->devices[0]))) return rc;
+        return render_multi(sc, cam, o, dev_out, nullptr, stats);
+    }
+    int device = o->device;
+    if (o->comm) {
+        int nr, r;
+        if ((rc = comm_rank_info(o->comm, &nr, &r, &device))) return rc;
+    }
     DeviceState* D;
-    if ((rc = get_device_state(sc, o->device, &D))) return rc;
+    if ((rc = get_device_state(sc, device, &D))) return rc;
+    if ((rc = check_device_buffer(dev_out, D->device))) return rc;
     // the caller's buffer may still be written by work on other streams (e.g. torch's)
     HIP_OK(hipDeviceSynchronize());
+    if (o->comm) return render_rank(sc, *D, cam, o, dev_out, stats);
     return render_on_device(sc, *D, cam, o, dev_out, stats);
 }
 
@@ -2568,15 +2946,28 @@ int mcpt_render(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* 
         set_error("null argument");
         return MCPT_E_INVALID;
     }
-    int rc = validate_camera(cam);
-    if (rc) return rc;
+    int rc;
+    if ((rc = check_opts(o)) || (rc = validate_camera(cam))) return rc;
     std::lock_guard<std::mutex> lk(sc->mu);
+    if (o->num_devices > 0) return render_multi(sc, cam, o, nullptr, out_rgb, stats);
+    int device = o->device;
+    if (o->comm) {
+        int nr, r;
+        if ((rc = comm_rank_info(o->comm, &nr, &r, &device))) return rc;
+    }
     DeviceState* D;
-    if ((rc = get_device_state(sc, o->device, &D))) return rc;
+    if ((rc = get_device_state(sc, device, &D))) return rc;
     const size_t n = 3ull * cam->width * cam->height;
     if ((rc = ensure(D->fb, n * sizeof(double)))) return rc;
     HIP_OK(hipMemcpyAsync(D->fb.p, out_rgb, n * sizeof(double), hipMemcpyHostToDevice, D->stream));
-    if ((rc = render_on_device(sc, *D, cam, o, (double*)D->fb.p, stats))) return rc;
+    if (o->comm)
+        rc = render_rank(sc, *D, cam, o, (double*)D->fb.p, stats);
+    else
+        rc = render_on_device(sc, *D, cam, o, (double*)D->fb.p, stats);
+    if (rc) return rc;
+    int nr = 1, rank = 0, dv;
+    if (o->comm && (rc = comm_rank_info(o->comm, &nr, &rank, &dv))) return rc;
+    if (rank != 0) return MCPT_OK;  // the job total lands on rank 0; this rank's out_rgb is unchanged
     HIP_OK(hipMemcpyAsync(out_rgb, D->fb.p, n * sizeof(double), hipMemcpyDeviceToHost, D->stream));
     HIP_OK(hipStreamSynchronize(D->stream));
     return MCPT_OK;

@@ -68,3 +68,33 @@ def dense_sphere(outdir, nseg=120, nring=60):
     obj.sphere("bulb", "bulb", (-0.8, 1.6, 0.0), 0.5, nseg, nring)
     mtls.append(("bulb", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0))
     return _write(outdir, "bulb", obj, mtls, [("bulb", (20.0, 18.0, 15.0))], CAM)
+
+
+def occluded_room(outdir):
+    """A closed room (inward faces of six wall slabs) with a down-facing ceiling lamp and an up-facing
+    floor lamp, each hidden behind a close, wider cap: a light sample from almost any point hits a
+    cap, and the cap's outer side faces the OTHER lamp, so an MIS node has two non-emitter children
+    with probability ~0.6 each -- a supercritical tree (~1.2 children per node, main.cpp:455-491)
+    whose generations outgrow any fixed wavefront queue."""
+    obj, mtls = gv.Obj(), []
+    X, Y, Z, T = 2.0, 3.0, 2.0, 0.1  # room half extents (y from 0 to Y), wall thickness
+    ex, ey, ez = (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0)
+    walls = [((0.0, -T, 0.0), [(ex, X + T), (ey, T), (ez, Z + T)]),
+             ((0.0, Y + T, 0.0), [(ex, X + T), (ey, T), (ez, Z + T)]),
+             ((-X - T, Y / 2, 0.0), [(ex, T), (ey, Y / 2), (ez, Z + T)]),
+             ((X + T, Y / 2, 0.0), [(ex, T), (ey, Y / 2), (ez, Z + T)]),
+             ((0.0, Y / 2, -Z - T), [(ex, X), (ey, Y / 2), (ez, T)]),
+             ((0.0, Y / 2, Z + T), [(ex, X), (ey, Y / 2), (ez, T)])]
+    for k, (c, axes) in enumerate(walls):
+        obj.box("wall%d" % k, "wall", c, axes)
+    faces = []
+    for x0, y, ny in ((-0.8, Y - 0.05, -1.0), (0.8, 0.05, 1.0)):  # lamp quads: 0.4 x 0.4
+        n = obj.normal((0.0, ny, 0.0))
+        q = [obj.vert((x0 + sx * 0.2, y, sz * 0.2)) for sx, sz in ((-1, -1), (1, -1), (1, 1), (-1, 1))]
+        tri = [(q[0], q[2], q[1]), (q[0], q[3], q[2])] if ny < 0 else [(q[0], q[1], q[2]), (q[0], q[2], q[3])]
+        tri = [t if ny > 0 else t for t in tri]
+        faces += [tuple((v, n) for v in t) for t in tri]
+        obj.box("cap%d" % len(faces), "wall", (x0, y + 0.1 * ny, 0.0), [(ex, 0.35), (ey, 0.01), (ez, 0.35)])
+    obj.groups.append(("lamp", "lamp", faces))
+    mtls += [("wall", (0.7, 0.7, 0.7), (0.0, 0.0, 0.0), 1.0), ("lamp", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0)]
+    return _write(outdir, "room", obj, mtls, [("lamp", (5.0, 5.0, 5.0))], ((0.0, 1.5, 1.8), (0.0, 0.4, 0.0)))

@@ -102,3 +102,38 @@ def test_camera_missing_everything():
     for mode in ("mis", "shade", "brdf"):
         img, st = mcpt.render(s, cam, 4, mode=mode, seed=SEED)
         assert not img.any() and st.shading_nodes == 0
+
+
+def test_occluded_room_is_supercritical(tmp_path):
+    """the oracle's own node count shows the room grows trees of ~1.2 children per node (CPU)"""
+    obj, xml = scenegen.occluded_room(str(tmp_path))
+    o = po.Scene(obj, xml)
+    c = o.camera()
+    c.width, c.height = 4, 3
+    e, _ = po.camera_ray(c, 0, 0)
+    o.build_grid(e)
+    _, ost = o.render(c, po.MODE_MIS, SEED, 1, nthreads=8)
+    assert ost[1] > 100 * 12  # prep nodes per camera sample, far above a subcritical tree's ~2
+
+
+@pytest.mark.gpu
+def test_supercritical_tree_spills_and_matches_oracle(tmp_path):
+    """Binary recursion main.cpp:455-491 with occluded lights: each generation outgrows the queue
+    (queue_factor 1, one camera sample per pixel per refill), so the excess is parked on the spill
+    stack and drained later; the frame must equal the default-queue render and the oracle, with
+    exactly the oracle's number of shading nodes (no node lost or duplicated)."""
+    obj, xml = scenegen.occluded_room(str(tmp_path))
+    s = mcpt.Scene.load(obj, xml)
+    g = s.camera()
+    g.width, g.height = 8, 6
+    img, st = mcpt.render(s, g, 2, mode="mis", seed=SEED, samples_per_launch=1, queue_factor=1)
+    big, st2 = mcpt.render(s, g, 2, mode="mis", seed=SEED)
+    o = po.Scene(obj, xml)
+    c = o.camera()
+    c.width, c.height = 8, 6
+    e, _ = po.camera_ray(c, 0, 0)
+    o.build_grid(e)
+    ref, ost = o.render(c, po.MODE_MIS, SEED, 2, nthreads=8)
+    assert st.spilled_nodes > 0
+    assert st.shading_nodes == st2.shading_nodes == int(ost[1])
+    assert ref.sum() > 0 and rel_l2(img, big) <= 1e-12 and rel_l2(img, ref) <= L2_TOL, (rel_l2(img, big), rel_l2(img, ref))

@@ -1,0 +1,168 @@
+"""Multi-GPU paths of the C ABI on the HIP kernels (the reference loop that shards
+is main.cpp:557-588, single-threaded in the reference, README.md:418).
+
+The box these run on has ONE MI355X, so the device-list path is exercised with the device repeated:
+devices=[0, 0] runs two sample-range shards (each a full wavefront render) into device 0's buffer
+and then the library's RCCL ncclReduce over its ncclCommInitAll communicator (one distinct device
+-> a 1-rank communicator); the multi-process path runs a 1-rank mcpt_comm, and two processes on
+cuda:0 render their shards through the HIP path and sum host copies over gloo.  Every form must
+equal the single-call frame to 1e-12 (fp64 summation order is the only difference, as the RNG is
+keyed by the global sample index), and the C4-shaped frame (1600x1200) must match the CPU oracle on
+its stride-20 pixel subset.
+
+Tolerances: frame relative L2 <= 1e-12 between HIP renders; <= 1e-3 (north star) vs the oracle,
+with the max per-pixel relative error reported and bounded the same way.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, SCENE_OBJ, SCENE_XML
+import monte_carlo_path_tracing_amd as mcpt
+from oracle import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+SEED = 20240430
+
+
+def rel_l2(g, c):
+    return float(np.linalg.norm(g - c) / max(np.linalg.norm(c), 1e-300))
+
+
+def max_px_rel(g, c):
+    """max over pixels of ||g_px - c_px|| / ||c_px|| (pixels black in both count 0)"""
+    d = np.linalg.norm((g - c).reshape(-1, 3), axis=1)
+    n = np.linalg.norm(c.reshape(-1, 3), axis=1)
+    return float(np.max(np.where(n > 0, d / np.maximum(n, 1e-300), np.where(d > 0, np.inf, 0.0))))
+
+
+@pytest.fixture(scope="module")
+def scene():
+    return mcpt.Scene.load(SCENE_OBJ, SCENE_XML)
+
+
+@pytest.fixture(scope="module")
+def single(scene):
+    cam = mcpt.Camera.reference(80, 60)
+    img, st = mcpt.render(scene, cam, 8, mode="mis", seed=SEED, device=0)
+    return img, st
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_device_list_equals_single_call(scene, single, devices):
+    cam = mcpt.Camera.reference(80, 60)
+    img, st = mcpt.render(scene, cam, 8, mode="mis", seed=SEED, devices=devices)
+    ref, st1 = single
+    assert rel_l2(img, ref) <= 1e-12
+    assert st.camera_samples == st1.camera_samples == 80 * 60 * 8
+    assert st.devices_used == 1 and st.reduce_seconds > 0
+    # the same shading nodes: each shard builds its own root-point cache (prep_cache_points per call)
+    nodes = lambda t: t.prep_full_nodes - t.prep_cache_points + t.prep_cached_nodes  # noqa: E731
+    assert nodes(st) == nodes(st1) and st.shading_nodes == st1.shading_nodes
+
+
+def test_device_list_into_device_buffer(scene, single):
+    import torch
+    cam = mcpt.Camera.reference(80, 60)
+    fb = torch.zeros((60, 80, 3), dtype=torch.float64, device="cuda:0")
+    st = mcpt.render_device(scene, cam, 8, fb.data_ptr(), mode="mis", seed=SEED, devices=[0, 0])
+    torch.cuda.synchronize()
+    assert rel_l2(fb.cpu().numpy(), single[0]) <= 1e-12 and st.devices_used == 1
+
+
+def test_device_list_job_range_and_empty_shards(scene):
+    """the device list splits the JOB's [sample_begin, sample_end); more shards than samples leaves
+    some empty"""
+    cam = mcpt.Camera.reference(40, 30)
+    a, _ = mcpt.render(scene, cam, 8, seed=SEED, sample_range=(3, 5), device=0)
+    b, st = mcpt.render(scene, cam, 8, seed=SEED, sample_range=(3, 5), devices=[0, 0, 0, 0])
+    assert rel_l2(b, a) <= 1e-12 and st.camera_samples == 40 * 30 * 2
+
+
+def test_comm_single_rank_equals_single_call(scene, single):
+    uid = mcpt.Comm.unique_id()
+    comm = mcpt.Comm(1, 0, uid, device=0)
+    try:
+        cam = mcpt.Camera.reference(80, 60)
+        img, st = mcpt.render(scene, cam, 8, mode="mis", seed=SEED, comm=comm)
+        assert rel_l2(img, single[0]) <= 1e-12
+        assert st.reduce_seconds > 0 and st.camera_samples == 80 * 60 * 8
+    finally:
+        comm.close()
+
+
+def test_device_list_rejects_bad_devices(scene):
+    cam = mcpt.Camera.reference(8, 6)
+    with pytest.raises(mcpt.MCPTError, match="no such device"):
+        mcpt.render(scene, cam, 2, devices=[0, 4096])
+
+
+def test_device_buffer_must_be_device_memory(scene):
+    import ctypes as C
+    cam = mcpt.Camera.reference(8, 6)
+    host = np.zeros((6, 8, 3))
+    with pytest.raises(mcpt.MCPTError, match="coarse-grained device memory"):
+        mcpt.render_device(scene, cam, 2, host.ctypes.data_as(C.c_void_p).value, device=0)
+
+
+_WORKER = r"""
+import os, sys
+sys.path.insert(0, os.environ["MCPT_ROOT"])
+import numpy as np
+import torch
+import torch.distributed as dist
+import monte_carlo_path_tracing_amd as mcpt
+from monte_carlo_path_tracing_amd.shard import sample_range
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%s" % os.environ["PORT"],
+                        rank=int(os.environ["RANK"]), world_size=2)
+rank = dist.get_rank()
+scene = mcpt.Scene.load(os.environ["OBJ"], os.environ["XML"])
+cam = mcpt.Camera.reference(80, 60)
+img, st = mcpt.render(scene, cam, 8, seed=20240430, sample_range=sample_range(rank, 2, 8), device=0)
+t = torch.from_numpy(img)
+dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+if rank == 0:
+    np.save(os.environ["OUT"], t.numpy())
+dist.destroy_process_group()
+"""
+
+
+def test_two_processes_render_hip_shards(tmp_path, single):
+    """world size 2 on the one GPU: two processes each run the HIP path on their sample shard of the
+    frame (main.cpp:557-588 split by sample), gloo sums the host copies"""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = tmp_path / "worker.py"
+    script.write_text(_WORKER)
+    out = tmp_path / "sum.npy"
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MCPT_ROOT=str(ROOT), PORT=str(port), RANK=str(r), OBJ=SCENE_OBJ, XML=SCENE_XML,
+                   OUT=str(out))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env))
+    for p in procs:
+        assert p.wait(timeout=110) == 0
+    assert rel_l2(np.load(out), single[0]) <= 1e-12
+
+
+def test_c4_frame_1600x1200_vs_oracle_subset(scene):
+    """config C4's frame size (1600x1200, the root-point cache at 60 GB) on the device-list path,
+    against the CPU oracle on every 20th pixel in x and y at the same seed and samples"""
+    W, H, spp = 1600, 1200, 4
+    cam = mcpt.Camera.reference(W, H)
+    img, st = mcpt.render(scene, cam, spp, mode="mis", seed=SEED, devices=[0, 0])
+    assert st.prep_cache_points > 0  # the root-point cache fits and was built
+    osc = po.Scene(SCENE_OBJ, SCENE_XML)
+    ocam = po.reference_camera(W, H)
+    e, _ = po.camera_ray(ocam, 0, 0)
+    osc.build_grid(e)
+    ref, _ = osc.render(ocam, po.MODE_MIS, SEED, spp, stride=20, offset=7, nthreads=16)
+    g, c = img[7::20, 7::20], ref[7::20, 7::20]
+    l2, mx = rel_l2(g, c), max_px_rel(g, c)
+    print("C4 1600x1200x%d MIS subset: rel L2 %.3e, max per-pixel %.3e" % (spp, l2, mx))
+    assert l2 <= 1e-3 and mx <= 1e-3

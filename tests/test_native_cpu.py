@@ -19,6 +19,52 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, name), name
     assert L.mcpt_version() == mcpt.MCPT_VERSION
     assert int(re.search(r"#define MCPT_VERSION (\d+)", hdr).group(1)) == mcpt.MCPT_VERSION
+    dbg = (ROOT / "include" / "mcpt_debug.h").read_text()
+    assert set(re.findall(r"\b(mcpt_[a-z_0-9]+)\s*\(", dbg)) == set(mcpt.DEBUG_EXPORTS)
+    for name in mcpt.DEBUG_EXPORTS:
+        assert hasattr(L, name), name
+
+
+def test_abi_struct_layouts_match_header(tmp_path):
+    """sizeof/offsetof of mcpt_render_opts, mcpt_stats and mcpt_camera from a C program compiled
+    against include/mcpt.h equal the ctypes mirror's; mcpt_render_opts_init sets struct_size."""
+    import ctypes as C
+    import subprocess
+    structs = {"mcpt_render_opts": mcpt.RenderOpts, "mcpt_stats": mcpt.Stats, "mcpt_camera": mcpt.Camera}
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "mcpt.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        src.append('printf("%s sizeof %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f, _ in py._fields_:
+            src.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (cname, f, cname, f))
+    src.append("return 0; }")
+    (tmp_path / "layout.c").write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", str(ROOT / "include"), str(tmp_path / "layout.c"), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        c, f, v = line.split()
+        got[(c, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+    o = mcpt.RenderOpts()
+    mcpt.lib().mcpt_render_opts_init(C.byref(o))
+    assert o.struct_size == C.sizeof(mcpt.RenderOpts) and o.device == -1 and o.spp == 10
+
+
+def test_render_rejects_a_foreign_struct_size():
+    """ABI guard (include/mcpt.h struct_size): a caller built against another header is refused
+    before any other field is read -- no GPU involved."""
+    import ctypes as C
+    s = mcpt.Scene.load(SCENE_OBJ, SCENE_XML)
+    cam = mcpt.Camera.reference(8, 6)
+    o = mcpt.RenderOpts()
+    mcpt.lib().mcpt_render_opts_init(C.byref(o))
+    o.struct_size -= 8
+    out = np.zeros((6, 8, 3))
+    rc = mcpt.lib().mcpt_render(s.h, C.byref(cam), C.byref(o), out.reshape(-1), None)
+    assert rc == -1 and b"struct_size" in mcpt.lib().mcpt_last_error()
 
 
 @pytest.fixture(scope="module")
