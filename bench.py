@@ -41,6 +41,19 @@ FLOPS_FULL = 269
 # algorithmic HBM bytes of one prep node: reads p, N (48 B) + pixel, sample, node id (16 B) for the
 # RNG key; writes weights_sum + pick (12 B).  The light table (240 KB) is L2/MALL resident.
 PREP_BYTES_PER_NODE = 76
+# traversal: a BVH node visit tests its children's slabs in fp32 -- 12 flops per
+# child box, 4 children per 4-wide node -- and every ray/triangle test is the reference's fp64 Cramer
+# rule (Myobj.cpp:165-192, 74 flops).  VALU model in fp32-equivalent flops (an fp64 op issues at
+# half the fp32 rate on MI355X: 78.6 vs 157.3 TFLOP/s).  Memory model: every node visit fetches its
+# 128-B node and every test its 48-B triangle, from the cache level that holds the structure --
+# the peak is MI355X_MICROARCH.md's measured chip-wide random-row gather rate of that level: L2
+# (an XCD's 4 MiB, 16.8-18.8 TB/s), Infinity Cache (256 MB, 8.6 TB/s), else HBM.
+FP32_VECTOR_PEAK_TFLOPS = 157.3
+GATHER_PEAKS = [(4 << 20, "l2", 17800.0), (256 << 20, "infinity_cache", 8600.0), (1 << 62, "hbm", HBM_PEAK_GBS)]
+FLOPS_NODE_VISIT = 48
+FLOPS_TRI_TEST_FP64 = 74
+BYTES_NODE_VISIT = 128
+BYTES_TRI_TEST = 48
 SCENE = os.path.join(ROOT, "scenes", "veach-mis")
 SCENES = {  # --scene: (metric, data note)
     "veach": (METRIC, "synthetic: Veach-MIS stand-in scene (scenes/gen_veach_mis.py; the reference's scene files are missing)"),
@@ -68,6 +81,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def load_json(path):
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def rel_l2(g, c):
+    return float(np.linalg.norm(g - c) / max(np.linalg.norm(c), 1e-300))
+
+
+def max_px_rel(g, c):
+    """max over pixels of ||g_px - c_px|| / ||c_px|| (pixels black in both count 0)"""
+    d = np.linalg.norm((g - c).reshape(-1, 3), axis=1)
+    n = np.linalg.norm(c.reshape(-1, 3), axis=1)
+    return float(np.max(np.where(n > 0, d / np.maximum(n, 1e-300), np.where(d > 0, np.inf, 0.0))))
+
+
 def cpu_baseline(scene_name, W, H, mode, seed, target_s):
     """The C oracle (oracle/liboracle.so), 1 thread, every 20th pixel in x and y, at an spp chosen
     so that the run takes about target_s seconds.  Returns (dict, subset image, spp)."""
@@ -82,7 +113,7 @@ def cpu_baseline(scene_name, W, H, mode, seed, target_s):
         ocam = po.reference_camera(W, H)
     e, _ = po.camera_ray(ocam, 0, 0)
     osc.build_grid(e)
-    m = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF, "shade": po.MODE_SHADE}[mode]
+    m = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF, "shade": po.MODE_SHADE, "shade_area": po.MODE_SHADE_AREA}[mode]
     t = time.perf_counter()
     osc.render(ocam, m, seed, 1, stride=20, offset=7, nthreads=1)
     t1 = time.perf_counter() - t
@@ -91,10 +122,25 @@ def cpu_baseline(scene_name, W, H, mode, seed, target_s):
     img, _ = osc.render(ocam, m, seed, spp, stride=20, offset=7, nthreads=1)
     dt = time.perf_counter() - t
     npx = len(range(7, H, 20)) * len(range(7, W, 20))
-    return ({"value": npx * spp / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-             "sample": "oracle/mcpt_oracle.c (fp64 C restatement incl. the reference's uniform grid), "
-                       "1 thread, every 20th pixel in x and y of %dx%d (%d px) x %d spp %s = %d camera samples "
-                       "in %.1f s" % (W, H, npx, spp, mode.upper(), npx * spp, dt)}, img, spp)
+    value = npx * spp / dt / 1e6
+    out = {"value": value, "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "sample": "oracle/mcpt_oracle.c (fp64 C restatement incl. the reference's uniform grid), "
+                     "1 thread, every 20th pixel in x and y of %dx%d (%d px) x %d spp %s = %d camera samples "
+                     "in %.1f s" % (W, H, npx, spp, mode.upper(), npx * spp, dt)}
+    # The reference itself cannot travel to the GPU box.  Its single-thread speed relative to this
+    # restatement was measured on identical frames in the build container (tools/time_reference_cpu.py):
+    # the restatement is faster (no std::map facet lookups), so the reference-equivalent baseline is
+    # value / ratio.
+    ref = load_json(os.path.join(ROOT, "profiles", "cpu_reference_vs_oracle.json"))
+    r = (ref or {}).get("modes", {}).get(mode) if scene_name == "veach" else None
+    if r:
+        out["oracle_over_reference"] = r["oracle_over_reference"]
+        out["reference_equivalent_value"] = value / r["oracle_over_reference"]
+        out["reference_equivalent_source"] = ("profiles/cpu_reference_vs_oracle.json: compiled reference %.0f vs oracle "
+                                              "%.0f samples/s, 1 core of '%s', %s" % (
+                                                  r["reference_samples_per_s"], r["oracle_samples_per_s"],
+                                                  ref.get("host", "?"), r["frame"]))
+    return out, img, spp
 
 
 def main():
@@ -108,7 +154,7 @@ def main():
     ap.add_argument("--spp-per-step", type=int, default=256)
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=600)
-    ap.add_argument("--mode", default="mis", choices=["mis", "brdf", "shade"])
+    ap.add_argument("--mode", default="mis", choices=["mis", "brdf", "shade", "shade_area"])
     ap.add_argument("--scene", default="veach", choices=sorted(SCENES),
                     help="veach: the north-star workload (C3); cornell1m: config C5")
     ap.add_argument("--seed", type=int, default=20240430)
@@ -176,62 +222,105 @@ def main():
         elapsed = float(t.item())
     samples = float(W * H) * frame_spp
     value = samples / elapsed / 1e6
-    # The timed steps skip the light-side cull statistic (mcpt_render_opts.flags; one compare per
-    # (node, light) in the hot loop).  The roofline's flop count needs it: replay the same steps
-    # (same seed and sample ranges, so the same nodes) untimed into the scratch buffer with the
-    # statistic on, and check that the work the two runs counted is identical.
-    if args.mode != "brdf":
-        rep = {}
-        for k in range(args.steps):
-            st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
-                                    sample_range=(k * world * S, (k + 1) * world * S), comm=comm)
-            for key, v in st.as_dict().items():
-                rep[key] = rep.get(key, 0) + v
-        for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes"):
-            assert rep.get(key) == totals.get(key), (key, rep.get(key), totals.get(key))
-        totals["light_evals_culled_backface"] = rep["light_evals_culled_backface"]
-        totals["light_evals_culled_plane"] = rep["light_evals_culled_plane"]
+    # Untimed statistics replay: the same steps (same seed and sample ranges, so the same nodes and
+    # rays) into the scratch buffer, with the light-side cull statistic on (the timed steps skip it,
+    # mcpt_render_opts.flags) and the traversal kernel's node-visit / triangle-test counters
+    # (MCPT_DEBUG_COUNT_TRAVERSAL); the work both runs counted must be identical.
+    rep = {}
+    for k in range(args.steps):
+        st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
+                                sample_range=(k * world * S, (k + 1) * world * S), comm=comm,
+                                flags=mcpt.DEBUG_COUNT_TRAVERSAL)
+        for key, v in st.as_dict().items():
+            rep[key] = rep.get(key, 0) + v
+    for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays",
+                "light_rays", "shading_nodes"):
+        assert rep.get(key) == totals.get(key), (key, rep.get(key), totals.get(key))
+    for key in ("light_evals_culled_backface", "light_evals_culled_plane", "node_visits", "tri_tests"):
+        totals[key] = rep[key]
 
     log("rank %d totals: %s" % (rank, json.dumps({k: v for k, v in totals.items()})))
     if rank != 0:
+        comm.close()
         dist.destroy_process_group()
         return
-    # ---- roofline of the dominant kernel (rank 0's launches; HIP events on its stream) ----
-    ev_tot, c1, c2, surv = (totals.get(k, 0) for k in ("light_evals_total", "light_evals_culled_backface",
-                                                         "light_evals_culled_plane", "light_evals_survived"))
-    launches = max(totals.get("prep_launches", 0), 1)
+    pmc = load_json(os.path.join(ROOT, "profiles", "pmc_latest.json")) or {"kernels": {}}
+    pk = pmc["kernels"]
+    busy = lambda *names: {n: pk[n]["valu_busy"] for n in names if n in pk}  # noqa: E731
+    dev_s = max(totals.get("seconds", 0.0), 1e-12)
+    # ---- roofline of the light prep (rank 0's launches; HIP events on its stream) ----
+    roof_prep = None
     prep_s = totals.get("prep_seconds", 0.0)
-    cand = totals.get("light_evals_candidates", 0)
-    c2 = ev_tot - c1 - cand
-    flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
     if args.mode != "brdf" and prep_s > 0:
-        achieved = flops / launches / (prep_s / launches) / 1e12
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "k_prep_hbm_bytes_per_node.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                per_node = json.load(f).get("hbm_bytes_per_node")
-            nodes = totals.get("prep_full_nodes", 0)
-            traffic = per_node * nodes / launches if per_node is not None else None
-        roofline = {"bound": "valu_fp64", "kernel": "k_prep", "achieved": round(achieved, 3),
-                    "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
-                    "traffic": traffic, "avg_launch_ms": round(prep_s / launches * 1e3, 3), "launches": launches,
-                    "flop_per_launch": flops / launches, "share_of_device_time": round(prep_s / max(totals["seconds"], 1e-12), 3),
-                    "hbm_algorithmic_GBs": round(totals.get("prep_full_nodes", 0) * PREP_BYTES_PER_NODE / prep_s / 1e9, 3),
-                    "full_prep_nodes": totals.get("prep_full_nodes", 0), "cached_root_nodes": totals.get("prep_cached_nodes", 0),
-                    "hbm_peak_GBs": HBM_PEAK_GBS}
-    else:
-        roofline = {"bound": "valu_fp64", "kernel": "k_extend_brdf", "achieved": None, "peak": FP64_VECTOR_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": None, "traffic": None}
+        ev_tot, c1, cand = (totals.get(k, 0) for k in ("light_evals_total", "light_evals_culled_backface",
+                                                       "light_evals_candidates"))
+        launches = max(totals.get("prep_launches", 0), 1)
+        c2 = ev_tot - c1 - cand
+        flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
+        t_launch = prep_s / launches
+        achieved = flops / launches / t_launch / 1e12
+        nodes = totals.get("prep_full_nodes", 0)
+        traffic, tsrc = None, None
+        hb = load_json(os.path.join(ROOT, "profiles", "k_prep_hbm_bytes_per_node.json"))
+        if hb and hb.get("hbm_bytes_per_node") is not None:
+            traffic = hb["hbm_bytes_per_node"] * nodes / launches
+            tsrc = ("PMC profile, not this run: %.1f HBM B/node (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                    "profiles/k_prep_hbm_bytes_per_node.json) x this run's %.0f full-prep nodes per launch"
+                    % (hb["hbm_bytes_per_node"], nodes / launches))
+        alg_gbs = nodes * PREP_BYTES_PER_NODE / prep_s / 1e9
+        roof_prep = {
+            "bound": "valu_fp64", "kernel": "k_prep_cull_lanes+k_prep_pk2", "achieved": round(achieved, 3),
+            "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
+            "traffic": traffic, "traffic_source": tsrc,
+            "valu_busy": busy("k_prep_cull_lanes<false>", "k_prep_pk2<5, false, true>"),
+            "valu_busy_source": pmc.get("source"),
+            "hbm_frac_algorithmic": round(alg_gbs / HBM_PEAK_GBS, 5),
+            "hbm_frac_measured": round(traffic / t_launch / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+            "avg_launch_ms": round(t_launch * 1e3, 3), "launches": launches, "flop_per_launch": flops / launches,
+            "share_of_device_time": round(prep_s / dev_s, 3), "hbm_algorithmic_GBs": round(alg_gbs, 3),
+            "full_prep_nodes": nodes, "cached_root_nodes": totals.get("prep_cached_nodes", 0),
+            "hbm_peak_GBs": HBM_PEAK_GBS}
+    # ---- roofline of the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf) ----
+    roof_trace = None
+    tr_s, tr_n = totals.get("trace_seconds", 0.0), max(totals.get("trace_launches", 0), 1)
+    visits, tests = totals.get("node_visits", 0), totals.get("tri_tests", 0)
+    if tr_s > 0 and visits > 0:
+        kname = "k_extend_brdf" if args.mode == "brdf" else "k_mis_rays"
+        t_launch = tr_s / tr_n
+        fl = (visits * FLOPS_NODE_VISIT + tests * FLOPS_TRI_TEST_FP64 * 2) / tr_n
+        by = (visits * BYTES_NODE_VISIT + tests * BYTES_TRI_TEST) / tr_n
+        accel = scene.accel_bytes()
+        _, level, mem_peak = next(g for g in GATHER_PEAKS if accel <= g[0])
+        v_frac, h_frac = fl / t_launch / 1e12 / FP32_VECTOR_PEAK_TFLOPS, by / t_launch / 1e9 / mem_peak
+        valu_bound = v_frac >= h_frac
+        pk_name = "k_extend_brdf" if args.mode == "brdf" else "k_mis_rays<false>"
+        hbm_meas = pk.get(pk_name, {}).get("hbm_bytes_per_dispatch")
+        roof_trace = {
+            "bound": "valu" if valu_bound else level, "kernel": kname,
+            "achieved": round(fl / t_launch / 1e12, 3) if valu_bound else round(by / t_launch / 1e9, 1),
+            "peak": FP32_VECTOR_PEAK_TFLOPS if valu_bound else mem_peak,
+            "unit": "TFLOP/s (fp32-equivalent: fp64 op = 2)" if valu_bound else "GB/s (node + triangle fetch model)",
+            "frac": round(max(v_frac, h_frac), 4), "valu_frac": round(v_frac, 4), "mem_model_frac": round(h_frac, 4),
+            "accel_bytes": accel, "hbm_model_frac": round(by / t_launch / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": hbm_meas, "traffic_source": ("PMC profile, not this run: %s" % pmc.get("source")) if hbm_meas else None,
+            "valu_busy": busy(pk_name), "valu_busy_source": pmc.get("source"),
+            "avg_launch_ms": round(t_launch * 1e3, 3), "launches": tr_n,
+            "node_visits_per_ray": round(visits / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),
+            "tri_tests_per_ray": round(tests / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),
+            "share_of_device_time": round(tr_s / dev_s, 3)}
+    # the line's roofline is the kernel with the larger share of device time
+    cands = [r for r in (roof_prep, roof_trace) if r]
+    roofline = max(cands, key=lambda r: r["share_of_device_time"]) if cands else None
 
     cpu = None
-    l2 = None
+    l2 = l2max = None
     if world == 1 and not args.no_cpu:
         log("cpu baseline (~%.0f s) ..." % args.cpu_seconds)
         cpu, cimg, cspp = cpu_baseline(args.scene, W, H, args.mode, args.seed, args.cpu_seconds)
         g, _ = mcpt.render(scene, cam, cspp, mode=args.mode, seed=args.seed, device=local)
         sub = (slice(7, None, 20), slice(7, None, 20))
-        l2 = float(np.linalg.norm(g[sub] - cimg[sub]) / max(np.linalg.norm(cimg[sub]), 1e-300))
+        l2 = rel_l2(g[sub], cimg[sub])
+        l2max = max_px_rel(g[sub], cimg[sub])
     if args.out:
         mcpt.write_bmp(args.out, mcpt.tone_map(fb.cpu().numpy()))
     line = {
@@ -244,12 +333,16 @@ def main():
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
                    "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world},
         "roofline": roofline,
+        "roofline_prep": roof_prep,
+        "roofline_trace": roof_trace,
         "cpu_baseline": cpu,
         "l2_vs_cpu": l2,
+        "l2_vs_cpu_max_pixel": l2max,
         "device_seconds": round(totals.get("seconds", 0.0), 4),
         "samples": samples,
     }
     print(json.dumps(line), flush=True)
+    comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -36,8 +36,11 @@ enum {
     MCPT_E_CANCELLED = -6, /* the progress callback asked to stop */
 };
 
-/* shade_with_mis main.cpp:402 / shade_with_brdf :348 / shade :269 (the one main() calls, :575) */
-enum { MCPT_MODE_MIS = 0, MCPT_MODE_BRDF = 1, MCPT_MODE_SHADE = 2 };
+/* shade_with_mis main.cpp:402 / shade_with_brdf :348 / shade :269 (the one main() calls, :575) with
+ * the spherical-triangle light sampler (main.cpp:297) / shade with the uniform-area light sampler
+ * select_a_point_from_lights (Mylight.cpp:102-160, the alternative commented out at main.cpp:296:
+ * a light by radiance, a triangle by area, a uniform point; no O(N_L) light prep) */
+enum { MCPT_MODE_MIS = 0, MCPT_MODE_BRDF = 1, MCPT_MODE_SHADE = 2, MCPT_MODE_SHADE_AREA = 3 };
 
 /* closest-hit acceleration: the BVH (default; the true closest hit) or the reference's own uniform
  * grid with its in-cell acceptance rule (Myobj.cpp:78-162, 334-622), crack included -- hit for hit
@@ -59,6 +62,9 @@ typedef struct {
     const float* materials;      /* nmaterials*7: Kd[3] Ks[3] Ns */
     const int32_t* light_facet;  /* nlights: facet of each light triangle */
     const double* light_radiance; /* nlights*3: radiance of its <light> material */
+    const int32_t* light_group;  /* optional, nlights: index of its <light> (ascending; the lights of
+                                  * select_a_point_from_lights, Mylight.cpp:102-160); NULL = each run of
+                                  * equal radiance is one light */
 } mcpt_scene_desc;
 
 /* Camera of main.cpp:507-510,547-564 generalised to width x height:
@@ -149,6 +155,10 @@ typedef struct {
     uint64_t spilled_nodes; /* nodes parked on the spill stack (generations larger than the queue) */
     double reduce_seconds;  /* the RCCL reduce of a multi-device / multi-rank call (0 otherwise) */
     int32_t devices_used;   /* distinct devices (or 1 per rank) that rendered */
+    double trace_seconds;   /* device time in the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf) */
+    uint64_t trace_launches;
+    uint64_t node_visits;   /* BVH node visits and ray/triangle tests of that kernel -- counted only when */
+    uint64_t tri_tests;     /* the render sets MCPT_DEBUG_COUNT_TRAVERSAL (mcpt_debug.h), else 0 */
 } mcpt_stats;
 /* With several devices, `seconds` is the wall time of the whole call (shards + reduce), counts are
  * summed over devices and prep_seconds is summed device time. */
@@ -163,6 +173,9 @@ int mcpt_scene_load(const char* obj_path, const char* xml_path, mcpt_scene** out
 int mcpt_scene_create(const mcpt_scene_desc* desc, mcpt_scene** out);
 void mcpt_scene_destroy(mcpt_scene* scene);
 int mcpt_scene_counts(const mcpt_scene* scene, int32_t* nfacets, int32_t* nmaterials, int32_t* nlights);
+/* device bytes of the acceleration structures the traversal reads (both BVHs' 4-wide nodes and leaf
+ * triangles; the reference's counterpart is its uniform grid, Myobj.cpp:110-162) */
+int mcpt_scene_accel_bytes(const mcpt_scene* scene, uint64_t* bytes);
 /* host copies of the loaded, flattened scene (any pointer may be NULL): the reference's data
  * after Myobj::read / gather_light_triangles, plus Myobj::get_unique_normal_of_facet (Myobj.cpp:680) */
 int mcpt_scene_arrays(const mcpt_scene* scene, float* positions, float* normals, int32_t* material_id,

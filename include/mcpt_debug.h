@@ -12,7 +12,10 @@ extern "C" {
 /* mcpt_render_opts.flags bits for A/B experiments (the library accepts them; images are unchanged):
  * MCPT_DEBUG_SPLIT_BRDF runs BRDF-only renders as gen / rays / combine kernels instead of the fused
  * k_extend_brdf; MCPT_DEBUG_NO_ROOT_CACHE disables the per-pixel root-point light-prep cache. */
-enum { MCPT_DEBUG_SPLIT_BRDF = 1 << 16, MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17 };
+enum { MCPT_DEBUG_SPLIT_BRDF = 1 << 16, MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17, MCPT_DEBUG_COUNT_TRAVERSAL = 1 << 18 };
+/* MCPT_DEBUG_COUNT_TRAVERSAL runs the traversal kernel's counting instance, which fills
+ * mcpt_stats.node_visits / tri_tests (the events of the traversal roofline; slower, for untimed
+ * replays). */
 
 /* diagnostics: run the light-prep kernel variant `variant` `iters` times on the n points and report
  * the mean device time per launch; outputs like those of mcpt_light_prep, pick = facet.  Variants: -1 auto

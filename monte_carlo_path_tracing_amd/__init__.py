@@ -16,11 +16,13 @@ import os
 import numpy as np
 
 __all__ = ["Scene", "Camera", "Comm", "render", "render_device", "closest_hit", "light_prep", "primary_hits",
-           "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "MODE_SHADE", "ACCEL_BVH", "ACCEL_GRID", "Stats", "MCPTError", "LIB_PATH", "lib"]
+           "tone_map", "write_bmp", "MODE_MIS", "MODE_BRDF", "MODE_SHADE", "MODE_SHADE_AREA", "ACCEL_BVH", "ACCEL_GRID", "Stats", "MCPTError", "LIB_PATH", "lib"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(HERE, "libmcpt_hip.so")  # override: A/B of two builds
 MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2  # shade_with_mis / shade_with_brdf / shade (main.cpp:402/348/269)
+MODE_SHADE_AREA = 3  # shade with select_a_point_from_lights (Mylight.cpp:102-160; main.cpp:296)
+MODES = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE, "shade_area": MODE_SHADE_AREA}
 ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
 HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
 DEFAULT_SEED = 20240430
@@ -58,7 +60,7 @@ class RenderOpts(C.Structure):
                 ("progress_user", C.c_void_p), ("flags", C.c_int32), ("num_devices", C.c_int32),
                 ("devices", C.POINTER(C.c_int32)), ("comm", C.c_void_p)]
 RENDER_NO_BACKFACE_STATS = 1  # mcpt_render_opts.flags (include/mcpt.h)
-DEBUG_SPLIT_BRDF, DEBUG_NO_ROOT_CACHE = 1 << 16, 1 << 17  # include/mcpt_debug.h A/B switches
+DEBUG_SPLIT_BRDF, DEBUG_NO_ROOT_CACHE, DEBUG_COUNT_TRAVERSAL = 1 << 16, 1 << 17, 1 << 18  # include/mcpt_debug.h
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_uint64)
@@ -71,7 +73,9 @@ class Stats(C.Structure):
                 ("light_evals_total", C.c_uint64), ("light_evals_culled_backface", C.c_uint64),
                 ("light_evals_culled_plane", C.c_uint64), ("light_evals_candidates", C.c_uint64),
                 ("prep_full_nodes", C.c_uint64), ("prep_cached_nodes", C.c_uint64), ("prep_cache_points", C.c_uint64),
-                ("spilled_nodes", C.c_uint64), ("reduce_seconds", C.c_double), ("devices_used", C.c_int32)]
+                ("spilled_nodes", C.c_uint64), ("reduce_seconds", C.c_double), ("devices_used", C.c_int32),
+                ("trace_seconds", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
+                ("tri_tests", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -81,7 +85,7 @@ _lib = None
 
 # every symbol include/mcpt.h declares (tests check the .so exports them all)
 EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_create", "mcpt_scene_destroy",
-           "mcpt_scene_counts", "mcpt_scene_arrays", "mcpt_scene_camera", "mcpt_scene_meshing", "mcpt_scene_grid_info",
+           "mcpt_scene_counts", "mcpt_scene_accel_bytes", "mcpt_scene_arrays", "mcpt_scene_camera", "mcpt_scene_meshing", "mcpt_scene_grid_info",
            "mcpt_render_opts_init", "mcpt_render", "mcpt_render_device",
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
@@ -116,6 +120,7 @@ def lib():
         L.mcpt_scene_destroy.argtypes = [P]
         L.mcpt_scene_destroy.restype = None
         L.mcpt_scene_counts.argtypes = [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]
+        L.mcpt_scene_accel_bytes.argtypes = [P, C.POINTER(C.c_uint64)]
         L.mcpt_scene_arrays.argtypes = [P, fp, fp, ip, fp, ip, dp, dp]
         L.mcpt_scene_camera.argtypes = [P, C.POINTER(Camera)]
         L.mcpt_scene_meshing.argtypes = [P, dp, I]
@@ -190,6 +195,12 @@ class Scene:
         _check(lib().mcpt_scene_grid_info(self.h, box, cells))
         return box, cells
 
+    def accel_bytes(self):
+        """device bytes of the BVHs the traversal reads (mcpt_scene_accel_bytes)"""
+        b = C.c_uint64()
+        _check(lib().mcpt_scene_accel_bytes(self.h, C.byref(b)))
+        return b.value
+
     def camera(self):
         c = Camera()
         _check(lib().mcpt_scene_camera(self.h, C.byref(c)))
@@ -246,9 +257,9 @@ def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_facto
         o.progress = C.cast(o._thunk, C.c_void_p)
     o.spp = int(spp)
     o.sample_begin = o.sample_end = 0
-    m = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE}.get(mode, -1) if isinstance(mode, str) else int(mode)
-    if m not in (MODE_MIS, MODE_BRDF, MODE_SHADE):
-        raise ValueError("mode must be 'mis', 'brdf' or 'shade'")
+    m = MODES.get(mode, -1) if isinstance(mode, str) else int(mode)
+    if m not in MODES.values():
+        raise ValueError("mode must be one of %s" % sorted(MODES))
     o.mode = m
     o.seed = int(seed)
     if sample_range is not None:

@@ -5,7 +5,7 @@
 // integrator and output path are flags instead of edits to main.cpp.
 //
 //   mcpt_render --scene scenes/veach-mis/veach-mis [--width 1280 --height 720] [--spp 10]
-//               [--mode mis|brdf|shade] [--seed 20240430] [--out test.bmp] [--hdr out.pfm] [--progress]
+//               [--mode mis|brdf|shade|shade-area] [--seed 20240430] [--out test.bmp] [--hdr out.pfm] [--progress]
 //               [--grid] [--devices 0,1,2,3,4,5,6,7]
 //   --devices renders on several GPUs of this node: the sample range is split into one contiguous shard
 //   per listed device, rendered concurrently, and summed by ONE RCCL reduce into the first device
@@ -96,8 +96,9 @@ int main(int argc, char** argv) {
             if (!std::strcmp(m, "mis")) mode = MCPT_MODE_MIS;
             else if (!std::strcmp(m, "brdf")) mode = MCPT_MODE_BRDF;
             else if (!std::strcmp(m, "shade")) mode = MCPT_MODE_SHADE;
+            else if (!std::strcmp(m, "shade-area")) mode = MCPT_MODE_SHADE_AREA;
             else {
-                std::fprintf(stderr, "unknown --mode %s (mis, brdf, shade)\n", m);
+                std::fprintf(stderr, "unknown --mode %s (mis, brdf, shade, shade-area)\n", m);
                 return 2;
             }
         }
@@ -152,7 +153,8 @@ int main(int argc, char** argv) {
     }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::printf("%dx%d @ %d spp (%s): %.3f s wall, %.3f s device, %.2f Msamples/s on %d device(s)\n", W, H, spp,
-                mode == MCPT_MODE_MIS ? "MIS" : mode == MCPT_MODE_BRDF ? "BRDF" : "shade", sec, st.seconds,
+                mode == MCPT_MODE_MIS ? "MIS" : mode == MCPT_MODE_BRDF ? "BRDF" : mode == MCPT_MODE_SHADE ? "shade" : "shade-area",
+                sec, st.seconds,
                 st.camera_samples / st.seconds * 1e-6, st.devices_used);
     std::vector<uint8_t> rgb8(hdr.size());
     mcpt_tone_map(hdr.data(), W, H, 380.0, 0.25, rgb8.data());  // main.cpp:583

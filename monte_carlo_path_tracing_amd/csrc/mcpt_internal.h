@@ -22,6 +22,11 @@ struct HostScene {
     std::vector<double> light_sum;      // NL  RadianceRGB::sum()
     std::vector<int32_t> light_of;      // F -> light index or -1
     std::vector<double> unique_n;       // F*3  Myobj::get_unique_normal_of_facet
+    std::vector<double> light_area;     // NL   lightTriangle::area (Mylight.cpp:66-69)
+    // Mylight::lightsRadiance in map order (every XML light, also one without triangles):
+    // RadianceRGB::sum() and the run [start, start + count) of its triangles in the light table
+    std::vector<double> group_rsum;
+    std::vector<int32_t> group_start, group_count;
     bool has_cam = false;
     mcpt_camera cam{};
 };
@@ -35,6 +40,7 @@ struct LightDef {
 bool load_light_xml(const std::string& xml_path, HostScene& s, std::vector<LightDef>& lights, std::string& err);
 // gather_light_triangles + unique normals (Mylight.cpp:32-100, Myobj.cpp:680-709)
 bool finalize_scene(HostScene& s, std::vector<LightDef> lights, std::string& err);
+double light_triangle_area(const HostScene& s, int f);  // Mylight.cpp:66-69
 
 // bvh.cpp -- binary BVH over a facet subset, flattened for the GPU.
 struct BvhNode {       // 64 B: both children's boxes in one node (one fetch per visit)

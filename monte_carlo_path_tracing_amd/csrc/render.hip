@@ -81,6 +81,15 @@ struct DScene {
     const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves)
     const BvhNode4* lbvh4;
     const float4* lleaf_v;
+    // select_a_point_from_lights (MCPT_MODE_SHADE_AREA): the lightsRadiance map in name order --
+    // RadianceRGB::sum() per light and its running sum, the light-table run of its triangles -- and
+    // the triangles' areas (Mylight.cpp:66-69) with their running sum within their light
+    int ngroups;
+    const double* grp_sum;
+    const double* grp_cum;
+    const int2* grp_range;    // (first light-table index, count)
+    const double* l_area;
+    const double* l_area_cum;
     // reference uniform grid (MCPT_ACCEL_GRID; null until mcpt_scene_meshing / a grid render)
     const int* g_start;       // CSR cell -> facets
     const int* g_tri;
@@ -154,9 +163,12 @@ struct Hit {
 //    nonzero quotient has the sign of its operands; the divisions of the surviving candidates are
 //    exactly tri_hit's, so accepted hits are bit-identical); origin facet excluded, t > 1e-8, ties
 //    to the lower facet id.
-template <int kLds>
+// kCount: also count node visits and triangle tests into *visits / *tests (the traversal roofline's
+// events; only the untimed statistics replay instantiates it)
+template <int kLds, bool kCount = false>
 __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
-                                int exclude, int* __restrict__ lds, int stride) {
+                                int exclude, int* __restrict__ lds, int stride, unsigned* visits = nullptr,
+                                unsigned* tests = nullptr) {
     constexpr int kDone = 0x7fffffff;
     Hit best{-1, DBL_MAX, 0, 0};
     if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
@@ -184,6 +196,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     int leaf = 0;
     while (node != kDone || leaf < 0) {
         while (node >= 0 && node != kDone) {
+            if (kCount) ++*visits;
             const BvhNode4* nd = nodes + node;
             const float4 lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
                          lz = *reinterpret_cast<const float4*>(nd->lo[2]);
@@ -231,6 +244,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                 const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
                 const int fac = __float_as_int(a4.w);
                 if (fac == exclude) continue;
+                if (kCount) ++*tests;
                 const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
                 const double detA = det3(ab, ac, rd);
                 if (fabs(detA) < MCPT_EPS) continue;
@@ -451,7 +465,7 @@ __device__ inline void node_entry(const Params& P, bool active, int f, double be
                     unsafeAtomicAdd(px + 0, tp.x * S.light_rad[3 * li + 0] * P.inv_spp);
                     unsafeAtomicAdd(px + 1, tp.y * S.light_rad[3 * li + 1] * P.inv_spp);
                     unsafeAtomicAdd(px + 2, tp.z * S.light_rad[3 * li + 2] * P.inv_spp);
-                } else if (P.mode == MCPT_MODE_SHADE) {
+                } else if (P.mode == MCPT_MODE_SHADE || P.mode == MCPT_MODE_SHADE_AREA) {
                     push = true;  // shade() samples direct light before its RR draw (main.cpp:295-327)
                 } else {
                     const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
@@ -585,6 +599,14 @@ __device__ inline unsigned long long wave_sum_u64(unsigned long long v) {
 __device__ inline int wave_sum_int(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
+}
+// adds a and b summed over the wave to ca / cb, one atomic each (every lane of the wave must call)
+__device__ inline void wave_count2(unsigned long long* ca, unsigned a, unsigned long long* cb, unsigned b) {
+    const unsigned long long sa = wave_sum_u64(a), sb = wave_sum_u64(b);
+    if (__lane_id() == 0) {
+        if (sa) atomicAdd(ca, sa);
+        if (sb) atomicAdd(cb, sb);
+    }
 }
 __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                    const double* __restrict__ qn, const int* __restrict__ qpixel,
@@ -1596,15 +1618,18 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 
 // closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
 // queue's shading points, excluding the origin facet
-template <bool kGrid>
-__global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set) {
+// kCount: counts node visits / triangle tests into cnt[0] / cnt[1] (statistics replay only)
+template <bool kGrid, bool kCount = false>
+__global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set,
+                                                          unsigned long long* cnt = nullptr) {
     __shared__ int stack[kRayLds * kRayBlock];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int set = blockIdx.y + first_set;
-    if (i >= n) return;
-    const int fl = A.flags[i];
+    if (!kCount && i >= n) return;
+    const int fl = i < n ? A.flags[i] : 0;
     int f = -1;
     double beta = 0, gamma = 0;
+    unsigned visits = 0, tests = 0;
     if (fl & (1 << set)) {
         const double* d = set == 0 ? A.d1 : A.d2;
         const d3 ro = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
@@ -1614,10 +1639,15 @@ __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, 
         if (kGrid)
             h = grid_trace(S, ro, rd, cur.f[i], set == 2);
         else
-            h = trace4_ww<kRayLds>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i], stack + threadIdx.x, kRayBlock);
+            h = trace4_ww<kRayLds, kCount>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i], stack + threadIdx.x,
+                                           kRayBlock, &visits, &tests);
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
+    }
+    if (kCount) {
+        wave_count2(cnt, visits, cnt + 1, tests);
+        if (i >= n) return;
     }
     const size_t o = (size_t)set * A.cap + i;
     A.hf[o] = f;
@@ -1667,6 +1697,56 @@ __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n,
 // in w1) and, after RR, the bounce (d2, the child's throughput in w2); combine splats L_dir if the
 // shadow ray's first hit is the sampled light facet (main.cpp:306-315) and spawns the bounce child
 // if it hits a non-emitter (main.cpp:335).
+// first index of the running sums cum[0..n) that is >= target (n - 1 if none): the counter-RNG
+// inverse CDF, equal to the oracle's linear scan (the same running sums)
+__device__ inline int cdf_search(const double* cum, int n, double target) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cum[mid] >= target) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+// Mylight::select_a_point_from_lights (Mylight.cpp:102-160) with the counter RNG: a light of the
+// lightsRadiance map by RadianceRGB::sum() (dim 1), one of its triangles by area (dim 7), a uniform
+// point beta = 1 - sqrt(1 - ksi1), gamma = (1 - beta) ksi2 (dims 2, 3); proba = p(light) p(triangle) /
+// area, an area-measure pdf.  Fewer than two choices: index 0, probability 1 (libstdc++'s
+// discrete_distribution).  Returns the light-table index, or -1 if the light has no triangles (the
+// reference throws std::out_of_range, Mylight.cpp:128).  The oracle's area_light_sample, op for op.
+__device__ inline int area_light_sample(const DScene& S, uint64_t key, d3* coord, double* prob) {
+    const int G = S.ngroups;
+    if (G == 0) return -1;
+    int k = 0;
+    double p1 = 1.0;
+    if (G >= 2) {
+        const double tot = S.grp_cum[G - 1];
+        k = cdf_search(S.grp_cum, G, counter_u(key, 1) * tot);
+        p1 = S.grp_sum[k] / tot;
+    }
+    const int2 r = S.grp_range[k];
+    if (r.y == 0) return -1;
+    int jj = 0;
+    double p2 = 1.0;
+    if (r.y >= 2) {
+        const double tot = S.l_area_cum[r.x + r.y - 1];
+        jj = cdf_search(S.l_area_cum + r.x, r.y, counter_u(key, 7) * tot);
+        p2 = S.l_area[r.x + jj] / tot;
+    }
+    const int j = r.x + jj;
+    const double ksi1 = counter_u(key, 2), ksi2 = counter_u(key, 3);
+    const double beta = 1 - sqrt(1 - ksi1);
+    const double gamma = (1 - beta) * ksi2;
+    const double alpha = 1 - beta - gamma;
+    *coord = add(add(mul(f3(S.lt_v[3 * j]), alpha), mul(f3(S.lt_v[3 * j + 1]), beta)), mul(f3(S.lt_v[3 * j + 2]), gamma));
+    double proba = 1.0;
+    proba *= p1;
+    proba *= p2;
+    proba *= 1.0 / S.l_area[j];
+    *prob = proba;
+    return j;
+}
+
 __global__ __launch_bounds__(256) void k_shade_gen(Params P, Queue cur, int n, Aux A) {
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1680,12 +1760,20 @@ __global__ __launch_bounds__(256) void k_shade_gen(Params P, Queue cur, int n, A
     const float* m = S.mtl + 7 * S.tri_mat[f];
     const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
     const double sh = m[6];
-    const int pick = cur.pick[i];
+    int pick = -1;
     int flags = 0;
     // ---- direct light (main.cpp:295-316) ----
     d3 coord, n1 = N, w1 = mk3(0, 0, 0);
     double lprob = 1;
-    if (pick >= 0) {
+    if (P.mode == MCPT_MODE_SHADE_AREA) {  // main.cpp:296: select_a_point_from_lights
+        pick = area_light_sample(S, key, &coord, &lprob);
+        if (pick >= 0) {
+            const double4 ln = S.lt_n[pick];
+            n1 = mk3(ln.x, ln.y, ln.z);
+        } else {
+            coord = add(mul(N, -1), p);
+        }
+    } else if ((pick = cur.pick[i]) >= 0) {
         const double4 ln = S.lt_n[pick];
         SphTri sph;
         light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), 2.0 * ln.w, p, N, &sph);
@@ -1787,6 +1875,7 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
 }
 
 // one BRDF-only path vertex (main.cpp:385-396)
+template <bool kCount = false>
 __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
     __shared__ int stack[kRayLds * kTraceBlock];
     const DScene& S = P.S;
@@ -1800,7 +1889,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
     const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
     const uint64_t node = cur.node[ii];
     bool c = false;
-    unsigned traced = 0;
+    unsigned traced = 0, visits = 0, tests = 0;
     Hit h{-1, 0, 0, 0};
     d3 wi = mk3(0, 0, 0), tpc = mk3(0, 0, 0);
     if (active) {
@@ -1812,7 +1901,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
         wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
         if (!(dot(wi, N) < 0)) {
             traced = 1;
-            h = trace4_ww<kRayLds>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock);
+            h = trace4_ww<kRayLds, kCount>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock, &visits, &tests);
             if (h.f >= 0) {
                 const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
                 tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
@@ -1822,6 +1911,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
     block_count(P.stats + 2, traced);
+    if (kCount) wave_count2(P.stats + 8, visits, P.stats + 9, tests);
 }
 
 // batch closest hit (test / FFI entry mcpt_closest_hit)
@@ -1872,7 +1962,7 @@ struct DeviceState {
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
     unsigned* pinned_count = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evp0 = nullptr, evp1 = nullptr, evr0 = nullptr, evr1 = nullptr;
 };
 
 }  // namespace
@@ -1988,6 +2078,25 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     }
     if ((rc = upload(*D, lv, &d.lt_v))) return rc;
     if ((rc = upload(*D, ln, &d.lt_n))) return rc;
+    {  // select_a_point_from_lights tables (MCPT_MODE_SHADE_AREA): running sums in table order, as the oracle
+        d.ngroups = (int)s.group_rsum.size();
+        std::vector<double> gcum(d.ngroups), acum(s.NL);
+        std::vector<int2> gr(d.ngroups);
+        double c = 0;
+        for (int k = 0; k < d.ngroups; k++) {
+            c += s.group_rsum[k];
+            gcum[k] = c;
+            gr[k] = make_int2(s.group_start[k], s.group_count[k]);
+            double a = 0;
+            for (int j = s.group_start[k]; j < s.group_start[k] + s.group_count[k]; j++) {
+                a += s.light_area[j];
+                acum[j] = a;
+            }
+        }
+        if ((rc = upload(*D, s.group_rsum, &d.grp_sum)) || (rc = upload(*D, gcum, &d.grp_cum)) || (rc = upload(*D, gr, &d.grp_range)) ||
+            (rc = upload(*D, s.light_area, &d.l_area)) || (rc = upload(*D, acum, &d.l_area_cum)))
+            return rc;
+    }
     const int nl_pad = 256 * ((prep_chunks(s.NL) + 3) / 4);  // whole groups of 4 chunks: the prep kernel reads past N_L unchecked
     std::vector<float4> lpk(3 * nl_pad, make_float4(0, 0, 0, 0));
     std::vector<float> ld(nl_pad, 0.0f);
@@ -2050,6 +2159,8 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     HIP_OK(hipEventCreate(&D->ev1));
     HIP_OK(hipEventCreate(&D->evp0));
     HIP_OK(hipEventCreate(&D->evp1));
+    HIP_OK(hipEventCreate(&D->evr0));
+    HIP_OK(hipEventCreate(&D->evr1));
     *out = D.get();
     sc->devs.push_back(std::move(D));
     return MCPT_OK;
@@ -2195,7 +2306,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int W = cam->width, H = cam->height, npx = W * H;
     const int s0 = (o->sample_begin == 0 && o->sample_end == 0) ? 0 : o->sample_begin;
     const int s1 = (o->sample_begin == 0 && o->sample_end == 0) ? o->spp : o->sample_end;
-    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF && o->mode != MCPT_MODE_SHADE) ||
+    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF && o->mode != MCPT_MODE_SHADE && o->mode != MCPT_MODE_SHADE_AREA) ||
         (o->accel != MCPT_ACCEL_BVH && o->accel != MCPT_ACCEL_GRID)) {
         set_error("invalid render options (spp %d, range [%d,%d), mode %d, accel %d)", o->spp, s0, s1, o->mode, o->accel);
         return MCPT_E_INVALID;
@@ -2222,15 +2333,18 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int qf = o->queue_factor > 0 ? o->queue_factor : 2;
     const int cap = (int)std::min<long long>((long long)qf * target + 1024, (1ll << 30));
     int rc;
-    if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) || (rc = ensure(D.stats, 64)) ||
+    if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) || (rc = ensure(D.stats, 128)) ||
         (rc = ensure(D.work, 256)))
         return rc;
     Queue qa, qb;
     if ((rc = alloc_queue(D.qa, cap, qa)) || (rc = alloc_queue(D.qb, cap, qb))) return rc;
     // extension kernels: MIS and shade split into gen / rays / combine (measured faster), BRDF-only
     // keeps the single kernel (one ray per node; measured faster).  A/B switches:
-#define K_MIS_RAYS (grid ? k_mis_rays<true> : k_mis_rays<false>)
+    const bool count_trav = (o->flags & MCPT_DEBUG_COUNT_TRAVERSAL) != 0;
+#define K_MIS_RAYS (grid ? k_mis_rays<true> : count_trav ? k_mis_rays<false, true> : k_mis_rays<false>)
     const bool split_brdf = (o->flags & MCPT_DEBUG_SPLIT_BRDF) != 0;
+    // the O(N_L) light prep runs for shade_with_mis and for shade() with the spherical sampler
+    const bool needs_prep = o->mode == MCPT_MODE_MIS || o->mode == MCPT_MODE_SHADE;
     const bool fused = !grid && o->mode == MCPT_MODE_BRDF && !split_brdf;  // BRDF-only: k_extend_brdf (the grid runs split)
     Aux aux{};
     if (!fused && (rc = alloc_aux(D.aux, cap, aux))) return rc;
@@ -2248,16 +2362,17 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
         return MCPT_E_SCENE;
     }
-    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE)) {
+    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE |
+                     MCPT_DEBUG_COUNT_TRAVERSAL)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
     const bool count_c1 = !(o->flags & MCPT_RENDER_NO_BACKFACE_STATS);
-    double prep_ms = 0;
-    uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0;
+    double prep_ms = 0, trace_ms = 0;
+    uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0, trace_launches = 0;
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
-    if (o->mode != MCPT_MODE_BRDF && D.d.NL > kSmallNL) {
+    if (needs_prep && D.d.NL > kSmallNL) {
         // + one tile of padding: k_prep_pk2 reads whole batches of kMaskBatch words past nchunks
         if ((rc = ensure(D.masks, ((size_t)((std::max(cap, npx) + 7) / 8 * 8) * nchunks + 8 * kMaskBatch) * 8))) return rc;
         masks = (uint64_t*)D.masks.p;
@@ -2273,7 +2388,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const size_t held = D.cache_bt.bytes + D.cache_lst.bytes + D.cache_info.bytes + D.cache_w.bytes;
     const size_t budget = free_b + held > (16ull << 30) ? free_b + held - (16ull << 30) : 0;
     const bool no_cache = (o->flags & MCPT_DEBUG_NO_ROOT_CACHE) != 0;  // A/B switch
-    if (o->mode != MCPT_MODE_BRDF && s1 - s0 >= 2 && cache_bytes <= budget && !no_cache && D.d.NL > kSmallNL &&
+    if (needs_prep && s1 - s0 >= 2 && cache_bytes <= budget && !no_cache && D.d.NL > kSmallNL &&
         prep_list_wave_bytes(nchunks) * 4 <= kPrepListMaxLds && D.d.NL <= 65535) {
         if ((rc = ensure(D.cache_bt, (size_t)npx * nchunks * 8)) || (rc = ensure(D.cache_lst, (size_t)npx * lstride * 2)) ||
             (rc = ensure(D.cache_info, (size_t)npx * 16)) || (rc = ensure(D.cache_w, (size_t)npx * lstride * 8)))
@@ -2287,7 +2402,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     }
     // every buffer is allocated above (first-call hipMalloc of the cache is not device work); the
     // timed region (seconds, HIP events) starts at the primary-hit kernel
-    HIP_OK(hipMemsetAsync(D.stats.p, 0, 64, st));
+    HIP_OK(hipMemsetAsync(D.stats.p, 0, 128, st));
     HIP_OK(hipEventRecord(D.ev0, st));
     hipLaunchKernelGGL(grid ? k_primary<true> : k_primary<false>, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock),
                        0, st, D.d, cf, (int*)D.hit_f.p, (double*)D.hit_tbg.p);
@@ -2406,7 +2521,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const int ni = (int)n;
         // prep_seconds / prep_launches time the full light-prep kernel (k_prep_pk2) launches only
         bool timed = false;
-        if (o->mode != MCPT_MODE_BRDF) {
+        if (needs_prep) {
             if (pc.use) {  // children: full prep; roots: pick from the root-point cache
                 const int nc = (int)n_children, nr = ni - nc;
                 if (nc > 0) {
@@ -2436,30 +2551,48 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         }
         HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
         const dim3 g256((ni + 255) / 256), b256(256);
+        unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
+        // trace_seconds: HIP events around the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf)
         if (!fused && o->mode == MCPT_MODE_MIS) {
             hipLaunchKernelGGL(k_mis_gen, g256, b256, 0, st, P, *cur, ni, aux);
+            HIP_OK(hipEventRecord(D.evr0, st));
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 3), dim3(kRayBlock), 0, st, D.d, *cur,
-                               ni, aux, 0);
+                               ni, aux, 0, tcnt);
+            HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(k_mis_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
-        } else if (!fused && o->mode == MCPT_MODE_SHADE) {
+        } else if (!fused && (o->mode == MCPT_MODE_SHADE || o->mode == MCPT_MODE_SHADE_AREA)) {
             hipLaunchKernelGGL(k_shade_gen, g256, b256, 0, st, P, *cur, ni, aux);
+            HIP_OK(hipEventRecord(D.evr0, st));
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 2), dim3(kRayBlock), 0, st, D.d, *cur,
-                               ni, aux, 0);
+                               ni, aux, 0, tcnt);
+            HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(k_shade_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else if (!fused) {
             hipLaunchKernelGGL(k_brdf_gen, g256, b256, 0, st, P, *cur, ni, aux);
+            HIP_OK(hipEventRecord(D.evr0, st));
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 1), dim3(kRayBlock), 0, st, D.d, *cur,
-                               ni, aux, 1);
+                               ni, aux, 1, tcnt);
+            HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(k_brdf_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
-        } else
-            hipLaunchKernelGGL(k_extend_brdf, dim3((ni + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, st,
-                               P, *cur, ni, *nxt);
+        } else {
+            HIP_OK(hipEventRecord(D.evr0, st));
+            hipLaunchKernelGGL(count_trav ? k_extend_brdf<true> : k_extend_brdf<false>, dim3((ni + kTraceBlock - 1) / kTraceBlock),
+                               dim3(kTraceBlock), 0, st, P, *cur, ni, *nxt);
+            HIP_OK(hipEventRecord(D.evr1, st));
+        }
         HIP_OK(hipGetLastError());
+        trace_launches++;
         if (timed) {
             float ms = 0;
             HIP_OK(hipEventSynchronize(D.evp1));
             HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
             prep_ms += ms;
+        }
+        {
+            float ms = 0;
+            HIP_OK(hipEventSynchronize(D.evr1));
+            HIP_OK(hipEventElapsedTime(&ms, D.evr0, D.evr1));
+            trace_ms += ms;
         }
         std::swap(cur, nxt);
         if (o->progress && o->progress(o->progress_user, (uint64_t)rnext, (uint64_t)R)) {
@@ -2473,8 +2606,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, D.ev0, D.ev1));
     if (stats) {
-        unsigned long long hs[8] = {0};
-        HIP_OK(hipMemcpy(hs, D.stats.p, 64, hipMemcpyDeviceToHost));
+        unsigned long long hs[16] = {0};
+        HIP_OK(hipMemcpy(hs, D.stats.p, 128, hipMemcpyDeviceToHost));
         stats->seconds = ms * 1e-3;
         stats->camera_samples = (uint64_t)(s1 - s0) * npx;
         stats->light_evals_survived = hs[1];
@@ -2485,7 +2618,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
 
         // k_prep_pk2 counts its full-prep nodes (hs[7]) and k_prep_pick the cached roots (hs[0]);
         // k_prep / k_prep_lane (huge / tiny light sets) run every node in full
-        const uint64_t full = hs[7] ? hs[7] : (o->mode != MCPT_MODE_BRDF ? nodes_total : 0);
+        const uint64_t full = hs[7] ? hs[7] : (needs_prep ? nodes_total : 0);
         stats->prep_full_nodes = full;
         stats->prep_cached_nodes = hs[0];
         stats->prep_cache_points = cache_points;
@@ -2494,6 +2627,10 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->light_evals_candidates = hs[5];
         stats->light_evals_culled_plane = stats->light_evals_total - hs[5] - stats->light_evals_culled_backface;
         stats->spilled_nodes = spilled;
+        stats->trace_seconds = trace_ms * 1e-3;
+        stats->trace_launches = trace_launches;
+        stats->node_visits = hs[8];
+        stats->tri_tests = hs[9];
         stats->reduce_seconds = 0;
         stats->devices_used = 1;
         stats->prep_seconds = prep_ms * 1e-3;
@@ -2576,6 +2713,10 @@ void add_stats(mcpt_stats& t, const mcpt_stats& x) {
     t.prep_cached_nodes += x.prep_cached_nodes;
     t.prep_cache_points += x.prep_cache_points;
     t.spilled_nodes += x.spilled_nodes;
+    t.trace_seconds += x.trace_seconds;
+    t.trace_launches += x.trace_launches;
+    t.node_visits += x.node_visits;
+    t.tri_tests += x.tri_tests;
 }
 
 // progress of a multi-device call: the shards' dispatched counts are summed and the caller's callback
@@ -2846,6 +2987,21 @@ int mcpt_scene_create(const mcpt_scene_desc* d, mcpt_scene** out) {
         }
         hs.light_sum[l] = hs.light_rad[3 * l] + hs.light_rad[3 * l + 1] + hs.light_rad[3 * l + 2];
         hs.light_of[hs.light_facet[l]] = l;
+        hs.light_area.push_back(light_triangle_area(hs, hs.light_facet[l]));
+        // lights (select_a_point_from_lights): desc->light_group, or runs of equal radiance
+        const bool same = l > 0 && (d->light_group ? d->light_group[l] == d->light_group[l - 1]
+                                                   : std::equal(&hs.light_rad[3 * l], &hs.light_rad[3 * l + 3],
+                                                                &hs.light_rad[3 * (l - 1)]));
+        if (!same) {
+            if (d->light_group && l > 0 && d->light_group[l] < d->light_group[l - 1]) {
+                set_error("light_group must be ascending");
+                return MCPT_E_INVALID;
+            }
+            hs.group_rsum.push_back(hs.light_sum[l]);
+            hs.group_start.push_back(l);
+            hs.group_count.push_back(0);
+        }
+        hs.group_count.back()++;
     }
     return finish_scene(std::move(hs), out);
 }
@@ -2864,11 +3020,20 @@ void mcpt_scene_destroy(mcpt_scene* sc) {
             if (b->p) (void)hipFree(b->p);
         if (D->pinned_count) (void)hipHostFree(D->pinned_count);
         if (D->stream) (void)hipStreamDestroy(D->stream);
-        hipEvent_t evs[] = {D->ev0, D->ev1, D->evp0, D->evp1};
+        hipEvent_t evs[] = {D->ev0, D->ev1, D->evp0, D->evp1, D->evr0, D->evr1};
         for (hipEvent_t e : evs)
             if (e) (void)hipEventDestroy(e);
     }
     delete sc;
+}
+
+int mcpt_scene_accel_bytes(const mcpt_scene* sc, uint64_t* bytes) {
+    if (!sc || !bytes) return MCPT_E_INVALID;
+    // 4-wide nodes (128 B) of both BVHs plus their leaf triangles (3 float4 = 48 B)
+    auto nodes4 = [](const Bvh& b) { return (uint64_t)collapse_bvh4(b).size(); };
+    *bytes = (nodes4(sc->bvh) + nodes4(sc->lbvh)) * sizeof(BvhNode4) +
+             (uint64_t)(sc->bvh.leaf_facets.size() + sc->lbvh.leaf_facets.size()) * 3 * sizeof(float4);
+    return MCPT_OK;
 }
 
 int mcpt_scene_counts(const mcpt_scene* sc, int32_t* nf, int32_t* nm, int32_t* nl) {

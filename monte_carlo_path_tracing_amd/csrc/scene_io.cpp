@@ -335,6 +335,32 @@ bool load_light_xml(const std::string& xml_path, HostScene& s, std::vector<Light
     return true;
 }
 
+// lightTriangle::area (Mylight.cpp:66-69): n = (b-a) x (c-a), n = n * (1 / |n|), area = 0.5 *
+// det(b-a, c-a, n) with det(a, b, c) = (a x b) . c (vec.cpp:84-87), in the reference's fp64 order
+double light_triangle_area(const HostScene& s, int f) {
+    double v[3][3], ba[3], ca[3], n[3], t[3];
+    for (int k = 0; k < 3; k++)
+        for (int c = 0; c < 3; c++) v[k][c] = s.pos[9 * f + 3 * k + c];
+    for (int c = 0; c < 3; c++) {
+        ba[c] = v[1][c] - v[0][c];
+        ca[c] = v[2][c] - v[0][c];
+    }
+    auto cross = [](const double* a, const double* b, double* o) {
+        o[0] = a[1] * b[2] - a[2] * b[1];
+        o[1] = a[2] * b[0] - a[0] * b[2];
+        o[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    cross(ba, ca, n);
+    const double inv = 1.0 / std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    for (int c = 0; c < 3; c++) n[c] = n[c] * inv;
+    cross(ba, ca, t);
+    double d = 0;
+    d += t[0] * n[0];
+    d += t[1] * n[1];
+    d += t[2] * n[2];
+    return 0.5 * d;
+}
+
 bool finalize_scene(HostScene& s, std::vector<LightDef> lights, std::string& err) {
     for (int f = 0; f < s.F; f++)
         if (s.mat[f] < 0 || s.mat[f] >= s.M) {
@@ -372,14 +398,23 @@ bool finalize_scene(HostScene& s, std::vector<LightDef> lights, std::string& err
     s.light_facet.clear();
     s.light_rad.clear();
     s.light_sum.clear();
-    for (size_t k = 0; k < lights.size(); k++)
+    s.light_area.clear();
+    s.group_rsum.clear();
+    s.group_start.clear();
+    s.group_count.clear();
+    for (size_t k = 0; k < lights.size(); k++) {
+        s.group_rsum.push_back(lights[k].rgb[0] + lights[k].rgb[1] + lights[k].rgb[2]);  // RadianceRGB::sum
+        s.group_start.push_back(static_cast<int32_t>(s.light_facet.size()));
         for (int f = 0; f < s.F; f++) {
             if (lmat[f] != static_cast<int>(k)) continue;
             s.light_of[f] = static_cast<int>(s.light_facet.size());
             s.light_facet.push_back(f);
             s.light_rad.insert(s.light_rad.end(), lights[k].rgb, lights[k].rgb + 3);
             s.light_sum.push_back(lights[k].rgb[0] + lights[k].rgb[1] + lights[k].rgb[2]);
+            s.light_area.push_back(light_triangle_area(s, f));
         }
+        s.group_count.push_back(static_cast<int32_t>(s.light_facet.size()) - s.group_start.back());
+    }
     s.NL = static_cast<int>(s.light_facet.size());
     // unique normals (Myobj.cpp:680-709): geometric normal flipped toward the vertex normals
     s.unique_n.resize(3 * static_cast<size_t>(s.F));

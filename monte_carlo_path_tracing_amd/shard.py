@@ -1,20 +1,22 @@
-"""Multi-GPU partitioning of a frame.
+"""Host-side mirror of the library's multi-GPU partitioning of a frame.
 
-Every (pixel, sample) is independent and the RNG is keyed by the GLOBAL sample index, so a frame
-shards by sample range with no data-path exchange: rank r renders samples
-[r*spp/G, (r+1)*spp/G) of every pixel into its own fp64 framebuffer, and ONE reduce (sum) over
-RCCL combines them.  The image is independent of G up to fp64 summation order.
+Every (pixel, sample) is independent (main.cpp:557-588) and the RNG is keyed by the GLOBAL sample
+index, so a frame shards by sample range with no data-path exchange.  The library
+(render.hip `shard_range`, used by mcpt_render_opts.devices and .comm) gives shard k of n of the job
+[begin, end) the samples [begin + len*k//n, begin + len*(k+1)//n); `sample_range` is the same
+formula, for callers that shard by hand (e.g. host copies summed over gloo in the tests).
 """
 
 
-def sample_range(rank, world_size, spp):
-    """Contiguous, balanced split of [0, spp) -- rank gets [begin, end)."""
+def sample_range(rank, world_size, spp, begin=0):
+    """Contiguous, balanced split of [begin, begin + spp) -- rank gets [a, b)."""
     if not (0 <= rank < world_size) or spp < 0:
         raise ValueError("bad rank/world/spp")
-    return rank * spp // world_size, (rank + 1) * spp // world_size
+    return begin + rank * spp // world_size, begin + (rank + 1) * spp // world_size
 
 
 def reduce_framebuffers(fb, dist, dst=0):
-    """Sum per-rank framebuffers onto `dst` (torch tensor, any backend: gloo on CPU, nccl=RCCL on GPU)."""
+    """Sum per-rank framebuffers onto `dst` with torch.distributed (host copies over gloo).  The GPU
+    path does this inside the library with RCCL (mcpt_render_opts.comm)."""
     dist.reduce(fb, dst=dst, op=dist.ReduceOp.SUM)
     return fb

@@ -16,7 +16,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-NAMES = {0: "mis", 1: "brdf", 2: "shade"}
+NAMES = {0: "mis", 1: "brdf", 2: "shade", 3: "shade_area"}
 
 
 def main():

@@ -82,6 +82,11 @@ struct orc_scene {
     double* larea;   /* NL */
     double* lrad;    /* NL*3 */
     double* lsum;    /* NL: RadianceRGB::sum() */
+    /* Mylight::lightsRadiance in map (name) order, every XML light, for the uniform-area sampler:
+     * RadianceRGB::sum(), and the run [start, start + count) of its triangles in the light table */
+    int nlname;
+    double* lname_sum;
+    int *lname_start, *lname_count;
     int has_cam;
     orc_camera cam;
     /* uniform grid */
@@ -493,7 +498,13 @@ orc_scene* orc_scene_load(const char* obj_path, const char* xml_path) {
     s->lrad = (double*)malloc(sizeof(double) * 3 * (NL + 1));
     s->lsum = (double*)malloc(sizeof(double) * (NL + 1));
     int li = 0;
-    for (int k = 0; k < nl; k++)          /* lightsTriangles map: name order, then facet order */
+    s->nlname = nl;
+    s->lname_sum = (double*)malloc(sizeof(double) * (nl + 1));
+    s->lname_start = (int*)malloc(sizeof(int) * (nl + 1));
+    s->lname_count = (int*)malloc(sizeof(int) * (nl + 1));
+    for (int k = 0; k < nl; k++) {        /* lightsTriangles map: name order, then facet order */
+        s->lname_sum[k] = L[k].rgb[0] + L[k].rgb[1] + L[k].rgb[2];  /* RadianceRGB::sum (RadianceRGB.cpp:70-73) */
+        s->lname_start[k] = li;
         for (int f = 0; f < s->F; f++) {
             if (lmat[f] != k) continue;
             v3 a = fvert(s, f, 0), b = fvert(s, f, 1), c = fvert(s, f, 2);
@@ -506,6 +517,8 @@ orc_scene* orc_scene_load(const char* obj_path, const char* xml_path) {
             s->light_of[f] = li;
             li++;
         }
+        s->lname_count[k] = li - s->lname_start[k];
+    }
     free(lmat);
     free(L);
     /* unique normals (Myobj.cpp:680-709) */
@@ -526,6 +539,7 @@ void orc_scene_free(orc_scene* s) {
     if (!s) return;
     free(s->v); free(s->vn); free(s->mat); free(s->light_of); free(s->un); free(s->mtl);
     free(s->lfacet); free(s->larea); free(s->lrad); free(s->lsum);
+    free(s->lname_sum); free(s->lname_start); free(s->lname_count);
     free(s->cell_start); free(s->cell_tri);
     free(s);
 }
@@ -1091,7 +1105,66 @@ typedef struct {
     uint64_t seed, pixel, sample;
     light_state L;    /* RefRng: the global Mylight member state (stale-pdf quirk) */
     uint64_t stats[4]; /* shading nodes, light preps, extension rays, light-only rays */
+    int area_lights;  /* shade(): select_a_point_from_lights instead of the spherical sampler */
 } ctx;
+
+/* discrete_distribution over w[0..n) as libstdc++ (random.tcc): fewer than two weights -> index 0,
+ * probability 1, NO draw; else one generate_canonical, normalised partial sums with the last forced
+ * to 1, lower_bound.  RefRng draws from *e; the counter rule is "first cumulative weight >= u * sum"
+ * (the GPU's).  *p = the index's probability as probabilities().at(i) = w[i] / sum. */
+static int discrete_pick(ctx* C, minstd* e, uint64_t key, uint32_t dim, const double* w, int n, double* p) {
+    if (n < 2) { *p = 1.0; return 0; }
+    double sum = 0.0;
+    for (int i = 0; i < n; i++) sum += w[i];
+    int r = n - 1;
+    if (C->rng == ORC_RNG_REF) {
+        const double u = canon(e);
+        double cp = 0;
+        for (int i = 0; i < n - 1; i++) {
+            cp = (i == 0) ? w[0] / sum : cp + w[i] / sum;
+            if (!(cp < u)) { r = i; break; }
+        }
+    } else {
+        const double target = counter_u(key, dim) * sum;
+        double cum = 0;
+        for (int i = 0; i < n; i++) {
+            cum += w[i];
+            if (cum >= target) { r = i; break; }
+        }
+    }
+    *p = w[r] / sum;
+    return r;
+}
+
+/* Mylight::select_a_point_from_lights (Mylight.cpp:102-160): a light of the lightsRadiance map by
+ * RadianceRGB::sum(), one of its triangles by area, a uniform point by beta = 1 - sqrt(1 - ksi1),
+ * gamma = (1 - beta) ksi2; proba = p(light) p(triangle) / area (an area-measure pdf).  RefRng: one
+ * engine, draws in that order; counter dims 1 (light), 7 (triangle), 2-3 (ksi1, ksi2).  Returns the
+ * light-table index, or -1 for a light whose material has no triangles (the reference throws
+ * std::out_of_range in lightsTriangles.at, Mylight.cpp:128). */
+static int area_light_sample(ctx* C, uint64_t key, v3* coord, double* prob) {
+    const orc_scene* s = C->s;
+    minstd e = {1};
+    if (C->rng == ORC_RNG_REF) e = ref_engine(&C->ctr);
+    double p1, p2;
+    const int k = discrete_pick(C, &e, key, 1, s->lname_sum, s->nlname, &p1);
+    if (s->nlname == 0 || s->lname_count[k] == 0) return -1;
+    const int j0 = s->lname_start[k];
+    const int j = j0 + discrete_pick(C, &e, key, 7, s->larea + j0, s->lname_count[k], &p2);
+    const double ksi1 = C->rng == ORC_RNG_REF ? canon(&e) : counter_u(key, 2);
+    const double ksi2 = C->rng == ORC_RNG_REF ? canon(&e) : counter_u(key, 3);
+    const double beta = 1 - sqrt(1 - ksi1);
+    const double gamma = (1 - beta) * ksi2;
+    const double alpha = 1 - beta - gamma;
+    const int f = s->lfacet[j];
+    *coord = vadd(vadd(vmul(fvert(s, f, 0), alpha), vmul(fvert(s, f, 1), beta)), vmul(fvert(s, f, 2), gamma));
+    double proba = 1.0;
+    proba *= p1;
+    proba *= p2;
+    proba *= 1.0 / s->larea[j];
+    *prob = proba;
+    return j;
+}
 
 static v3 rgb_mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 
@@ -1255,33 +1328,45 @@ static v3 shade_direct(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t
 
     /* direct light (main.cpp:295-316) */
     v3 L_dir = mk(0, 0, 0);
-    C->stats[1]++;
-    light_prep(s, p, N, &C->L);
     v3 coord, I = mk(0, 0, 0);
     double lprob = 1;
     int lfacet = 0;  /* sampledLightPoint(0, 0, ...) of the empty set (Mylight.cpp:263-266): facet (0,0) */
-    if (C->L.count == 0 || fabs(C->L.wsum) < EPS) {
-        coord = vadd(vmul(N, -1), p);
-    } else {
-        double k1, k2;
-        int rind;
-        if (C->rng == ORC_RNG_REF) {
-            minstd e = ref_engine(&C->ctr);
-            rind = C->L.count >= 2 ? ref_pick(&C->L, canon(&e)) : 0;
-            k1 = canon(&e);
-            k2 = canon(&e);
+    int have_light = 1;
+    if (C->area_lights) {  /* main.cpp:296: select_a_point_from_lights */
+        const int li = area_light_sample(C, key, &coord, &lprob);
+        if (li >= 0) {
+            lfacet = s->lfacet[li];
+            I = ld3(s->lrad + 3 * li);
         } else {
-            rind = counter_pick(&C->L, counter_u(key, 1));
-            k1 = counter_u(key, 2);
-            k2 = counter_u(key, 3);
+            have_light = 0;
+            coord = vadd(vmul(N, -1), p);
         }
-        int li = light_sample_after_pick(s, &C->L, rind, p, k1, k2, &coord, &lprob);
-        lfacet = s->lfacet[li];
-        I = ld3(s->lrad + 3 * li);
+    } else {  /* select_a_point_from_lights_spherical_triangle (Mylight.cpp:163-318) */
+        C->stats[1]++;
+        light_prep(s, p, N, &C->L);
+        if (C->L.count == 0 || fabs(C->L.wsum) < EPS) {
+            coord = vadd(vmul(N, -1), p);
+        } else {
+            double k1, k2;
+            int rind;
+            if (C->rng == ORC_RNG_REF) {
+                minstd e = ref_engine(&C->ctr);
+                rind = C->L.count >= 2 ? ref_pick(&C->L, canon(&e)) : 0;
+                k1 = canon(&e);
+                k2 = canon(&e);
+            } else {
+                rind = counter_pick(&C->L, counter_u(key, 1));
+                k1 = counter_u(key, 2);
+                k2 = counter_u(key, 3);
+            }
+            int li = light_sample_after_pick(s, &C->L, rind, p, k1, k2, &coord, &lprob);
+            lfacet = s->lfacet[li];
+            I = ld3(s->lrad + 3 * li);
+        }
     }
     v3 n1 = ld3(s->un + 3 * lfacet);
     v3 wl = vnormalized(vsub(coord, p));
-    if (vdot(wl, N) > 0 && vdot(vmul(wl, -1), n1) > 0) {
+    if (have_light && vdot(wl, N) > 0 && vdot(vmul(wl, -1), n1) > 0) {
         hitrec h;
         C->stats[2]++;
         int g = grid_trace(s, p, wl, f, 0, &h);
@@ -1323,7 +1408,8 @@ static v3 shade_direct(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t
 
 static v3 shade_root(ctx* C, int mode, int f, double beta, double gamma, v3 wo) {
     if (mode == ORC_MODE_MIS) return shade_mis(C, f, beta, gamma, wo, 1);
-    if (mode == ORC_MODE_SHADE) return shade_direct(C, f, beta, gamma, wo, 1);
+    C->area_lights = mode == ORC_MODE_SHADE_AREA;
+    if (mode == ORC_MODE_SHADE || mode == ORC_MODE_SHADE_AREA) return shade_direct(C, f, beta, gamma, wo, 1);
     return shade_brdf(C, f, beta, gamma, wo, 1);
 }
 

@@ -25,7 +25,9 @@ extern "C" {
 
 typedef struct orc_scene orc_scene;
 
-enum { ORC_MODE_MIS = 0, ORC_MODE_BRDF = 1, ORC_MODE_SHADE = 2 }; /* main.cpp:402 / :348 / :269 */
+/* main.cpp:402 / :348 / :269; SHADE_AREA = shade() with the uniform-area light sampler
+ * select_a_point_from_lights (Mylight.cpp:102-160, the alternative commented out at main.cpp:296) */
+enum { ORC_MODE_MIS = 0, ORC_MODE_BRDF = 1, ORC_MODE_SHADE = 2, ORC_MODE_SHADE_AREA = 3 };
 enum { ORC_RNG_REF = 0, ORC_RNG_COUNTER = 1 };
 
 /* camera: eye, lookat, up, fovy parameter (the reference's tan(fovy/360) quirk), eye pull-back

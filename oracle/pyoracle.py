@@ -10,7 +10,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-MODE_MIS, MODE_BRDF, MODE_SHADE = 0, 1, 2
+MODE_MIS, MODE_BRDF, MODE_SHADE, MODE_SHADE_AREA = 0, 1, 2, 3  # ORC_MODE_* (mcpt_oracle.h)
 RNG_REF, RNG_COUNTER = 0, 1
 
 

@@ -142,8 +142,10 @@ static RadianceRGB ref_shade_mis(intersec_result point, vec wo) {
 }
 
 // Restatement of main.cpp:269-344 (shade, the integrator main() ships with, main.cpp:575); direct
-// light through the reference's select_a_point_from_lights_spherical_triangle (Mylight.cpp:163).
-static RadianceRGB ref_shade(intersec_result point, vec wo) {
+// light through the reference's select_a_point_from_lights_spherical_triangle (Mylight.cpp:163),
+// or -- area = true -- through its uniform-area sampler select_a_point_from_lights
+// (Mylight.cpp:102-160), the alternative left commented out at main.cpp:296.
+static RadianceRGB ref_shade(intersec_result point, vec wo, bool area = false) {
     vec p = interp(veach->get_vertexes_of_facet(point.s, point.f), point.beta, point.gamma);
     vec N = interp(veach->get_normals_of_facet(point.s, point.f), point.beta, point.gamma).normalized();
     if (N.dot_product(wo) < 0) return RadianceRGB(0, 0, 0);
@@ -151,7 +153,8 @@ static RadianceRGB ref_shade(intersec_result point, vec wo) {
     if (li != lights->islight.end()) return li->second;
     tinyobj::material_t mtl = mat_of(point.s, point.f);
     RadianceRGB L_dir;
-    sampledLightPoint lp = lights->select_a_point_from_lights_spherical_triangle(p, N, *veach);
+    sampledLightPoint lp = area ? lights->select_a_point_from_lights(*veach)
+                                : lights->select_a_point_from_lights_spherical_triangle(p, N, *veach);
     vec x1 = lp.coord;
     vec n1 = veach->get_unique_normal_of_facet(lp.s, lp.f);
     vec wl = (x1 - p).normalized();
@@ -169,7 +172,7 @@ static RadianceRGB ref_shade(intersec_result point, vec wo) {
     intersec_result r2 = veach->closet_ray_intersect(p, wi.dir, triangle(point.s, point.f));
     if (r2.isIntersec && lights->islight.find(triangle(r2.s, r2.f)) == lights->islight.end()) {
         BRDF brdf = BRDF::get_brdf_phong(N, wi.dir, wo, kd_of(mtl), ks_of(mtl), mtl.shininess);
-        L_indir = ref_shade(r2, wi.dir * -1) * brdf * (wi.dir.dot_product(N) / wi.pdf / 0.6);
+        L_indir = ref_shade(r2, wi.dir * -1, area) * brdf * (wi.dir.dot_product(N) / wi.pdf / 0.6);
     }
     return L_dir + L_indir;
 }
@@ -248,7 +251,7 @@ int main(int argc, char** argv) {
                 double s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
                 for (int k = 0; k < spp && rs.isIntersec; k++) {
                     RadianceRGB L = mode == 0 ? ref_shade_mis(rs, dir * -1)
-                                    : mode == 1 ? ref_shade_brdf(rs, dir * -1) : ref_shade(rs, dir * -1);
+                                    : mode == 1 ? ref_shade_brdf(rs, dir * -1) : ref_shade(rs, dir * -1, mode == 3);
                     for (int q = 0; q < 3; q++) {
                         s1[q] += L.RGB[q];
                         s2[q] += L.RGB[q] * L.RGB[q];
@@ -485,7 +488,7 @@ int main(int argc, char** argv) {
     }
 
     // ---- G7 per-sample radiance, both integrators, RefRng replay keys -----------------------
-    for (int mode = 0; mode < 3; mode++) {  // 0 shade_with_mis, 1 shade_with_brdf, 2 shade
+    for (int mode = 0; mode < 4; mode++) {  // 0 shade_with_mis, 1 shade_with_brdf, 2 shade, 3 shade (area lights)
         std::vector<double> o;
         const int NS = mode == 1 ? 6000 : 3000;  // MIS / shade run a light prep per node
         for (int r = 0; r < NS; r++) {
@@ -496,14 +499,16 @@ int main(int argc, char** argv) {
             clk() = c0;
             RadianceRGB L(0, 0, 0);
             if (rs.isIntersec)
-                L = mode == 0 ? ref_shade_mis(rs, dir * -1) : mode == 1 ? ref_shade_brdf(rs, dir * -1) : ref_shade(rs, dir * -1);
+                L = mode == 0 ? ref_shade_mis(rs, dir * -1) : mode == 1 ? ref_shade_brdf(rs, dir * -1)
+                                                                  : ref_shade(rs, dir * -1, mode == 3);
             o.push_back(i);
             o.push_back(j);
             o.push_back((double)c0);
             o.push_back((double)(clk() - c0));
             for (int c = 0; c < 3; c++) o.push_back(L.RGB[c]);
         }
-        npy_f64(out + (mode == 0 ? "/sample_mis.npy" : mode == 1 ? "/sample_brdf.npy" : "/sample_shade.npy"), o, 7);
+        npy_f64(out + (mode == 0 ? "/sample_mis.npy" : mode == 1 ? "/sample_brdf.npy"
+                                           : mode == 2 ? "/sample_shade.npy" : "/sample_shade_area.npy"), o, 7);
     }
     printf("golden vectors written to %s (F=%zu)\n", out.c_str(), F);
     return 0;

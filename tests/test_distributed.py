@@ -1,7 +1,8 @@
-"""Multi-rank sharding on CPU (gloo, world size 2): each rank renders its sample range of the frame
--- here with the CPU oracle standing in for the GPU kernels, since this runs without a GPU -- and
-shard.reduce_framebuffers sums them on rank 0, exactly as bench.py does over RCCL.  The reduced
-frame must equal the single-process frame (the RNG is keyed by the global sample index)."""
+"""Multi-rank sharding logic on CPU (gloo, world size 2): each rank renders its sample range of the
+frame with the CPU oracle (this container has no GPU) and gloo sums them on rank 0.  The reduced
+frame must equal the single-process frame (the RNG is keyed by the global sample index), which is
+the property the library's RCCL paths rely on.  The same split on the HIP kernels -- two processes
+on one GPU, the device-list path and the library communicator -- is tests/test_multi_gpu.py (-m gpu)."""
 import os
 import sys
 
@@ -41,9 +42,11 @@ def test_sample_range_partition():
     from monte_carlo_path_tracing_amd.shard import sample_range
     for world in (1, 2, 3, 8):
         for spp in (0, 1, 7, 1024):
-            r = [sample_range(k, world, spp) for k in range(world)]
-            assert r[0][0] == 0 and r[-1][1] == spp
-            assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))
+            for begin in (0, 5):
+                r = [sample_range(k, world, spp, begin) for k in range(world)]
+                assert r[0][0] == begin and r[-1][1] == begin + spp
+                assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))
+                assert max(b - a for a, b in r) - min(b - a for a, b in r) <= 1
     with pytest.raises(ValueError):
         sample_range(2, 2, 8)
 

@@ -108,7 +108,8 @@ def test_tone_mapping():
 
 
 @pytest.mark.parametrize("mode,name", [(po.MODE_MIS, "sample_mis.npy"), (po.MODE_BRDF, "sample_brdf.npy"),
-                                       (po.MODE_SHADE, "sample_shade.npy")])
+                                       (po.MODE_SHADE, "sample_shade.npy"),
+                                       (po.MODE_SHADE_AREA, "sample_shade_area.npy")])
 def test_integrator_refrng_replay_bitexact(scene, mode, name):
     """RefRng replay of main.cpp:269-494 (DFS order, stale-pdf quirk) vs the reference components."""
     cam = po.reference_camera(400, 300)

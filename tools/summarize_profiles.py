@@ -42,6 +42,30 @@ def counters(d):
     return {k: dict(v, dispatches=len(disp[k])) for k, v in agg.items()}
 
 
+def pmc_latest(tag, summary):
+    """Per-kernel PMC figures bench.py attaches to its roofline objects (profiles/pmc_latest.json):
+    VALU busy = 4 * SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs),
+    the effective clock GRBM_GUI_ACTIVE / 8 / duration, and HBM-side bytes per dispatch (FETCH_SIZE
+    x2 + WRITE_SIZE, MI355X_MICROARCH.md); the SQ and GRBM counters come from separate passes over
+    the same workload, so both are taken per dispatch."""
+    ks, sq, hbm = summary.get("kernel_stats", {}), summary.get("sq", {}), summary.get("hbm", {})
+    out = {"source": "profiles/%s_summary.json (rocprofv3 --pmc passes; tools/summarize_profiles.py)" % tag,
+           "kernels": {}}
+    for k, h in hbm.items():
+        if not k.startswith("k_") or k not in sq or not h.get("grbm_gui_active"):
+            continue
+        g = h["grbm_gui_active"] / h["dispatches"]  # summed over the 8 XCDs, per dispatch
+        a = sq[k]["SQ_ACTIVE_INST_VALU"] / sq[k]["dispatches"]
+        e = {"valu_busy": round(4 * a / (1024 * g / 8), 4),
+             "hbm_bytes_per_dispatch": h["fetch_bytes_per_dispatch"] + h["write_bytes_per_dispatch"],
+             "dispatches": h["dispatches"]}
+        if k in ks:
+            e["avg_us"] = ks[k]["avg_us"]
+            e["eff_clock_GHz"] = round(g / 8 / (ks[k]["avg_us"] * 1e-6) / 1e9, 3)
+        out["kernels"][k] = e
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
@@ -93,6 +117,10 @@ def main():
                 summary["bench_totals"] = json.loads(line.split(":", 1)[1])
     with open(os.path.join(out, "%s_summary.json" % a.tag), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
+    latest = pmc_latest(a.tag, summary)
+    if latest["kernels"]:
+        with open(os.path.join(out, "pmc_latest.json"), "w") as f:
+            json.dump(latest, f, indent=1, sort_keys=True)
     print(json.dumps({k: summary[k] for k in summary if k != "sq"}, indent=1)[:3000])
 
 
