@@ -160,6 +160,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20240430)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and L2 check")
+    ap.add_argument("--fresh-pdf", action="store_true",
+                    help="MIS with the node's own light pdf (MCPT_RENDER_FRESH_PDF) instead of the reference's stale one")
     ap.add_argument("--out", default="", help="optional .bmp of the rendered frame (rank 0)")
     args = ap.parse_args()
 
@@ -196,7 +198,7 @@ def main():
     fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
     scratch = torch.zeros_like(fb)
 
-    flags = mcpt.RENDER_NO_BACKFACE_STATS
+    flags = mcpt.RENDER_NO_BACKFACE_STATS | (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0)
     for k in range(args.warmup):  # warmup renders (same kernels and flags as the timed steps) go to scratch
         mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
                            sample_range=(0, world * S), comm=comm, flags=flags)
@@ -230,7 +232,7 @@ def main():
     for k in range(args.steps):
         st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
                                 sample_range=(k * world * S, (k + 1) * world * S), comm=comm,
-                                flags=mcpt.DEBUG_COUNT_TRAVERSAL)
+                                flags=mcpt.DEBUG_COUNT_TRAVERSAL | (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0))
         for key, v in st.as_dict().items():
             rep[key] = rep.get(key, 0) + v
     for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays",

@@ -130,6 +130,12 @@ typedef struct {
  * mcpt_stats.light_evals_culled_backface then reads 0 and _culled_plane holds both cheap-stage culls
  * (every prep variant reports it that way).  Images and all other statistics are unchanged. */
 enum { MCPT_RENDER_NO_BACKFACE_STATS = 1 };
+/* mcpt_render_opts.flags: shade_with_mis evaluates the BRDF branch's light pdf with the node's OWN
+ * light prep instead of the reference's stale sampler state (main.cpp:443 vs :487: the state the
+ * last prep inside the light branch's recursion left, Mylight.cpp:484-493).  The default follows
+ * the reference; this flag is the "fixed" estimator (4.6e-3 relative L2 from the reference's on the
+ * Veach stand-in, profiles/stale_pdf_delta.json). */
+enum { MCPT_RENDER_FRESH_PDF = 2 };
 
 /* zero-fills *opts and sets struct_size, device = -1, seed = 20240430, spp = 10 (main.cpp:567),
  * mode = MCPT_MODE_MIS */

@@ -356,6 +356,7 @@ struct Queue {
     int* pixel;     // cap
     int* sample;    // cap
     uint64_t* node; // cap   heap id (MIS) / depth+1 (BRDF)
+    int* par;       // cap   MIS tree reduction: parent slot * 2 + (0 light, 1 BRDF child), -1 root
     double* wsum;   // cap   (MIS prep output)
     int* pick;      // cap   (MIS prep output)
     unsigned* count;
@@ -446,58 +447,67 @@ __device__ inline void node_point(const DScene& S, int f, double beta, double ga
 }
 
 // node entry of shade_with_* (main.cpp:406-437 / :351-383): interpolate, back-face -> 0,
-// emitter -> emit, Russian roulette; survivors are appended to the queue.
-// Must be called by ALL threads of the workgroup (block_append); `active` masks the lane.
-__device__ inline void node_entry(const Params& P, bool active, int f, double beta, double gamma, d3 wo, d3 tp,
-                                  int pixel, int sample, uint64_t node, Queue& q) {
-    const DScene& S = P.S;
+// emitter -> its emission, Russian roulette (MIS / BRDF: dim 0; shade() draws it later); kind:
+// 0 contributes nothing, 1 emitter (light index li), 2 shading node (p, N) to push.
+struct Entry {
+    int kind, li;
     d3 p, N;
-    bool push = false;
-    if (active) {
-        // MIS: heap ids (root 1, children 2n, 2n+1); BRDF / shade: paths (node = depth + 1)
-        const bool too_deep = P.mode == MCPT_MODE_MIS ? node >= (2ull << MCPT_MAX_DEPTH) : node > MCPT_MAX_DEPTH + 1;
-        if (!too_deep) {
-            node_point(S, f, beta, gamma, &p, &N);
-            if (!(dot(N, wo) < 0)) {
-                const int li = S.tri_light[f];
-                if (li >= 0) {
-                    double* px = P.fb + 3 * (size_t)pixel;
-                    unsafeAtomicAdd(px + 0, tp.x * S.light_rad[3 * li + 0] * P.inv_spp);
-                    unsafeAtomicAdd(px + 1, tp.y * S.light_rad[3 * li + 1] * P.inv_spp);
-                    unsafeAtomicAdd(px + 2, tp.z * S.light_rad[3 * li + 2] * P.inv_spp);
-                } else if (P.mode == MCPT_MODE_SHADE || P.mode == MCPT_MODE_SHADE_AREA) {
-                    push = true;  // shade() samples direct light before its RR draw (main.cpp:295-327)
-                } else {
-                    const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
-                    push = !(counter_u(key, 0) > MCPT_P_RR);
-                }
-            }
-        }
+};
+__device__ inline Entry entry_eval(const Params& P, bool active, int f, double beta, double gamma, d3 wo, int pixel,
+                                   int sample, uint64_t node) {
+    const DScene& S = P.S;
+    Entry e{0, -1, mk3(0, 0, 0), mk3(0, 0, 0)};
+    if (!active) return e;
+    // MIS: heap ids (root 1, children 2n, 2n+1); BRDF / shade: paths (node = depth + 1)
+    const bool too_deep = P.mode == MCPT_MODE_MIS ? node >= (2ull << MCPT_MAX_DEPTH) : node > MCPT_MAX_DEPTH + 1;
+    if (too_deep) return e;
+    node_point(S, f, beta, gamma, &e.p, &e.N);
+    if (dot(e.N, wo) < 0) return e;
+    const int li = S.tri_light[f];
+    if (li >= 0) {
+        e.kind = 1;
+        e.li = li;
+    } else if (P.mode == MCPT_MODE_SHADE || P.mode == MCPT_MODE_SHADE_AREA) {
+        e.kind = 2;  // shade() samples direct light before its RR draw (main.cpp:295-327)
+    } else {
+        const uint64_t key = counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, node);
+        e.kind = counter_u(key, 0) > MCPT_P_RR ? 0 : 2;
     }
+    return e;
+}
+// appends a shading node to q.  Must be called by ALL threads of the workgroup (block_append).
+__device__ inline void queue_push(const Params& P, bool push, const Entry& e, int f, d3 wo, d3 tp, int pixel, int sample,
+                                  uint64_t node, int par, Queue& q) {
     const int slot = block_append(q.count, push);
-    if (push) {
-        if (slot >= q.cap) {
-            atomicOr((unsigned long long*)(P.stats + 4), 1ull);
-            return;
-        }
-        const size_t s = (size_t)slot;
-        q.p[3 * s] = p.x;
-        q.p[3 * s + 1] = p.y;
-        q.p[3 * s + 2] = p.z;
-        q.n[3 * s] = N.x;
-        q.n[3 * s + 1] = N.y;
-        q.n[3 * s + 2] = N.z;
-        q.wo[3 * s] = wo.x;
-        q.wo[3 * s + 1] = wo.y;
-        q.wo[3 * s + 2] = wo.z;
-        q.tp[3 * s] = tp.x;
-        q.tp[3 * s + 1] = tp.y;
-        q.tp[3 * s + 2] = tp.z;
-        q.f[s] = f;
-        q.pixel[s] = pixel;
-        q.sample[s] = sample;
-        q.node[s] = node;
+    if (!push) return;
+    if (slot >= q.cap) {
+        atomicOr((unsigned long long*)(P.stats + 4), 1ull);
+        return;
     }
+    const size_t s = (size_t)slot;
+    q.p[3 * s] = e.p.x, q.p[3 * s + 1] = e.p.y, q.p[3 * s + 2] = e.p.z;
+    q.n[3 * s] = e.N.x, q.n[3 * s + 1] = e.N.y, q.n[3 * s + 2] = e.N.z;
+    q.wo[3 * s] = wo.x, q.wo[3 * s + 1] = wo.y, q.wo[3 * s + 2] = wo.z;
+    q.tp[3 * s] = tp.x, q.tp[3 * s + 1] = tp.y, q.tp[3 * s + 2] = tp.z;
+    q.f[s] = f;
+    q.pixel[s] = pixel;
+    q.sample[s] = sample;
+    q.node[s] = node;
+    q.par[s] = par;
+}
+// entry + push with forward throughput: emitters add tp x emission to the framebuffer (BRDF-only,
+// shade() and the fresh-pdf MIS path).  Must be called by ALL threads of the workgroup.
+__device__ inline void node_entry(const Params& P, bool active, int f, double beta, double gamma, d3 wo, d3 tp,
+                                  int pixel, int sample, uint64_t node, Queue& q, int par = -1) {
+    const Entry e = entry_eval(P, active, f, beta, gamma, wo, pixel, sample, node);
+    if (e.kind == 1) {
+        const DScene& S = P.S;
+        double* px = P.fb + 3 * (size_t)pixel;
+        unsafeAtomicAdd(px + 0, tp.x * S.light_rad[3 * e.li + 0] * P.inv_spp);
+        unsafeAtomicAdd(px + 1, tp.y * S.light_rad[3 * e.li + 1] * P.inv_spp);
+        unsafeAtomicAdd(px + 2, tp.z * S.light_rad[3 * e.li + 2] * P.inv_spp);
+    }
+    queue_push(P, e.kind == 2, e, f, wo, tp, pixel, sample, node, par, q);
 }
 
 // ============================================================================================
@@ -561,6 +571,7 @@ __global__ __launch_bounds__(256) void k_queue_move(Queue src, int sb, Queue dst
     dst.pixel[d] = src.pixel[s];
     dst.sample[d] = src.sample[s];
     dst.node[d] = src.node[s];
+    dst.par[d] = src.par[s];
 }
 
 // root shading points of the pixels whose primary hit is a front-facing non-emitter (the nodes
@@ -1556,11 +1567,98 @@ __global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int 
 //   flags    bit 0 trace d1, bit 1 trace d2, bit 2 trace d2 against the light BVH
 //   hf/hbg   ray set k in [k*cap, (k+1)*cap): hit facet, (beta, gamma)
 struct Aux {
-    double *d1, *d2, *w1, *w2, *c2, *hbg;
+    double *d1, *d2, *w1, *w2, *c2, *hbg, *s1;
     int *flags, *hf;
     int cap;
 };
 
+// ---- shade_with_mis as a bottom-up tree reduction (the reference's stale light pdf) ------------
+// The reference evaluates the BRDF branch's light pdf with the light sampler's state after the
+// light branch's recursion: the prep of the LAST node that ran one in DFS order inside the light
+// child's subtree (main.cpp:443 vs :487, Mylight.cpp:484-493).  That node is the end of the path
+// from the light child that steps to the BRDF child when it is a shading node (passes entry + RR),
+// else to the light child when it is, else stops -- known only once the subtree below has been
+// expanded.  So the radiance is reduced bottom-up, as the reference's recursion returns it: a node
+// with shading children holds a slot until both have reported their radiance and their path end's
+// prep state (x, N, weights_sum); then L = L_light + L_brdf with the reference's operation order
+// (main.cpp:464, :491) and the node reports to its parent (the root splats L / spp).  Expansion is
+// unchanged (it needs no weights), so the wavefront stays as wide as before.
+struct Slots {
+    int* par;      // parent code: slot * 4 + role * 2 (0 light, 1 BRDF child) + need; -1 = root (need:
+                   // some ancestor will evaluate a light pdf at this subtree's path-end state)
+    int* pix;      // pixel (root splat)
+    int* pend;     // shading children still to report
+    int* fl;       // bit0 light child shading, bit1 BRDF child shading, bit2 BRDF child emitter, bit3 BRDF edge,
+                   // bit4 this node's path-end state is needed (its own parent code's need bit)
+    int* li;       // light triangle along the BRDF direction (light-only ray) or -1
+    double* w;     // 10 per slot: brdf of the light edge [3], its scalar s1, brdf of the BRDF edge [3], pdf, cos, s2
+    double* Ll;    // 3: light child's radiance (or the light edge's finished contribution)
+    double* Lb;    // 3: BRDF child's radiance (or its emitter's emission)
+    double* last;  // 14: path-end prep state (x, N, weights_sum) reported by the light / BRDF child
+    // Allocation, freeing and the ready lists are split over kSlotShards shards, each with its own
+    // counters on its own 64-B line: a single counter word saturates at ~88 atomics/us
+    // (MI355X_MICROARCH.md), and a generation makes ~10^5 of these appends.  Slot ids carry their
+    // allocating shard in the low bits (bump allocation: local << 5 | shard); a workgroup allocates
+    // from shard blockIdx & 31, a wave frees and appends to shard (global wave index) & 31.
+    int* ring;     // per shard: free slot ids (FIFO), rcap_ring entries each
+    int* ready0;   // per shard: slots whose children have all reported, rcap_ready entries each (parity 0)
+    int* ready1;   //   (parity 1)
+    unsigned* ctrl;  // per shard, 16 words: [0] bump [1] ring head [2] ring tail [3] ring end this pass [4..5] ready counts
+    int cap;       // slot ids < cap (= rcap << 5)
+    int rcap;      // slots per shard
+    int ring_cap, ready_cap;  // entries per shard of ring / ready lists
+};
+constexpr int kSlotShards = 32;
+constexpr int kCtrlBytes = kSlotShards * 16 * 4;
+__device__ inline int wave_shard() {  // the shard of this wave (global wave index)
+    return (int)((blockIdx.y * gridDim.x + blockIdx.x) * ((blockDim.x + 63) >> 6) + (threadIdx.x >> 6)) & (kSlotShards - 1);
+}
+
+// the light pdf of light triangle li at a prep state (x, N, weights_sum) -- Mylight.cpp:484-493: sum L
+// / weights_sum if li survived that prep, else 0
+__device__ inline double state_light_pdf(const DScene& S, int li, const double* st) {
+    if (li < 0 || fabs(st[6]) < MCPT_EPS) return 0.0;
+    const d3 x = mk3(st[0], st[1], st[2]), N = mk3(st[3], st[4], st[5]);
+    const PrepLight L = load_light(S, li);
+    double w_unused;
+    if (light_cheap(L.p0, L.p1, L.p2, L.nl, x, N) && light_weight(L.p0, L.p1, L.p2, L.lsum2, x, &w_unused))
+        return S.light_sum[li] / st[6];
+    return 0.0;
+}
+
+// a finished node reports radiance L -- and, when its parent code's need bit asks for it, its path-end
+// state st -- to its parent slot; the parent goes to ready list rp once both children have (one
+// append per wave: a single counter word saturates at ~88 atomics/us, MI355X_MICROARCH.md); a root
+// adds L / spp to its pixel.  Every lane of the wave that reaches the call must make it.
+__device__ inline void mis_report(const Params& P, const Slots& T, bool act, int par, int pixel, d3 L, const double* st,
+                                  int rp) {
+    bool ready = false;
+    int ps = 0;
+    if (act && par < 0) {
+        double* px = P.fb + 3 * (size_t)pixel;
+        unsafeAtomicAdd(px + 0, L.x * P.inv_spp);
+        unsafeAtomicAdd(px + 1, L.y * P.inv_spp);
+        unsafeAtomicAdd(px + 2, L.z * P.inv_spp);
+    } else if (act) {
+        ps = par >> 2;
+        const int role = (par >> 1) & 1;
+        double* dl = (role ? T.Lb : T.Ll) + 3 * (size_t)ps;
+        dl[0] = L.x, dl[1] = L.y, dl[2] = L.z;
+        if (par & 1) {
+            double* ds = T.last + 14 * (size_t)ps + 7 * role;
+#pragma unroll
+            for (int k = 0; k < 7; k++) ds[k] = st[k];
+        }
+        // the parent's fields are read by a LATER kernel (the next k_mis_complete), so kernel
+        // boundaries order these stores before those reads; only the count needs an atomic
+        ready = atomicSub(&T.pend[ps], 1) == 1;
+    }
+    const int sh = wave_shard();
+    const int q = wave_append(&T.ctrl[16 * sh + 4 + rp], ready);
+    if (ready) (rp ? T.ready1 : T.ready0)[(size_t)sh * T.ready_cap + q] = ps;
+}
+
+template <bool kStale>
 __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux A) {
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1593,11 +1691,13 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
     }
     const d3 wl = normalized(sub(coord, p));
     d3 w1 = mk3(0, 0, 0);
+    double s1 = 0;
     if (dot(wl, N) > 0) {
         flags |= 1;
         const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
         const double pp = phong_pdf(N, wl, wo, kd, ks, sh);
-        w1 = mul(hmul(tp, b), dot(wl, N) / (lprob + pp) / MCPT_P_RR);
+        s1 = dot(wl, N) / (lprob + pp) / MCPT_P_RR;
+        w1 = kStale ? b : mul(hmul(tp, b), s1);
     }
     // ---- BRDF branch (main.cpp:469-493) ----
     double pdf;
@@ -1606,13 +1706,14 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
     if (!(dot(wi, N) < 0)) {
         flags |= 2;
         if (!(fabs(wsum) < MCPT_EPS)) flags |= 4;  // light pdf can only be nonzero with a light set
-        w2 = hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh));
+        w2 = kStale ? brdf_phong(N, wi, wo, kd, ks, sh) : hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh));
     }
     A.d1[3 * i] = wl.x, A.d1[3 * i + 1] = wl.y, A.d1[3 * i + 2] = wl.z;
     A.d2[3 * i] = wi.x, A.d2[3 * i + 1] = wi.y, A.d2[3 * i + 2] = wi.z;
     A.w1[3 * i] = w1.x, A.w1[3 * i + 1] = w1.y, A.w1[3 * i + 2] = w1.z;
     A.w2[3 * i] = w2.x, A.w2[3 * i + 1] = w2.y, A.w2[3 * i + 2] = w2.z;
     A.c2[2 * i] = pdf, A.c2[2 * i + 1] = dot(wi, N);
+    if (kStale) A.s1[i] = s1;
     A.flags[i] = flags;
 }
 
@@ -1657,7 +1758,46 @@ __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, 
     }
 }
 
-__global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt) {
+// workgroup-aggregated slot allocation: ring entries freed by earlier passes first, then new
+// slots from the bump counter.  Must be called by ALL threads of the workgroup.
+__device__ inline int block_alloc_slot(const Slots& T, bool want) {
+    __shared__ unsigned s_cnt[16];
+    __shared__ unsigned s_base, s_ring, s_bump;
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    const uint64_t m = __ballot(want);
+    if (lane == 0) s_cnt[wid] = (unsigned)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot = 0;
+        for (int w = 0; w < nw; w++) {
+            const unsigned c = s_cnt[w];
+            s_cnt[w] = tot;
+            tot += c;
+        }
+        unsigned base = 0, from_ring = 0, bump = 0;
+        if (tot) {
+            unsigned* c = T.ctrl + 16 * (blockIdx.x & (kSlotShards - 1));
+            base = atomicAdd(&c[1], tot);
+            const unsigned end = c[3];
+            from_ring = base >= end ? 0u : min(tot, end - base);
+            if (tot > from_ring) bump = atomicAdd(&c[0], tot - from_ring);
+        }
+        s_base = base, s_ring = from_ring, s_bump = bump;
+    }
+    __syncthreads();
+    const uint64_t below = lane == 0 ? 0ull : (m & ((~0ull) >> (64 - lane)));
+    const unsigned j = s_cnt[wid] + (unsigned)__popcll(below);
+    const int sh = blockIdx.x & (kSlotShards - 1);
+    int slot = -1;
+    if (want)
+        slot = j < s_ring ? T.ring[(size_t)sh * T.ring_cap + (s_base + j) % (unsigned)T.ring_cap]
+                          : (int)(((s_bump + (j - s_ring)) << 5) | (unsigned)sh);
+    __syncthreads();
+    return slot;
+}
+
+template <bool kStale>
+__global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
@@ -1668,35 +1808,121 @@ __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n,
     const size_t o1 = ii, o2 = (size_t)A.cap + ii, ol = 2 * (size_t)A.cap + ii;
     const bool c1 = active && (fl & 1) && A.hf[o1] >= 0;
     const bool c2 = active && (fl & 2) && A.hf[o2] >= 0;
-    d3 tp2 = mk3(0, 0, 0);
-    if (c2) {
-        double lpdf = 0;
-        const int lf = (fl & 4) ? A.hf[ol] : -1;
-        if (lf >= 0) {
-            const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
-            const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
-            const int li = S.tri_light[lf];
-            const PrepLight L = load_light(S, li);
-            double wl_unused;
-            if (light_cheap(L.p0, L.p1, L.p2, L.nl, p, N) && light_weight(L.p0, L.p1, L.p2, L.lsum2, p, &wl_unused))
-                lpdf = S.light_sum[li] / cur.wsum[ii];  // fresh-state eval (Mylight.cpp:484-493)
-        }
-        tp2 = mul(mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]), A.c2[2 * ii + 1] / (A.c2[2 * ii] + lpdf) / MCPT_P_RR);
-    }
+    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
+    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
+    const int li = (c2 && (fl & 4) && A.hf[ol] >= 0) ? S.tri_light[A.hf[ol]] : -1;
+    const double own[7] = {p.x, p.y, p.z, N.x, N.y, N.z, cur.wsum[ii]};
     const d3 d1 = mk3(A.d1[3 * ii], A.d1[3 * ii + 1], A.d1[3 * ii + 2]);
     const d3 d2 = mk3(A.d2[3 * ii], A.d2[3 * ii + 1], A.d2[3 * ii + 2]);
-    const d3 tp1 = mk3(A.w1[3 * ii], A.w1[3 * ii + 1], A.w1[3 * ii + 2]);
-    node_entry(P, c1, c1 ? A.hf[o1] : -1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), tp1, pixel, sample, 2 * node, nxt);
-    node_entry(P, c2, c2 ? A.hf[o2] : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), tp2, pixel, sample, 2 * node + 1, nxt);
+    const d3 w1 = mk3(A.w1[3 * ii], A.w1[3 * ii + 1], A.w1[3 * ii + 2]);
+    const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
+    const double pdf = A.c2[2 * ii], cosb = A.c2[2 * ii + 1];
+    if (!kStale) {  // fresh light pdf (this node's own prep) and forward throughputs
+        d3 tp2 = mk3(0, 0, 0);
+        if (c2) tp2 = mul(w2, cosb / (pdf + state_light_pdf(S, li, own)) / MCPT_P_RR);
+        node_entry(P, c1, c1 ? A.hf[o1] : -1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), w1, pixel, sample, 2 * node, nxt);
+        node_entry(P, c2, c2 ? A.hf[o2] : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), tp2, pixel, sample,
+                   2 * node + 1, nxt);
+    } else {
+        const int f1 = c1 ? A.hf[o1] : -1, f2 = c2 ? A.hf[o2] : -1;
+        const Entry e1 = entry_eval(P, c1, f1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), pixel, sample, 2 * node);
+        const Entry e2 = entry_eval(P, c2, f2, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), pixel, sample, 2 * node + 1);
+        const bool lsh = e1.kind == 2, bsh = e2.kind == 2;
+        // light edge: an emitter child finishes it now (main.cpp:464 with the child's emission)
+        d3 Llight = mk3(0, 0, 0);
+        if (e1.kind == 1) Llight = mul(hmul(mk3(S.light_rad[3 * e1.li], S.light_rad[3 * e1.li + 1], S.light_rad[3 * e1.li + 2]), w1), A.s1[ii]);
+        // BRDF edge scalar: without a shading light child the sampler state is this node's own
+        double s2 = 0;
+        if (c2 && !lsh) s2 = cosb / (pdf + state_light_pdf(S, li, own)) / MCPT_P_RR;
+        const bool hold = lsh || bsh;
+        const int slot = block_alloc_slot(T, hold);
+        const int pc = cur.par[ii];
+        const bool need = pc >= 0 && (pc & 1);  // this subtree's path end is needed above
+        d3 Lbr = mk3(0, 0, 0);
+        if (e2.kind == 1) Lbr = mul(hmul(mk3(S.light_rad[3 * e2.li], S.light_rad[3 * e2.li + 1], S.light_rad[3 * e2.li + 2]), w2), s2);
+        // finished now (no shading child): L = L_light + L_brdf (main.cpp:493); its path end is itself
+        mis_report(P, T, active && !hold, pc, pixel, add(Llight, Lbr), own, rp);
+        if (active && hold) {
+            const size_t q = (size_t)slot;
+            T.par[q] = pc;
+            T.pix[q] = pixel;
+            T.pend[q] = (int)lsh + (int)bsh;
+            T.fl[q] = (int)lsh | ((int)bsh << 1) | ((e2.kind == 1) << 2) | ((int)c2 << 3) | ((int)need << 4);
+            T.li[q] = li;
+            double* w = T.w + 10 * q;
+            w[0] = w1.x, w[1] = w1.y, w[2] = w1.z, w[3] = A.s1[ii];
+            w[4] = w2.x, w[5] = w2.y, w[6] = w2.z, w[7] = pdf, w[8] = cosb, w[9] = s2;
+            if (!lsh) T.Ll[3 * q] = Llight.x, T.Ll[3 * q + 1] = Llight.y, T.Ll[3 * q + 2] = Llight.z;
+            if (e2.kind == 1)
+                T.Lb[3 * q] = S.light_rad[3 * e2.li], T.Lb[3 * q + 1] = S.light_rad[3 * e2.li + 1],
+                T.Lb[3 * q + 2] = S.light_rad[3 * e2.li + 2];
+        }
+        // the light child's path end is needed by this node's stale BRDF-edge pdf, and by whoever
+        // needs this node's path end when the light child is on this node's path (no shading BRDF child)
+        const bool need_l = (c2 && li >= 0) || (need && !bsh);
+        const bool need_b = need;
+        const d3 z = mk3(0, 0, 0);
+        queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt);
+        queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt);
+    }
     block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, P.stats + 3,
                 (active && c2) ? 1u : 0u);
 }
 
-// ---- shade() and shade_with_brdf nodes in the same split form (k_mis_rays traces sets 0-1 / 1) ----
-// shade: gen samples the light point (d1, its facet in hf[2 cap + i], the splat tp * L_dir / spp
-// in w1) and, after RR, the bounce (d2, the child's throughput in w2); combine splats L_dir if the
-// shadow ray's first hit is the sampled light facet (main.cpp:306-315) and spawns the bounce child
-// if it hits a non-emitter (main.cpp:335).
+// the slots whose children have all reported (ready list rp_in): L = L_light + L_brdf with the BRDF
+// edge's light pdf at the light child's path-end state, the slot goes back to the free ring, and the
+// node reports to its parent (ready list 1 - rp_in) -- one tree level per pass, in step with the
+// wavefront; grid-stride over the device-side count
+// grid: x blocks per shard, y = ready-list shard
+__global__ __launch_bounds__(256) void k_mis_complete(Params P, Slots T, int rp_in) {
+    const DScene& S = P.S;
+    const unsigned n = T.ctrl[16 * blockIdx.y + 4 + rp_in];
+    const int* ready = (rp_in ? T.ready1 : T.ready0) + (size_t)blockIdx.y * T.ready_cap;
+    const unsigned stride = gridDim.x * blockDim.x;
+    // whole waves iterate together (wave-level appends inside)
+    for (unsigned base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+        const unsigned i = base + lane_id();
+        const bool act = i < n;
+        const size_t q = act ? (size_t)ready[i] : 0;
+        const int fl = act ? T.fl[q] : 0;
+        const double* w = T.w + 10 * q;
+        const bool lsh = fl & 1, bsh = fl & 2;
+        d3 L = mk3(0, 0, 0);
+        double stc[7] = {0, 0, 0, 0, 0, 0, 0};
+        int par = -1, pix = 0;
+        if (act) {
+            const d3 Ll = mk3(T.Ll[3 * q], T.Ll[3 * q + 1], T.Ll[3 * q + 2]);
+            const d3 Llight = lsh ? mul(hmul(Ll, mk3(w[0], w[1], w[2])), w[3]) : Ll;
+            const double* last_l = T.last + 14 * q;
+            double s2 = w[9];
+            if (lsh && (fl & 8)) s2 = w[8] / (w[7] + state_light_pdf(S, T.li[q], last_l)) / MCPT_P_RR;  // stale state
+            d3 Lbr = mk3(0, 0, 0);
+            if (bsh || (fl & 4)) Lbr = mul(hmul(mk3(T.Lb[3 * q], T.Lb[3 * q + 1], T.Lb[3 * q + 2]), mk3(w[4], w[5], w[6])), s2);
+            L = add(Llight, Lbr);
+            if (fl & 16) {  // this subtree's path end, for an ancestor
+                const double* st = bsh ? last_l + 7 : last_l;
+#pragma unroll
+                for (int k = 0; k < 7; k++) stc[k] = st[k];
+            }
+            par = T.par[q];
+            pix = T.pix[q];
+        }
+        const int fs = wave_shard();
+        const int r = wave_append(&T.ctrl[16 * fs + 2], act);  // free the slot
+        if (act) T.ring[(size_t)fs * T.ring_cap + (unsigned)r % (unsigned)T.ring_cap] = (int)q;
+        mis_report(P, T, act, par, pix, L, stc, 1 - rp_in);
+    }
+}
+
+// between passes: ring entries freed so far become allocatable, unconsumed reservations are returned,
+// and the consumed ready list is emptied
+__global__ void k_slot_fixup(Slots T, int rp_consumed) {  // one thread per shard
+    unsigned* c = T.ctrl + 16 * threadIdx.x;
+    c[1] = min(c[1], c[3]);
+    c[3] = c[2];
+    c[4 + rp_consumed] = 0;
+}
+
 // first index of the running sums cum[0..n) that is >= target (n - 1 if none): the counter-RNG
 // inverse CDF, equal to the oracle's linear scan (the same running sums)
 __device__ inline int cdf_search(const double* cum, int n, double target) {
@@ -1957,7 +2183,7 @@ struct DeviceState {
     std::vector<void*> allocs;
     hipStream_t stream = nullptr;
     // reusable work buffers
-    DevBuf hit_f, hit_tbg, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[8], cache_bt, cache_lst, cache_info, cache_w, masks;
+    DevBuf hit_f, hit_tbg, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[9], sl[13], cache_bt, cache_lst, cache_info, cache_w, masks;
     int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
@@ -2154,7 +2380,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, lb4, &d.lbvh4))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
-    HIP_OK(hipHostMalloc(&D->pinned_count, 64));
+    HIP_OK(hipHostMalloc(&D->pinned_count, 64 + kCtrlBytes));
     HIP_OK(hipEventCreate(&D->ev0));
     HIP_OK(hipEventCreate(&D->ev1));
     HIP_OK(hipEventCreate(&D->evp0));
@@ -2168,8 +2394,8 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
 
 int alloc_aux(DevBuf* b, int cap, Aux& a) {
     const size_t c = (size_t)cap;
-    const size_t sz[8] = {24 * c, 24 * c, 24 * c, 24 * c, 16 * c, 2 * 16 * c, 4 * c, 3 * 4 * c};
-    for (int k = 0; k < 8; k++) {
+    const size_t sz[9] = {24 * c, 24 * c, 24 * c, 24 * c, 16 * c, 2 * 16 * c, 4 * c, 3 * 4 * c, 8 * c};
+    for (int k = 0; k < 9; k++) {
         int rc = ensure(b[k], sz[k]);
         if (rc) return rc;
     }
@@ -2181,14 +2407,87 @@ int alloc_aux(DevBuf* b, int cap, Aux& a) {
     a.hbg = (double*)b[5].p;
     a.flags = (int*)b[6].p;
     a.hf = (int*)b[7].p;
+    a.s1 = (double*)b[8].p;
     a.cap = cap;
+    return MCPT_OK;
+}
+
+// the MIS tree-reduction slot pool (Slots): per-slot arrays, per-shard free rings and ready lists,
+// control words.  grow = true keeps the contents of a smaller pool (called between passes, stream
+// idle: each shard's ring entries [head, tail) are re-packed from 0, its ready list rp keeps its
+// entries; slot ids stay valid).
+constexpr int kSlotArrays = 13;
+int slot_bytes_per(int k) {  // par pix pend fl li | w Ll Lb last
+    static const int b[9] = {4, 4, 4, 4, 4, 80, 24, 24, 112};
+    return b[k];
+}
+size_t slot_array_bytes(int k, int rcap) {
+    const size_t cap = (size_t)rcap * kSlotShards;
+    if (k < 9) return (size_t)slot_bytes_per(k) * cap;
+    if (k == 9) return 4 * cap * kSlotShards;                    // rings: cap entries per shard
+    if (k < 12) return 4ull * kSlotShards * (2ull * rcap + 256);  // ready lists
+    return kCtrlBytes;
+}
+void slots_view(DevBuf* b, int rcap, Slots& T) {
+    T.par = (int*)b[0].p, T.pix = (int*)b[1].p, T.pend = (int*)b[2].p, T.fl = (int*)b[3].p, T.li = (int*)b[4].p;
+    T.w = (double*)b[5].p, T.Ll = (double*)b[6].p, T.Lb = (double*)b[7].p, T.last = (double*)b[8].p;
+    T.ring = (int*)b[9].p, T.ready0 = (int*)b[10].p, T.ready1 = (int*)b[11].p, T.ctrl = (unsigned*)b[12].p;
+    T.rcap = rcap;
+    T.cap = rcap * kSlotShards;
+    T.ring_cap = T.cap;
+    T.ready_cap = 2 * rcap + 256;
+}
+int alloc_slots(DevBuf* b, int rcap, Slots& T, hipStream_t st, bool grow, int rp, const unsigned* ctrl_host) {
+    if (!grow) {
+        for (int k = 0; k < kSlotArrays; k++) {
+            int rc = ensure(b[k], slot_array_bytes(k, rcap));
+            if (rc) return rc;
+        }
+        slots_view(b, rcap, T);
+        HIP_OK(hipMemsetAsync(T.ctrl, 0, kCtrlBytes, st));
+        return MCPT_OK;
+    }
+    const Slots old = T;
+    DevBuf nb[kSlotArrays];
+    for (int k = 0; k < kSlotArrays; k++) {
+        int rc = ensure(nb[k], slot_array_bytes(k, rcap));
+        if (rc) return rc;
+    }
+    Slots nt{};
+    slots_view(nb, rcap, nt);
+    for (int k = 0; k < 9; k++)  // per-slot data keep their slot ids
+        HIP_OK(hipMemcpyAsync(nb[k].p, b[k].p, (size_t)slot_bytes_per(k) * old.cap, hipMemcpyDeviceToDevice, st));
+    std::vector<unsigned> c(kSlotShards * 16, 0u);
+    for (int sh = 0; sh < kSlotShards; sh++) {
+        const unsigned* oc = ctrl_host + 16 * sh;
+        const unsigned head = oc[1], nfree = oc[2] - oc[1], nready = oc[4 + rp];
+        for (unsigned k = 0; k < nfree;) {  // this shard's ring, in contiguous pieces of the old circle
+            const unsigned from = (head + k) % (unsigned)old.ring_cap, len = std::min(nfree - k, (unsigned)old.ring_cap - from);
+            HIP_OK(hipMemcpyAsync(nt.ring + (size_t)sh * nt.ring_cap + k, old.ring + (size_t)sh * old.ring_cap + from, 4ull * len,
+                                  hipMemcpyDeviceToDevice, st));
+            k += len;
+        }
+        if (nready)
+            HIP_OK(hipMemcpyAsync((rp ? nt.ready1 : nt.ready0) + (size_t)sh * nt.ready_cap,
+                                  (rp ? old.ready1 : old.ready0) + (size_t)sh * old.ready_cap, 4ull * nready,
+                                  hipMemcpyDeviceToDevice, st));
+        unsigned* w = &c[16 * sh];
+        w[0] = oc[0], w[1] = 0, w[2] = nfree, w[3] = nfree, w[4 + rp] = nready;
+    }
+    HIP_OK(hipMemcpyAsync(nt.ctrl, c.data(), kCtrlBytes, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (int k = 0; k < kSlotArrays; k++) {
+        if (b[k].p) HIP_OK(hipFree(b[k].p));
+        b[k] = nb[k];
+    }
+    T = nt;
     return MCPT_OK;
 }
 
 int alloc_queue(DevBuf* b, int cap, Queue& q) {
     const size_t c = (size_t)cap;
-    const size_t sz[14] = {24 * c, 24 * c, 24 * c, 24 * c, 4 * c, 4 * c, 4 * c, 8 * c, 8 * c, 4 * c, 64, 0, 0, 0};
-    for (int k = 0; k < 11; k++) {
+    const size_t sz[14] = {24 * c, 24 * c, 24 * c, 24 * c, 4 * c, 4 * c, 4 * c, 8 * c, 8 * c, 4 * c, 64, 4 * c, 0, 0};
+    for (int k = 0; k < 12; k++) {
         int rc = ensure(b[k], sz[k]);
         if (rc) return rc;
     }
@@ -2203,6 +2502,7 @@ int alloc_queue(DevBuf* b, int cap, Queue& q) {
     q.wsum = (double*)b[8].p;
     q.pick = (int*)b[9].p;
     q.count = (unsigned*)b[10].p;
+    q.par = (int*)b[11].p;
     q.cap = cap;
     return MCPT_OK;
 }
@@ -2348,7 +2648,14 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const bool fused = !grid && o->mode == MCPT_MODE_BRDF && !split_brdf;  // BRDF-only: k_extend_brdf (the grid runs split)
     Aux aux{};
     if (!fused && (rc = alloc_aux(D.aux, cap, aux))) return rc;
+    // shade_with_mis reduces its trees bottom-up to evaluate the BRDF branch's light pdf with the
+    // reference's (stale) sampler state, unless MCPT_RENDER_FRESH_PDF asks for the node's own
+    const bool stale = o->mode == MCPT_MODE_MIS && !(o->flags & MCPT_RENDER_FRESH_PDF);
+    Slots T{};
+    int rp = 0;  // ready list being filled
+    const unsigned* hctrl = D.pinned_count + 16;  // slot control words, read back with the queue count
     hipStream_t st = D.stream;
+    if (stale && (rc = alloc_slots(D.sl, std::max(cap, 1 << 16) / kSlotShards + 1, T, st, false, 0, nullptr))) return rc;
     Params P;
     P.S = D.d;
     P.seed = o->seed;
@@ -2362,8 +2669,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
         return MCPT_E_SCENE;
     }
-    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE |
-                     MCPT_DEBUG_COUNT_TRAVERSAL)) {
+    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_DEBUG_SPLIT_BRDF |
+                     MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
@@ -2475,6 +2782,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     auto read_count = [&](unsigned* out) -> int {  // cur's node count; fails on a queue overflow
         HIP_OK(hipMemcpyAsync(D.pinned_count, cur->count, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipMemcpyAsync(D.pinned_count + 2, (char*)D.stats.p + 32, 8, hipMemcpyDeviceToHost, st));
+        if (stale) HIP_OK(hipMemcpyAsync(D.pinned_count + 16, T.ctrl, kCtrlBytes, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         if (*(unsigned long long*)(D.pinned_count + 2)) {
             set_error("wavefront queue overflow (capacity %d); raise queue_factor", cap);
@@ -2516,6 +2824,19 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             if (rnext >= R && spill_n == 0) break;
             continue;  // every root of the refill terminated at entry: refill again
         }
+        if (stale) {  // a shard serves at most ceil(blocks / 32) workgroups of 256 nodes per generation
+            const unsigned per_shard = ((n + 255) / 256 + kSlotShards - 1) / kSlotShards * 256;
+            unsigned bump = 0;
+            for (int sh = 0; sh < kSlotShards; sh++) bump = std::max(bump, hctrl[16 * sh]);
+            if (bump + per_shard > (unsigned)T.rcap) {
+                const long long nr = std::max<long long>(2ll * T.rcap, (long long)bump + per_shard + 4096);
+                if (nr * kSlotShards > (1ll << 30)) {
+                    set_error("MIS reduction slot pool beyond 2^30 slots");
+                    return MCPT_E_DEVICE;
+                }
+                if ((rc = alloc_slots(D.sl, (int)nr, T, st, true, rp, hctrl))) return rc;
+            }
+        }
         gens++;
         nodes_total += (uint64_t)n;
         const int ni = (int)n;
@@ -2554,12 +2875,18 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
         // trace_seconds: HIP events around the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf)
         if (!fused && o->mode == MCPT_MODE_MIS) {
-            hipLaunchKernelGGL(k_mis_gen, g256, b256, 0, st, P, *cur, ni, aux);
+            hipLaunchKernelGGL(stale ? k_mis_gen<true> : k_mis_gen<false>, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 3), dim3(kRayBlock), 0, st, D.d, *cur,
                                ni, aux, 0, tcnt);
             HIP_OK(hipEventRecord(D.evr1, st));
-            hipLaunchKernelGGL(k_mis_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
+            hipLaunchKernelGGL(stale ? k_mis_combine<true> : k_mis_combine<false>, g256, b256, 0, st, P, *cur, ni, aux,
+                               *nxt, T, rp);
+            if (stale) {  // one level of the bottom-up reduction per generation
+                hipLaunchKernelGGL(k_mis_complete, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
+                hipLaunchKernelGGL(k_slot_fixup, dim3(1), dim3(kSlotShards), 0, st, T, rp);
+                rp ^= 1;
+            }
         } else if (!fused && (o->mode == MCPT_MODE_SHADE || o->mode == MCPT_MODE_SHADE_AREA)) {
             hipLaunchKernelGGL(k_shade_gen, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
@@ -2600,6 +2927,16 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             set_error("render cancelled by the progress callback after %lld of %lld camera samples", rnext, R);
             return MCPT_E_CANCELLED;
         }
+    }
+    while (stale) {  // drain the reduction: the trees' remaining levels up to their roots
+        HIP_OK(hipMemcpyAsync(D.pinned_count + 16, T.ctrl, kCtrlBytes, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        unsigned pending = 0;
+        for (int sh = 0; sh < kSlotShards; sh++) pending += hctrl[16 * sh + 4 + rp];
+        if (pending == 0) break;
+        hipLaunchKernelGGL(k_mis_complete, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
+        hipLaunchKernelGGL(k_slot_fixup, dim3(1), dim3(kSlotShards), 0, st, T, rp);
+        rp ^= 1;
     }
     HIP_OK(hipEventRecord(D.ev1, st));
     HIP_OK(hipEventSynchronize(D.ev1));
@@ -3015,7 +3352,8 @@ void mcpt_scene_destroy(mcpt_scene* sc) {
         std::vector<DevBuf*> bufs = {&D->hit_f, &D->hit_tbg, &D->fb, &D->rank_fb, &D->stats, &D->work, &D->cache_bt, &D->cache_lst,
                                      &D->cache_info, &D->cache_w, &D->masks, &D->g_start, &D->g_tri};
         for (int k = 0; k < 14; k++) bufs.insert(bufs.end(), {&D->qa[k], &D->qb[k], &D->qs[k]});
-        for (int k = 0; k < 8; k++) bufs.push_back(&D->aux[k]);
+        for (int k = 0; k < 9; k++) bufs.push_back(&D->aux[k]);
+        for (int k = 0; k < 13; k++) bufs.push_back(&D->sl[k]);
         for (DevBuf* b : bufs)
             if (b->p) (void)hipFree(b->p);
         if (D->pinned_count) (void)hipHostFree(D->pinned_count);

@@ -1106,7 +1106,7 @@ typedef struct {
     light_state L;    /* RefRng: the global Mylight member state (stale-pdf quirk) */
     uint64_t stats[4]; /* shading nodes, light preps, extension rays, light-only rays */
     int area_lights;  /* shade(): select_a_point_from_lights instead of the spherical sampler */
-    int stale_pdf;    /* counter RNG with the reference's stale light pdf (ORC_FLAG_STALE_PDF) */
+    int fresh_pdf;    /* counter RNG with the node's own light pdf (ORC_FLAG_FRESH_PDF) */
 } ctx;
 
 /* discrete_distribution over w[0..n) as libstdc++ (random.tcc): fewer than two weights -> index 0,
@@ -1293,7 +1293,7 @@ static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t no
         int lg = grid_trace(s, p, wi, f, 1, &hl);
         if (lg >= 0) {
             int li = s->light_of[lg];
-            if (C->rng == ORC_RNG_REF || C->stale_pdf) {  /* stale state, as the reference (Mylight.cpp:484-493) */
+            if (!C->fresh_pdf) {  /* stale state, as the reference (Mylight.cpp:484-493) */
                 if (C->L.member[li] == C->L.gen && !(fabs(C->L.wsum) < EPS)) light_pdf = s->lsum[li] / C->L.wsum;
             } else {                       /* fresh: this node's own prep */
                 if (!(fabs(wsum_here) < EPS) && light_tri_eval(s, li, p, N, NULL)) light_pdf = s->lsum[li] / wsum_here;
@@ -1408,7 +1408,7 @@ static v3 shade_direct(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t
 }
 
 static v3 shade_root(ctx* C, int mode, int f, double beta, double gamma, v3 wo) {
-    C->stale_pdf = (mode & ORC_FLAG_STALE_PDF) != 0;
+    C->fresh_pdf = C->rng == ORC_RNG_COUNTER && (mode & ORC_FLAG_FRESH_PDF) != 0;
     mode &= 0xff;
     if (mode == ORC_MODE_MIS) return shade_mis(C, f, beta, gamma, wo, 1);
     C->area_lights = mode == ORC_MODE_SHADE_AREA;

@@ -28,12 +28,12 @@ typedef struct orc_scene orc_scene;
 /* main.cpp:402 / :348 / :269; SHADE_AREA = shade() with the uniform-area light sampler
  * select_a_point_from_lights (Mylight.cpp:102-160, the alternative commented out at main.cpp:296) */
 enum { ORC_MODE_MIS = 0, ORC_MODE_BRDF = 1, ORC_MODE_SHADE = 2, ORC_MODE_SHADE_AREA = 3 };
-/* or-ed into the mode of orc_render / orc_shade_sample with the counter RNG: shade_with_mis evaluates
- * the BRDF branch's light pdf with the light-sampler state the LAST prep left, after the light
- * branch's recursion (main.cpp:443 vs :487, Mylight.cpp:484-493) -- the reference's stale-pdf quirk,
- * which the RefRng replay always has -- instead of the node's own prep.  Quantifies the quirk the
- * GPU path (fresh semantics) leaves out (tools/stale_pdf_delta.py). */
-enum { ORC_FLAG_STALE_PDF = 0x100 };
+/* With the counter RNG, shade_with_mis evaluates the BRDF branch's light pdf like the reference:
+ * with the light-sampler state the LAST prep left, after the light branch's recursion (main.cpp:443
+ * vs :487, Mylight.cpp:484-493 -- the "stale-pdf" behaviour, which the RefRng replay has too).
+ * ORC_FLAG_FRESH_PDF, or-ed into the mode, uses the node's own prep instead (a fix of the
+ * reference; tools/stale_pdf_delta.py measures the difference). */
+enum { ORC_FLAG_FRESH_PDF = 0x200 };
 enum { ORC_RNG_REF = 0, ORC_RNG_COUNTER = 1 };
 
 /* camera: eye, lookat, up, fovy parameter (the reference's tan(fovy/360) quirk), eye pull-back

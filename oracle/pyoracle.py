@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 MODE_MIS, MODE_BRDF, MODE_SHADE, MODE_SHADE_AREA = 0, 1, 2, 3  # ORC_MODE_* (mcpt_oracle.h)
-FLAG_STALE_PDF = 0x100  # ORC_FLAG_STALE_PDF: or into MODE_MIS for the reference's stale light pdf (counter RNG)
+FLAG_FRESH_PDF = 0x200  # ORC_FLAG_FRESH_PDF: or into MODE_MIS for the node's own light pdf instead of the reference's stale one
 RNG_REF, RNG_COUNTER = 0, 1
 
 

@@ -165,6 +165,25 @@ def test_render_parity_full_size_pixel_subset(scene, oscene, mode, spp):
     assert g.mean() > 0
 
 
+@pytest.mark.parametrize("W,H,spp", [(80, 60, 8), (800, 600, 16)])
+def test_mis_fresh_pdf_flag_vs_oracle(scene, oscene, W, H, spp):
+    """MCPT_RENDER_FRESH_PDF (the node's own light pdf, not the reference's stale sampler state,
+    main.cpp:443 vs :487) against the oracle's ORC_FLAG_FRESH_PDF; the default (stale) render must
+    differ from it where light branches recurse"""
+    cam = mcpt.Camera.reference(W, H)
+    g, _ = mcpt.render(scene, cam, spp, mode="mis", seed=SEED, flags=mcpt.RENDER_FRESH_PDF)
+    stride = 1 if W < 200 else 20
+    off = 0 if stride == 1 else 7
+    c, _ = oscene.render(po.reference_camera(W, H), po.MODE_MIS | po.FLAG_FRESH_PDF, SEED, spp, stride=stride,
+                         offset=off, nthreads=8)
+    sub = (slice(off, None, stride), slice(off, None, stride))
+    err, mx = rel_l2(g[sub], c[sub]), max_px_rel(g[sub], c[sub])
+    print("fresh-pdf MIS %dx%dx%d rel L2 %.3e, max per-pixel %.3e" % (W, H, spp, err, mx))
+    assert err <= L2_TOL and mx <= L2_TOL
+    d, _ = mcpt.render(scene, cam, spp, mode="mis", seed=SEED)
+    assert rel_l2(d[sub], g[sub]) > 1e-9
+
+
 def test_sample_range_split_is_invariant(scene):
     """Sharding by sample range (multi-GPU, sequential calls) gives the same frame up to fp64 order."""
     cam = mcpt.Camera.reference(64, 48)
@@ -233,7 +252,7 @@ def test_no_backface_stats_flag(scene, small_lights, tmp_path):
     for k in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays"):
         assert a[k] == b[k], k
     with pytest.raises(mcpt.MCPTError, match="flags"):
-        mcpt.render_device(scene, cam, 8, fb.data_ptr(), seed=SEED, device=dev, flags=2)
+        mcpt.render_device(scene, cam, 8, fb.data_ptr(), seed=SEED, device=dev, flags=1 << 12)
 
 
 def test_progress_callback_and_cancel(scene):

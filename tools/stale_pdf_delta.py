@@ -3,7 +3,8 @@
 item 5).  shade_with_mis evaluates the BRDF branch's light pdf after the light branch's recursion
 has overwritten the light sampler's members (main.cpp:443 vs :487, Mylight.cpp:484-493); the GPU
 path uses the node's own prep (fresh).  The oracle renders the same pixels and samples with the same
-counter RNG both ways (ORC_FLAG_STALE_PDF), so the difference is the quirk alone.
+counter RNG both ways (default = the reference's stale state; ORC_FLAG_FRESH_PDF), so the
+difference is the quirk alone.
 
     python tools/stale_pdf_delta.py [--spp 1024 --threads 8]   -> profiles/stale_pdf_delta.json
 """
@@ -36,9 +37,9 @@ def main():
     s.build_grid(e)
     off = 7
     t = time.perf_counter()
-    fresh, _ = s.render(cam, po.MODE_MIS, a.seed, a.spp, stride=a.stride, offset=off, nthreads=a.threads)
-    stale, _ = s.render(cam, po.MODE_MIS | po.FLAG_STALE_PDF, a.seed, a.spp, stride=a.stride, offset=off,
+    fresh, _ = s.render(cam, po.MODE_MIS | po.FLAG_FRESH_PDF, a.seed, a.spp, stride=a.stride, offset=off,
                         nthreads=a.threads)
+    stale, _ = s.render(cam, po.MODE_MIS, a.seed, a.spp, stride=a.stride, offset=off, nthreads=a.threads)
     dt = time.perf_counter() - t
     sub = (slice(off, None, a.stride), slice(off, None, a.stride))
     f, g = fresh[sub], stale[sub]
@@ -56,7 +57,7 @@ def main():
         "max_pixel_rel": float(np.max(np.where(npx > 0, dpx / np.maximum(npx, 1e-300), 0.0))),
         "north_star_tolerance": 1e-3,
         "seconds": round(dt, 1),
-        "method": "tools/stale_pdf_delta.py (oracle/liboracle.so, ORC_FLAG_STALE_PDF)",
+        "method": "tools/stale_pdf_delta.py (oracle/liboracle.so, default vs ORC_FLAG_FRESH_PDF)",
     }
     out["within_tolerance"] = out["rel_l2_stale_vs_fresh"] <= 1e-3
     print(json.dumps(out, indent=1))
