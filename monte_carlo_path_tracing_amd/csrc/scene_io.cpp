@@ -37,6 +37,13 @@ bool read_text(const std::string& path, std::string& out) {
 
 // tinyobjloader's decimal parser: integer digits accumulated in a double, fraction digits
 // added as digit * 10^-k (table for k < 8), exponent applied as ldexp(m * 5^e, e).
+// A restructured restatement of tinyobjloader's tryParseDouble (tiny_obj_loader.h:897-1028, as
+// vendored by the reference), kept so that vertices parse to the reference's exact floats.
+// tinyobjloader: The MIT License (MIT), Copyright (c) 2012-Present, Syoyo Fujita and many
+// contributors.  Permission is hereby granted, free of charge, to any person obtaining a copy of
+// that software and associated documentation files, to deal in the Software without restriction,
+// subject to including the copyright notice and permission notice in all copies or substantial
+// portions of the Software; it is provided "AS IS", without warranty of any kind.
 bool parse_decimal(const char* s, const char* e, double* result) {
     static const double kFrac[] = {1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001};
     if (s >= e) return false;

@@ -1,0 +1,55 @@
+"""Config C1 of BASELINE.json -- the Veach-MIS frame at 400x300 @ 4 spp, the reference's CPU path
+(main.cpp:547-596: render, tone map 380 / 0.25, BMP) -- end to end:
+  * CPU (no GPU): the oracle renders the whole C1 frame (MIS and BRDF-only) and the C ABI's tone
+    map + BMP writer (RadianceRGB.cpp:51-67, main.cpp:583-596) turn it into the reference's 32-bpp
+    bottom-up BMP;
+  * GPU: the HIP path renders the same frame, which must equal the oracle's to <= 1e-3 relative L2
+    and per pixel (north-star tolerance; measured ~1e-11)."""
+import numpy as np
+import pytest
+
+from conftest import SCENE_OBJ, SCENE_XML
+import monte_carlo_path_tracing_amd as mcpt
+from oracle import pyoracle as po
+
+W, H, SPP, SEED = 400, 300, 4, 20240430
+OMODE = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF}
+
+
+def oracle_c1(mode):
+    s = po.Scene(SCENE_OBJ, SCENE_XML)
+    cam = po.reference_camera(W, H)
+    e, _ = po.camera_ray(cam, 0, 0)
+    s.build_grid(e)
+    img, st = s.render(cam, OMODE[mode], SEED, SPP, nthreads=8)
+    return img, st
+
+
+@pytest.mark.parametrize("mode", ["mis", "brdf"])
+def test_c1_cpu_path_to_bmp(tmp_path, mode):
+    img, st = oracle_c1(mode)
+    assert np.isfinite(img).all() and (img >= 0).all() and img.mean() > 0
+    assert st[0] > W * H  # shading nodes: the frame really was path traced
+    rgb8 = mcpt.tone_map(img)
+    assert np.array_equal(rgb8[..., 0].astype(np.int64), np.array([po.tone_map(v) for v in img.reshape(-1, 3)])[:, 0].reshape(H, W))
+    path = tmp_path / ("c1_%s.bmp" % mode)
+    mcpt.write_bmp(str(path), rgb8)
+    raw = path.read_bytes()
+    assert raw[:2] == b"BM" and len(raw) == 54 + 4 * W * H
+    # bottom-up rows, BGRA: the first stored pixel is the bottom-left image pixel
+    assert tuple(raw[54:57]) == tuple(int(x) for x in rgb8[H - 1, 0, ::-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["mis", "brdf"])
+def test_c1_gpu_equals_cpu_path(mode):
+    ref, _ = oracle_c1(mode)
+    scene = mcpt.Scene.load(SCENE_OBJ, SCENE_XML)
+    img, st = mcpt.render(scene, mcpt.Camera.reference(W, H), SPP, mode=mode, seed=SEED)
+    err = float(np.linalg.norm(img - ref) / np.linalg.norm(ref))
+    d = np.linalg.norm((img - ref).reshape(-1, 3), axis=1)
+    n = np.linalg.norm(ref.reshape(-1, 3), axis=1)
+    mx = float(np.max(np.where(n > 0, d / np.maximum(n, 1e-300), np.where(d > 0, np.inf, 0.0))))
+    print("C1 %s 400x300x4: rel L2 %.3e, max per-pixel %.3e" % (mode, err, mx))
+    assert err <= 1e-3 and mx <= 1e-3
+    assert np.array_equal(mcpt.tone_map(img), mcpt.tone_map(ref)) or np.mean(mcpt.tone_map(img) != mcpt.tone_map(ref)) < 1e-4
