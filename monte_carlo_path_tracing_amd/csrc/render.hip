@@ -78,8 +78,9 @@ struct DScene {
     const double2* lt_w;      // NL*5: p0, p1, p2 (fp64), 2 RadianceRGB::sum()
     const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
-    const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves)
+    const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves), breadth-first node order
     const BvhNode4* lbvh4;
+    int nbvh4, nlbvh4;        // node counts
     const float4* lleaf_v;
     // select_a_point_from_lights (MCPT_MODE_SHADE_AREA): the lightsRadiance map in name order --
     // RadianceRGB::sum() per light and its running sum, the light-table run of its triangles -- and
@@ -142,6 +143,16 @@ constexpr int kStack = 48;
 constexpr int kLeafBits = 5;  // leaf code ~((first slot << kLeafBits) | count)
 constexpr int kRayBlock = 256;
 constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB per 256 lanes)
+// k_mis_rays: the first kRayTop nodes of the traversed BVH4 (breadth-first numbering: its top
+// levels) staged in LDS per workgroup; 0 = off.  A/B builds: -DMCPT_RAY_TOP=N -DMCPT_RAY_LDS=M.
+#ifndef MCPT_RAY_TOP
+#define MCPT_RAY_TOP 0
+#endif
+#ifndef MCPT_RAY_LDS
+#define MCPT_RAY_LDS 16
+#endif
+constexpr int kRayTop = MCPT_RAY_TOP;
+constexpr int kRayTopLds = MCPT_RAY_LDS;
 constexpr int kTraceBlock = 128;
 
 struct Hit {
@@ -165,10 +176,12 @@ struct Hit {
 //    to the lower facet id.
 // kCount: also count node visits and triangle tests into *visits / *tests (the traversal roofline's
 // events; only the untimed statistics replay instantiates it)
-template <int kLds, bool kCount = false>
+// kTop > 0: nodes [0, kTop) are read from `top` (an LDS copy of the tree's top levels) through a
+// generic pointer, the rest from `nodes`
+template <int kLds, bool kCount = false, int kTop = 0>
 __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
                                 int exclude, int* __restrict__ lds, int stride, unsigned* visits = nullptr,
-                                unsigned* tests = nullptr) {
+                                unsigned* tests = nullptr, const BvhNode4* top = nullptr) {
     constexpr int kDone = 0x7fffffff;
     Hit best{-1, DBL_MAX, 0, 0};
     if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
@@ -197,7 +210,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     while (node != kDone || leaf < 0) {
         while (node >= 0 && node != kDone) {
             if (kCount) ++*visits;
-            const BvhNode4* nd = nodes + node;
+            const BvhNode4* nd = (kTop > 0 && node < kTop) ? top + node : nodes + node;
             const float4 lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
                          lz = *reinterpret_cast<const float4*>(nd->lo[2]);
             const float4 hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
@@ -1723,9 +1736,18 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 template <bool kGrid, bool kCount = false>
 __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set,
                                                           unsigned long long* cnt = nullptr) {
-    __shared__ int stack[kRayLds * kRayBlock];
+    constexpr int kTop = kGrid ? 0 : kRayTop;
+    __shared__ int stack[kRayTopLds * kRayBlock];
+    __shared__ BvhNode4 top[kTop > 0 ? kTop : 1];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int set = blockIdx.y + first_set;
+    if (kTop > 0) {  // the tree's top levels into LDS (uniform per block: blockIdx.y picks the tree)
+        const BvhNode4* src = set == 2 ? S.lbvh4 : S.bvh4;
+        const int cnt4 = min(kTop, set == 2 ? S.nlbvh4 : S.nbvh4) * (int)(sizeof(BvhNode4) / sizeof(float4));
+        for (int k = threadIdx.x; k < cnt4; k += blockDim.x)
+            reinterpret_cast<float4*>(top)[k] = reinterpret_cast<const float4*>(src)[k];
+        __syncthreads();
+    }
     if (!kCount && i >= n) return;
     const int fl = i < n ? A.flags[i] : 0;
     int f = -1;
@@ -1740,8 +1762,8 @@ __global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, 
         if (kGrid)
             h = grid_trace(S, ro, rd, cur.f[i], set == 2);
         else
-            h = trace4_ww<kRayLds, kCount>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i], stack + threadIdx.x,
-                                           kRayBlock, &visits, &tests);
+            h = trace4_ww<kRayTopLds, kCount, kTop>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
+                                                    stack + threadIdx.x, kRayBlock, &visits, &tests, top);
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
@@ -2225,6 +2247,33 @@ int upload(DeviceState& D, const std::vector<T>& v, const T** out) {
     return MCPT_OK;
 }
 
+// renumbers a 4-wide BVH breadth-first (root 0, then each level in order), so the first nodes are
+// its top levels (k_mis_rays stages them in LDS); inner-child indices are remapped
+std::vector<BvhNode4> bfs_order(const std::vector<BvhNode4>& in) {
+    if (in.empty()) return in;
+    std::vector<int32_t> order, newidx(in.size(), -1);
+    order.reserve(in.size());
+    order.push_back(0);
+    newidx[0] = 0;
+    for (size_t h = 0; h < order.size(); h++)
+        for (int k = 0; k < 4; k++) {
+            const int32_t c = in[order[h]].child[k];
+            if (c >= 0 && c != kBvh4Empty && newidx[c] < 0) {
+                newidx[c] = (int32_t)order.size();
+                order.push_back(c);
+            }
+        }
+    std::vector<BvhNode4> out(order.size());
+    for (size_t h = 0; h < order.size(); h++) {
+        out[h] = in[order[h]];
+        for (int k = 0; k < 4; k++) {
+            const int32_t c = out[h].child[k];
+            if (c >= 0 && c != kBvh4Empty) out[h].child[k] = newidx[c];
+        }
+    }
+    return out;
+}
+
 // leaf children as the traversal stack code ~((first leaf slot << 3) | count), so a node visit needs
 // no count load or decode (trace4_ww)
 int pack_leaf_codes(std::vector<BvhNode4>& nodes) {
@@ -2374,8 +2423,10 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, ld, &d.lt_d))) return rc;
     if ((rc = upload(*D, lw, &d.lt_w))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
-    std::vector<BvhNode4> b4 = collapse_bvh4(sc->bvh), lb4 = collapse_bvh4(sc->lbvh);
+    std::vector<BvhNode4> b4 = bfs_order(collapse_bvh4(sc->bvh)), lb4 = bfs_order(collapse_bvh4(sc->lbvh));
     if ((rc = pack_leaf_codes(b4)) || (rc = pack_leaf_codes(lb4))) return rc;
+    d.nbvh4 = (int)b4.size();
+    d.nlbvh4 = (int)lb4.size();
     if ((rc = upload(*D, b4, &d.bvh4))) return rc;
     if ((rc = upload(*D, lb4, &d.lbvh4))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
