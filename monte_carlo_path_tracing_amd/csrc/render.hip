@@ -1628,14 +1628,17 @@ __device__ inline int wave_shard() {  // the shard of this wave (global wave ind
 }
 
 // the light pdf of light triangle li at a prep state (x, N, weights_sum) -- Mylight.cpp:484-493: sum L
-// / weights_sum if li survived that prep, else 0
+// / weights_sum if li survived that prep, else 0.  Survival by the reference's literal cull chain
+// (light_tri_eval: acos-based edge and vertex angles, alpha + beta + gamma - pi >= 0), not the
+// prep's Van Oosterom-Strackee form: the two agree except on spherical triangles of ~zero area
+// (seen edge-on, e.g. on a sphere light's silhouette), whose weight is negligible in weights_sum but
+// whose survival decides whether this pdf is sum L / weights_sum or 0 -- one triangle per node, so
+// the exact chain is cheap here.
 __device__ inline double state_light_pdf(const DScene& S, int li, const double* st) {
     if (li < 0 || fabs(st[6]) < MCPT_EPS) return 0.0;
     const d3 x = mk3(st[0], st[1], st[2]), N = mk3(st[3], st[4], st[5]);
     const PrepLight L = load_light(S, li);
-    double w_unused;
-    if (light_cheap(L.p0, L.p1, L.p2, L.nl, x, N) && light_weight(L.p0, L.p1, L.p2, L.lsum2, x, &w_unused))
-        return S.light_sum[li] / st[6];
+    if (light_tri_eval(L.p0, L.p1, L.p2, L.nl, S.light_sum[li], x, N, nullptr)) return S.light_sum[li] / st[6];
     return 0.0;
 }
 
@@ -1671,6 +1674,8 @@ __device__ inline void mis_report(const Params& P, const Slots& T, bool act, int
     if (ready) (rp ? T.ready1 : T.ready0)[(size_t)sh * T.ready_cap + q] = ps;
 }
 
+// kStale: the tree-reduction form (Slots) -- w1 / w2 hold the edges' BRDF values and s1 the light
+// edge's scalar, applied bottom-up; else w1 / w2 are forward throughputs (fresh-pdf path)
 template <bool kStale>
 __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux A) {
     const DScene& S = P.S;

@@ -1210,6 +1210,11 @@ static v3 shade_brdf(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t n
     return vmul(rgb_mul(Li, brdf), vdot(wi, N) / pdf / P_RR);
 }
 
+/* debugging aid (orc_debug_mis_sample): per-node records of one camera sample's MIS tree */
+enum { DBG_REC = 20 };
+static __thread double* g_dbg;
+static __thread int g_dbg_n, g_dbg_cap;
+
 static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t node) {
     const orc_scene* s = C->s;
     if (C->rng == ORC_RNG_COUNTER && node >= ((uint64_t)2 << COUNTER_MAX_DEPTH)) return mk(0, 0, 0); /* heap id */
@@ -1257,7 +1262,16 @@ static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t no
             k1 = counter_u(key, 2);
             k2 = counter_u(key, 3);
         }
-        light_sample_after_pick(s, &C->L, rind, p, k1, k2, &coord, &lprob);
+        const int li_pick = light_sample_after_pick(s, &C->L, rind, p, k1, k2, &coord, &lprob);
+        if (g_dbg && g_dbg_n < g_dbg_cap) g_dbg[DBG_REC * g_dbg_n + 9] = li_pick;
+    }
+    int dbg_slot = -1;
+    if (g_dbg && g_dbg_n < g_dbg_cap) {
+        dbg_slot = g_dbg_n++;
+        double* r = g_dbg + DBG_REC * dbg_slot;
+        r[0] = (double)node, r[1] = f, r[2] = p.x, r[3] = p.y, r[4] = p.z, r[5] = N.x, r[6] = N.y, r[7] = N.z;
+        r[8] = wsum_here, r[10] = lprob;
+        if (C->L.count == 0 || fabs(C->L.wsum) < EPS) r[9] = -1;
     }
     v3 wl = vnormalized(vsub(coord, p));
     if (vdot(wl, N) > 0) {
@@ -1301,9 +1315,19 @@ static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t no
         }
         v3 Li = shade_mis(C, g, h.beta, h.gamma, vmul(wi, -1), 2 * node + 1);
         L_brdf = vmul(rgb_mul(Li, brdf), vdot(wi, N) / (pdf + light_pdf) / P_RR);
+        if (dbg_slot >= 0) {
+            double* r = g_dbg + DBG_REC * dbg_slot;
+            r[11] = lg >= 0 ? s->light_of[lg] : -1, r[12] = light_pdf, r[13] = pdf;
+        }
+    }
+    if (dbg_slot >= 0) {
+        double* r = g_dbg + DBG_REC * dbg_slot;
+        r[14] = L_light.x, r[15] = L_light.y, r[16] = L_light.z, r[17] = L_brdf.x, r[18] = L_brdf.y, r[19] = L_brdf.z;
     }
     return vadd(L_light, L_brdf);
 }
+
+
 
 /* shade() (main.cpp:269-344): emission at the hit itself; direct light from one point chosen by the
  * non-staged spherical-triangle sampler select_a_point_from_lights_spherical_triangle
@@ -1490,4 +1514,27 @@ int orc_render(const orc_scene* s, const orc_camera* cam, int mode, uint64_t see
     }
     if (stats4) for (int k = 0; k < 4; k++) stats4[k] = tot[k];
     return 0;
+}
+
+/* one MIS camera sample of pixel (i, j) with the counter RNG (mode flags as orc_render); fills up
+ * to max_nodes records of DBG_REC doubles: node id, facet, p[3], N[3], weights_sum, picked light
+ * (-1 none), light prob, light hit along the BRDF direction, its light pdf, BRDF pdf, L_light[3],
+ * L_brdf[3].  Returns the record count. */
+int orc_debug_mis_sample(const orc_scene* s, const orc_camera* cam, int mode, uint64_t seed, int i, int j, int sample,
+                         double* rec, int max_nodes) {
+    ctx C;
+    ctx_init(&C, s, ORC_RNG_COUNTER);
+    C.seed = seed;
+    C.pixel = (uint64_t)i * cam->width + j;
+    C.sample = (uint64_t)sample;
+    cam_frame fr = cam_setup(cam);
+    v3 dir = cam_dir(&fr, i, j);
+    hitrec h;
+    g_dbg = rec, g_dbg_n = 0, g_dbg_cap = max_nodes;
+    for (int k = 0; k < DBG_REC * max_nodes; k++) rec[k] = 0;
+    int f = grid_trace(s, fr.eye, dir, -1, 0, &h);
+    if (f >= 0) shade_root(&C, mode, f, h.beta, h.gamma, vmul(dir, -1));
+    g_dbg = NULL;
+    ls_free(&C.L);
+    return g_dbg_n;
 }

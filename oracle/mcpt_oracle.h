@@ -108,6 +108,10 @@ void orc_shade_sample(const orc_scene* s, const orc_camera* cam, int mode, int r
 int orc_render(const orc_scene* s, const orc_camera* cam, int mode, uint64_t seed, int spp, int s0, int s1,
                int stride, int offset, int nthreads, double* out_rgb, uint64_t* stats4);
 
+/* debugging aid: per-node records of one MIS camera sample (counter RNG), see mcpt_oracle.c */
+int orc_debug_mis_sample(const orc_scene* s, const orc_camera* cam, int mode, uint64_t seed, int i, int j, int sample,
+                         double* rec, int max_nodes);
+
 /* counter RNG: uniform in [0,1) for (seed, pixel, sample, node, dim) -- shared with the GPU */
 double orc_counter_uniform(uint64_t seed, uint64_t pixel, uint64_t sample, uint64_t node, uint32_t dim);
 
