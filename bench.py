@@ -295,7 +295,7 @@ def main():
         _, level, mem_peak = next(g for g in GATHER_PEAKS if accel <= g[0])
         v_frac, h_frac = fl / t_launch / 1e12 / FP32_VECTOR_PEAK_TFLOPS, by / t_launch / 1e9 / mem_peak
         valu_bound = v_frac >= h_frac
-        pk_name = "k_extend_brdf" if args.mode == "brdf" else "k_mis_rays<false>"
+        pk_name = "k_extend_brdf<false>" if args.mode == "brdf" else "k_mis_rays<false, false>"
         hbm_meas = pk.get(pk_name, {}).get("hbm_bytes_per_dispatch")
         roof_trace = {
             "bound": "valu" if valu_bound else level, "kernel": kname,
