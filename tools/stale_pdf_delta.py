@@ -46,7 +46,7 @@ def main():
     dpx = np.linalg.norm((g - f).reshape(-1, 3), axis=1)
     npx = np.linalg.norm(f.reshape(-1, 3), axis=1)
     out = {
-        "what": "shade_with_mis, counter RNG, stale (reference) vs fresh (GPU) light pdf of the BRDF branch, "
+        "what": "shade_with_mis, counter RNG, stale (the reference's, and the GPU default since round 2) vs fresh (MCPT_RENDER_FRESH_PDF) light pdf of the BRDF branch, "
                 "same pixels and samples",
         "frame": "%dx%d, every %dth pixel in x and y from %d (%d px) x %d spp, seed %d" % (
             a.width, a.height, a.stride, off, f.shape[0] * f.shape[1], a.spp, a.seed),
