@@ -294,6 +294,45 @@ __device__ inline double atan2_pos_wave(double y, double x) {
     return atan2_pos(y, x);
 }
 
+// atan(z) for |z| <= 0.03 by its Taylor series to z^9: the truncation is below z^10/11 <= 5.4e-17
+// relative, under half an ulp, so this agrees with atan_core to rounding (5 instructions instead of
+// 11).  In the light prep almost every spherical triangle is small (tan(sA/2) ~ 1e-4..1e-2).
+#ifdef MCPT_ATAN_SHORT5  // A/B: to z^11, |z| <= 0.05 (truncation <= 0.05^12/13 = 1.9e-17)
+constexpr double kAtanShortMax = 0.05;
+__device__ inline double atan_short(double z) {
+    const double s = z * z;
+    double p;
+    asm("v_fma_f64 %0, %1, %2, %3\n\t"
+        "v_fma_f64 %0, %0, %1, %4\n\t"
+        "v_fma_f64 %0, %0, %1, %5\n\t"
+        "v_fma_f64 %0, %0, %1, %6"
+        : "=&v"(p)
+        : "v"(s), "v"(-0.09090909090909091), "s"(0.1111111111111111), "s"(-0.14285714285714285), "s"(0.2),
+          "s"(-0.3333333333333333));
+    return fma(z * s, p, z);
+}
+#else
+constexpr double kAtanShortMax = 0.03;
+__device__ inline double atan_short(double z) {
+    const double s = z * z;
+    double p;
+    asm("v_fma_f64 %0, %1, %2, %3\n\t"
+        "v_fma_f64 %0, %0, %1, %4\n\t"
+        "v_fma_f64 %0, %0, %1, %5"
+        : "=&v"(p)
+        : "v"(s), "v"(0.1111111111111111), "s"(-0.14285714285714285), "s"(0.2), "s"(-0.3333333333333333));
+    return fma(z * s, p, z);
+}
+#endif
+// atan2_pos_wave with a second wave-uniform fast path for the light prep's batches: when every
+// lane has x > 0 and y <= 0.03 x, atan_short.  Only the prep's batch evaluation uses it, where the
+// wave's lanes are one node's candidate batch (fixed by the node), so a weight never depends on
+// how nodes were batched.
+__device__ inline double atan2_pos_prep(double y, double x) {
+    if (__ballot(!(x > 0.0 && y <= kAtanShortMax * x)) == 0) return atan_short(fdiv_pos(y, x));
+    return atan2_pos_wave(y, x);
+}
+
 // Stage 3 (Mylight.cpp:360-413) in fp64 with fewer instructions than the reference's literal
 // formulation; identical up to rounding (DESIGN.md "light prep numerics"):
 //  * unit vectors A, B, C by rsqrt instead of sqrt + 3 divisions;
@@ -306,13 +345,15 @@ __device__ inline double atan2_pos_wave(double y, double x) {
 //    triangle) as sA <= 0.
 // Every consumer (the prep batches, the small-N_L lane prep, the pdf's survival test in
 // k_mis_combine and the picked triangle's Arvo setup in k_mis_gen / k_shade_gen) goes through
-// sph_excess on the same unswapped vectors, so they agree bit for bit on survival and sA.
+// sph_excess on the same unswapped vectors, so they agree bit for bit on survival; sA agrees bit
+// for bit except that the prep's batches (kPrepBatch) may take atan_short, equal to rounding.
 struct SphEx {
     d3 A, B, C;     // unit vectors towards p0, p1, p2 (reference vertex order)
     double ab;      // A.B
     double half;    // sA / 2
     bool edges_ok;  // A.B, B.C, C.A < 1
 };
+template <bool kPrepBatch = false>
 __device__ inline SphEx sph_excess(d3 a, d3 b, d3 c) {
     SphEx e;
     e.A = funit(a);
@@ -321,7 +362,8 @@ __device__ inline SphEx sph_excess(d3 a, d3 b, d3 c) {
     const double ab = fdot(e.A, e.B), bc = fdot(e.B, e.C), ca = fdot(e.C, e.A);
     e.ab = ab;
     e.edges_ok = (ab < 1.0) & (bc < 1.0) & (ca < 1.0);
-    e.half = atan2_pos_wave(fabs(fdot(e.A, fcross(e.B, e.C))), 1.0 + ab + bc + ca);
+    const double num = fabs(fdot(e.A, fcross(e.B, e.C))), den = 1.0 + ab + bc + ca;
+    e.half = kPrepBatch ? atan2_pos_prep(num, den) : atan2_pos_wave(num, den);
     return e;
 }
 
@@ -330,8 +372,9 @@ __device__ inline SphEx sph_excess(d3 a, d3 b, d3 c) {
 // w = (sA/2) lsum2 rounds exactly like the reference's sA * sum (scaling by 2 is exact) without
 // the doubling of sA; 0 <= w <= DBL_MAX is one v_cmp_class (-0, +0, +denormal, +normal).
 // Returns w, or 0 if culled (*ok = false).
+template <bool kPrepBatch = false>
 __device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, bool* ok) {
-    const SphEx e = sph_excess(sub(p0, x1), sub(p1, x1), sub(p2, x1));
+    const SphEx e = sph_excess<kPrepBatch>(sub(p0, x1), sub(p1, x1), sub(p2, x1));
     const double w = e.half * lsum2;
     const bool good = e.edges_ok & (e.half > 0) & __builtin_amdgcn_class(w, 0x1e0);
     *ok = good;

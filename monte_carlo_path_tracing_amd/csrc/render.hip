@@ -1023,7 +1023,7 @@ __device__ inline double prep_weight_buf(__amdgpu_buffer_rsrc_t rw, int li, d3 x
     const v4u c = struct_load_b128(rw, li, 32, 0, 0);
     const v4u d = struct_load_b128(rw, li, 48, 0, 0);
     const v4u e = struct_load_b128(rw, li, 64, 0, 0);
-    return light_weight_bf(mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y)),
+    return light_weight_bf<true>(mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y)),
                            mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
                            mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1, ok);
 }
@@ -1131,14 +1131,18 @@ __device__ inline double prep_select(const double* bt, const unsigned short* lst
 }
 
 constexpr int kChunkUnroll = 2;
-// chunk splits of k_prep_cull_lanes (more waves in flight to hide the table's scalar-load latency):
-// 4, at least 4 chunks per split; MCPT_CULL_SPLITS overrides (A/B)
-inline int cull_splits(int n, int nchunks) {
-    static const int env = getenv("MCPT_CULL_SPLITS") ? atoi(getenv("MCPT_CULL_SPLITS")) : 0;
-    (void)n;
-    const int s = env > 0 ? env : 4;  // measured: 1 -> 305, 2 -> 316, 3 -> 323, 4 -> 323, 6 -> 321, 8 -> 312 Msamples/s
-    return std::max(1, std::min(s, std::max(1, nchunks / 4)));
-}
+// candidate words, node-major: word (node, chunk) at node * mask_stride + chunk, the row padded to
+// whole 64-B lines (zero words past nchunks), so k_prep_pk2 reads a node's words as s_load_dwordx16
+// of whole lines (each line fetched once) and the cull writes them two chunks (16 B) at a time
+constexpr int kMaskLine = 8;  // words per 64-B line
+__host__ __device__ inline int mask_stride(int nchunks) { return (nchunks + kMaskLine - 1) / kMaskLine * kMaskLine; }
+// chunk splits of k_prep_cull_lanes over blockIdx.y (more waves in flight to hide the table's
+// scalar-load latency): 4, each a whole number of chunk pairs (measured with the tiled layout: 1 ->
+// 305, 2 -> 316, 3 -> 323, 4 -> 323, 6 -> 321, 8 -> 312 Msamples/s)
+#ifndef MCPT_CULL_SPLITS
+#define MCPT_CULL_SPLITS 4
+#endif
+inline int cull_splits(int nchunks) { return std::max(1, std::min(MCPT_CULL_SPLITS, nchunks / 4)); }
 // Phase A with a lane per shading node and the light table in scalar registers: each light pair
 // (LightPair, two s_load_dwordx16) is read once per 64 nodes from the scalar cache, and the two
 // cheap stages of both lights run as 13 v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 with one
@@ -1149,12 +1153,6 @@ inline int cull_splits(int n, int nchunks) {
 // decisions are the reference's (err as in node_f; the threshold is folded into d and cn).
 // raw v_max3_f32 / v_min_f32 (the builtins canonicalise operands that came out of packed ops
 // first; NaN handling is irrelevant here: a NaN light value never reaches the cull)
-// candidate words in tiles of 8 nodes: word (node, chunk) at (node / 8) [chunk] [node % 8], so the
-// lane-per-node cull writes whole 64-B segments (8 lanes each) and k_prep_pk2's per-node reads of
-// the 8 nodes of a tile (claimed by neighbouring waves at about the same time) hit the same lines
-__device__ inline size_t mask_index(int node, int chunk, int nchunks) {
-    return ((size_t)(node >> 3) * nchunks + chunk) * 8 + (node & 7);
-}
 __device__ inline float max3_raw(float a, float b, float c) {
     float r;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -1199,6 +1197,58 @@ struct CullLane {
     }
 };
 
+// one chunk (64 lights, two halves of 32) of the cull for this lane's node: the candidate word
+// (bit j = light 64 c + j)
+template <bool kCountC1>
+__device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const LightPair* __restrict__ T, int c,
+                                      float err, uint64_t actm, bool act, d3 x1, d3 nn, unsigned long long& c1) {
+    unsigned word[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const LightPair* __restrict__ Th = T + 32 * c + 16 * h;
+        unsigned w = 0, c1w = 0;
+        float amin = __builtin_inff();  // min over the 32 lights of min(|s|, |min(s, max t)|)
+#pragma unroll 2
+        for (int q = 0; q < 16; q++) {
+            v2f s1, t[3];
+            cl.eval(Th[q], &s1, t);
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const float sv = s1[e];
+                const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
+                // ambiguous lanes (a value within err of the threshold) have s >= -err and a clear bit here
+                amin = min3_abs_raw(amin, sv, mn);
+                if (kCountC1) c1w += __popcll(__ballot(sv < -err) & actm);  // statistic only
+                w = shift_in(w, __ballot(mn > err));
+            }
+        }
+        if (__ballot(amin <= err) & actm) {  // rare: the reference's exact fp64 stages for the ambiguous (node, light) pairs
+            for (int q = 0; q < 16; q++) {
+                v2f s1, t[3];
+                cl.eval(Th[q], &s1, t);
+                for (int e = 0; e < 2; e++) {
+                    const float sv = s1[e];
+                    const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
+                    const int li = 64 * c + 32 * h + 2 * q + e;
+                    int st = -1;
+                    if (act && min_abs_raw(sv, mn) <= err && li < S.NL) {
+                        const LightPair& L = Th[q];
+                        auto pc = [&](int i) { return (double)(e ? L.p[i].y : L.p[i].x); };
+                        const double4 ln = S.lt_n[li];
+                        st = light_cheap_stage(mk3(pc(0), pc(1), pc(2)), mk3(pc(3), pc(4), pc(5)),
+                                               mk3(pc(6), pc(7), pc(8)), mk3(ln.x, ln.y, ln.z), x1, nn);
+                        if (st == 0) w |= 1u << (31 - (2 * q + e));
+                    }
+                    if (kCountC1) c1w += __popcll(__ballot(st == 1));  // uniform: every lane of the wave
+                }
+            }
+        }
+        c1 += c1w;
+        word[h] = __builtin_bitreverse32(w);
+    }
+    return ((uint64_t)word[1] << 32) | word[0];
+}
+
 template <bool kCountC1>
 __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
                                                          const double* __restrict__ qn, uint64_t* __restrict__ masks,
@@ -1222,62 +1272,27 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
     const uint64_t actm = __ballot(act);
     unsigned long long c1 = 0;
     const LightPair* __restrict__ T = S.lt_pair;
-    // blockIdx.y splits the chunks: more waves per SIMD to hide the scalar-load latency of the table
-    const int per = (nchunks + gridDim.y - 1) / gridDim.y;
-    const int cb = blockIdx.y * per, ce = min(nchunks, cb + per);
-    for (int c = cb; c < ce; c++) {
-        unsigned word[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const LightPair* __restrict__ Th = T + 32 * c + 16 * h;
-            unsigned w = 0, c1w = 0;
-            float amin = __builtin_inff();  // min over the 32 lights of min(|s|, |min(s, max t)|)
-#pragma unroll 2
-            for (int q = 0; q < 16; q++) {
-                v2f s1, t[3];
-                cl.eval(Th[q], &s1, t);
-#pragma unroll
-                for (int e = 0; e < 2; e++) {
-                    const float sv = s1[e];
-                    const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
-                    // ambiguous lanes (a value within err of the threshold) have s >= -err and a clear bit here
-                    amin = min3_abs_raw(amin, sv, mn);
-                    if (kCountC1) c1w += __popcll(__ballot(sv < -err) & actm);  // statistic only
-                    w = shift_in(w, __ballot(mn > err));
-                }
-            }
-            if (__ballot(amin <= err) & actm) {  // rare: the reference's exact fp64 stages for the ambiguous (node, light) pairs
-                for (int q = 0; q < 16; q++) {
-                    v2f s1, t[3];
-                    cl.eval(Th[q], &s1, t);
-                    for (int e = 0; e < 2; e++) {
-                        const float sv = s1[e];
-                        const float mn = min_raw(sv, max3_raw(t[0][e], t[1][e], t[2][e]));
-                        const int li = 64 * c + 32 * h + 2 * q + e;
-                        int st = -1;
-                        if (act && min_abs_raw(sv, mn) <= err && li < S.NL) {
-                            const LightPair& L = Th[q];
-                            auto pc = [&](int i) { return (double)(e ? L.p[i].y : L.p[i].x); };
-                            const double4 ln = S.lt_n[li];
-                            st = light_cheap_stage(mk3(pc(0), pc(1), pc(2)), mk3(pc(3), pc(4), pc(5)),
-                                                   mk3(pc(6), pc(7), pc(8)), mk3(ln.x, ln.y, ln.z), x1, nn);
-                            if (st == 0) w |= 1u << (31 - (2 * q + e));
-                        }
-                        if (kCountC1) c1w += __popcll(__ballot(st == 1));  // uniform: every lane of the wave
-                    }
-                }
-            }
-            c1 += c1w;
-            word[h] = __builtin_bitreverse32(w);
-        }
-        if (act) masks[mask_index(node, c, nchunks)] = ((uint64_t)word[1] << 32) | word[0];
+    // blockIdx.y splits the chunks (whole pairs): more waves per SIMD to hide the scalar-load
+    // latency of the table.  Each pair of words is one 16-B store into the node's row.
+    const int pairs = (nchunks + 1) >> 1;
+    const int per = (pairs + gridDim.y - 1) / gridDim.y;
+    const int pb = blockIdx.y * per, pe = min(pairs, pb + per);
+    uint4* __restrict__ row = reinterpret_cast<uint4*>(masks + (size_t)nd * mask_stride(nchunks));
+    for (int p = pb; p < pe; p++) {
+        const int c = 2 * p;
+        const uint64_t w0 = cull_chunk<kCountC1>(S, cl, T, c, err, actm, act, x1, nn, c1);
+        const uint64_t w1 = c + 1 < nchunks ? cull_chunk<kCountC1>(S, cl, T, c + 1, err, actm, act, x1, nn, c1) : 0ull;
+        if (act) row[p] = make_uint4((unsigned)w0, (unsigned)(w0 >> 32), (unsigned)w1, (unsigned)(w1 >> 32));
     }
+    // zero words past nchunks up to the row's last whole line (k_prep_pk2 reads whole lines)
+    if (act && pe == pairs)
+        for (int p = pairs; p < mask_stride(nchunks) / 2; p++) row[p] = make_uint4(0, 0, 0, 0);
     // padding lights (index >= N_L, d = 1e30) were counted as light-side culled by every active lane
-    if (kCountC1 && ce == nchunks) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
+    if (kCountC1 && pe == pairs) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
 
-constexpr int kMaskBatch = 8;  // candidate words per batch of scalar loads (k_prep_pk2)
+constexpr int kMaskBatch = kMaskLine;  // candidate words per batch of scalar loads (k_prep_pk2): one line
 template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
@@ -1319,20 +1334,19 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         };
         int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
         if (kMaskIn) {  // phase A done by k_prep_cull_lanes: rebuild the list from the candidate words
-            // The node's words are wave-uniform: scalar loads (8 in flight) put each straight into
-            // SGPRs, so a word costs 3 VALU (2 v_mbcnt + 1 v_lshl_add) + 1 v_add for the index
-            // instead of 2 v_readlane more.  Words past nchunks are read (the scratch is padded by
-            // one tile) and zeroed by a scalar select.
+            // The node's words are wave-uniform: scalar loads of whole 64-B lines (s_load_dwordx16,
+            // kMaskBatch words each, the row zero-padded to whole lines) put them straight into SGPRs,
+            // so a word costs 3 VALU (2 v_mbcnt + 1 v_lshl_add) + 1 v_add for the index.
             const unsigned lds_lst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lst);  // LDS offset (low half of the flat address)
-            const uint64_t* __restrict__ mrow = masks + mask_index(node, 0, nchunks);
+            const uint64_t* __restrict__ mrow = masks + (size_t)node * mask_stride(nchunks);
             unsigned idx = (unsigned)lane;
             for (int c0 = 0; c0 < nchunks; c0 += kMaskBatch) {
                 uint64_t mw[kMaskBatch];
 #pragma unroll
-                for (int q = 0; q < kMaskBatch; q++) mw[q] = mrow[(size_t)(c0 + q) * 8];
+                for (int q = 0; q < kMaskBatch; q++) mw[q] = mrow[c0 + q];
 #pragma unroll
                 for (int q = 0; q < kMaskBatch; q++) {
-                    const uint64_t m = c0 + q < nchunks ? mw[q] : 0ull;
+                    const uint64_t m = mw[q];
                     append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_lst + 2u * (unsigned)ncand, idx);
                     ncand += __popcll(m);
                     idx += 64;
@@ -2609,10 +2623,10 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
         if (count_c1 || !stats)
-            hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d,
+            hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
                                n, qp, qn, masks, nchunks, stats);
         else
-            hipLaunchKernelGGL(k_prep_cull_lanes<false>, dim3((n + 255) / 256, cull_splits(n, nchunks)), dim3(256), 0, st, d,
+            hipLaunchKernelGGL(k_prep_cull_lanes<false>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
                                n, qp, qn, masks, nchunks, stats);
         if (cache.build)
             hipLaunchKernelGGL((k_prep_pk2<5, true, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
@@ -2736,8 +2750,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
     if (needs_prep && D.d.NL > kSmallNL) {
-        // + one tile of padding: k_prep_pk2 reads whole batches of kMaskBatch words past nchunks
-        if ((rc = ensure(D.masks, ((size_t)((std::max(cap, npx) + 7) / 8 * 8) * nchunks + 8 * kMaskBatch) * 8))) return rc;
+        if ((rc = ensure(D.masks, (size_t)std::max(cap, npx) * mask_stride(nchunks) * 8))) return rc;
         masks = (uint64_t*)D.masks.p;
     }
     // root-point cache (see PrepCache): built here when the call has >= 2 samples per pixel and the
@@ -3616,7 +3629,7 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
     void *dp, *dn, *du, *dw, *dc, *dk, *dm;
-    HIP_OK(hipMalloc(&dm, 8ull * ((n + 7) / 8 * 8) * prep_chunks(D->d.NL)));  // candidate words of the split prep (variant 17)
+    HIP_OK(hipMalloc(&dm, 8ull * n * mask_stride(prep_chunks(D->d.NL))));  // candidate words of the split prep (variant 17)
     HIP_OK(hipMalloc(&dp, 24ull * n));
     HIP_OK(hipMalloc(&dn, 24ull * n));
     HIP_OK(hipMalloc(&du, 8ull * n));
@@ -3651,7 +3664,7 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
     void *dp, *dn, *du, *dw, *dk, *dm;
-    HIP_OK(hipMalloc(&dm, 8ull * ((n + 7) / 8 * 8) * prep_chunks(D->d.NL)));
+    HIP_OK(hipMalloc(&dm, 8ull * n * mask_stride(prep_chunks(D->d.NL))));
     HIP_OK(hipMalloc(&dp, 24ull * n));
     HIP_OK(hipMalloc(&dn, 24ull * n));
     HIP_OK(hipMalloc(&du, 8ull * n));
