@@ -162,6 +162,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and L2 check")
     ap.add_argument("--fresh-pdf", action="store_true",
                     help="MIS with the node's own light pdf (MCPT_RENDER_FRESH_PDF) instead of the reference's stale one")
+    ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
+                    help="light-prep precision: fp64 (the reference's, the headline) or the opt-in FP32_STABLE mode "
+                         "(MCPT_RENDER_PRECISION_FP32: packed-fp32 weights summed in fp64)")
     ap.add_argument("--out", default="", help="optional .bmp of the rendered frame (rank 0)")
     args = ap.parse_args()
 
@@ -198,7 +201,9 @@ def main():
     fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
     scratch = torch.zeros_like(fb)
 
-    flags = mcpt.RENDER_NO_BACKFACE_STATS | (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0)
+    mode_flags = (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0) | (
+        mcpt.RENDER_PRECISION_FP32 if args.precision == "fp32" else 0)
+    flags = mcpt.RENDER_NO_BACKFACE_STATS | mode_flags
     for k in range(args.warmup):  # warmup renders (same kernels and flags as the timed steps) go to scratch
         mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
                            sample_range=(0, world * S), comm=comm, flags=flags)
@@ -232,7 +237,7 @@ def main():
     for k in range(args.steps):
         st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
                                 sample_range=(k * world * S, (k + 1) * world * S), comm=comm,
-                                flags=mcpt.DEBUG_COUNT_TRAVERSAL | (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0))
+                                flags=mcpt.DEBUG_COUNT_TRAVERSAL | mode_flags)
         for key, v in st.as_dict().items():
             rep[key] = rep.get(key, 0) + v
     for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays",
@@ -319,7 +324,7 @@ def main():
     if world == 1 and not args.no_cpu:
         log("cpu baseline (~%.0f s) ..." % args.cpu_seconds)
         cpu, cimg, cspp = cpu_baseline(args.scene, W, H, args.mode, args.seed, args.cpu_seconds)
-        g, _ = mcpt.render(scene, cam, cspp, mode=args.mode, seed=args.seed, device=local)
+        g, _ = mcpt.render(scene, cam, cspp, mode=args.mode, seed=args.seed, device=local, flags=mode_flags)
         sub = (slice(7, None, 20), slice(7, None, 20))
         l2 = rel_l2(g[sub], cimg[sub])
         l2max = max_px_rel(g[sub], cimg[sub])
@@ -328,11 +333,13 @@ def main():
     line = {
         "metric": SCENES[args.scene][0], "value": round(value, 4), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64" if args.precision == "fp64" else "f64 (light-prep weights f32, MCPT_RENDER_PRECISION_FP32)",
         "data": SCENES[args.scene][1],
         "config": {"workload": "%s %s %dx%d" % ("veach-mis" if args.scene == "veach" else "cornell-1M", args.mode.upper(), W, H),
                    "width": W, "height": H,
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
+                   "precision": args.precision,
                    "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world},
         "roofline": roofline,
         "roofline_prep": roof_prep,

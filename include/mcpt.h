@@ -136,6 +136,15 @@ enum { MCPT_RENDER_NO_BACKFACE_STATS = 1 };
  * the reference; this flag is the "fixed" estimator (4.6e-3 relative L2 from the reference's on the
  * Veach stand-in, profiles/stale_pdf_delta.json). */
 enum { MCPT_RENDER_FRESH_PDF = 2 };
+/* mcpt_render_opts.flags: precision of the light prep's full stage (SURVEY.md §8(b) FP32_STABLE,
+ * opt-in).  Default (flag clear) = FP64_LIGHT: the reference's fp64, required for parity.  With the
+ * flag, the spherical-triangle weights (Mylight.cpp:360-413) are evaluated two lights per lane in
+ * packed fp32 by a cancellation-free Van Oosterom-Strackee form (p - x1 with x1 split hi + lo, the
+ * triple product against a precomputed area normal) and summed in fp64: weights within ~1e-6 of the
+ * fp64 ones, rendered frames within the 1e-3 relative L2 tolerance of the fp64 render; the edge-length
+ * and vertex-angle culls below 1e-8 rad reduce to "sA > 0".  Applies to scenes with more than 64
+ * light triangles (the split prep); cheap culls, pick, sampling, pdf and shading stay fp64. */
+enum { MCPT_RENDER_PRECISION_FP32 = 4 };
 
 /* zero-fills *opts and sets struct_size, device = -1, seed = 20240430, spp = 10 (main.cpp:567),
  * mode = MCPT_MODE_MIS */

@@ -61,6 +61,7 @@ class RenderOpts(C.Structure):
                 ("devices", C.POINTER(C.c_int32)), ("comm", C.c_void_p)]
 RENDER_NO_BACKFACE_STATS = 1  # mcpt_render_opts.flags (include/mcpt.h)
 RENDER_FRESH_PDF = 2  # shade_with_mis: the node's own light pdf instead of the reference's stale one
+RENDER_PRECISION_FP32 = 4  # opt-in FP32_STABLE light prep (packed-fp32 weights, fp64 sums); default FP64_LIGHT
 DEBUG_SPLIT_BRDF, DEBUG_NO_ROOT_CACHE, DEBUG_COUNT_TRAVERSAL = 1 << 16, 1 << 17, 1 << 18  # include/mcpt_debug.h
 
 

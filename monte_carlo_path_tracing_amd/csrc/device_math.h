@@ -386,6 +386,77 @@ __device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, do
     return ok;
 }
 
+// ---- MCPT_RENDER_PRECISION_FP32 (opt-in): the full stage of two candidates in packed fp32 ----
+// The same Van Oosterom-Strackee excess, evaluated for two light triangles per lane with
+// v_pk_fma/mul/add_f32 (two lights per VALU instruction) from 10-float records: p0, the edges
+// e1 = p1 - p0, e2 = p2 - p0 (differences of nearby floats, exact in fp32 for small triangles),
+// 2 RadianceRGB::sum().  Three record loads per light instead of five (the fp64 batch loop is
+// co-limited by its light-record load instructions):
+//  * a = p0 - x1 with x1 split into float hi + lo parts (~1e-7 relative even next to a light);
+//    b = a + e1, c = a + e2;
+//  * the triple product as a . (e1 x e2) (= a . (b x c) exactly in real arithmetic), free of the
+//    cancellation of b x c for small, distant triangles;
+//  * tan(sA/2) = |a.n| / (|a||b||c| + (a.b)|c| + (b.c)|a| + (c.a)|b|) from rsqrt of the squared
+//    lengths (no Newton step) and atan by its series to z^7 when the wave's z <= 0.1 (else atanf);
+//  * w = double(sA/2) * double(2 sum), accumulated in fp64 like the default path.
+// Weights agree with the fp64 path to ~1e-6 relative.  Culls: w finite, sA > 0; the reference's
+// edge-length and vertex-angle culls (< 1e-8 rad) are not resolvable in fp32 and are subsumed by
+// sA > 0 for degenerate triangles (a nondegenerate triangle below 1e-8 rad keeps its ~1e-16 weight).
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+struct LightF32 {  // one record as loaded: (p0, e1.x), (e1.y, e1.z, e2.x, e2.y), (e2.z, 2 sum)
+    v4f_t q0, q1;
+    v2f_t q2;
+};
+__device__ inline v2f_t pk_fma(v2f_t a, v2f_t b, v2f_t c) { return __builtin_elementwise_fma(a, b, c); }
+// weights of lights I, J for the node at x1 = xh + xl (floats per component)
+__device__ inline void light_weight_f32x2(const LightF32& I, const LightF32& J, v2f_t xh, v2f_t yh, v2f_t zh,
+                                          v2f_t xl, v2f_t yl, v2f_t zl, double* w0, double* w1, bool* ok0, bool* ok1) {
+    // {light I, light J} pairs of each record float (v_pk_mov_b32 from the two loads)
+    const v2f_t ax = (__builtin_shufflevector(I.q0, J.q0, 0, 4) - xh) - xl,
+                ay = (__builtin_shufflevector(I.q0, J.q0, 1, 5) - yh) - yl,
+                az = (__builtin_shufflevector(I.q0, J.q0, 2, 6) - zh) - zl;
+    const v2f_t e1x = __builtin_shufflevector(I.q0, J.q0, 3, 7), e1y = __builtin_shufflevector(I.q1, J.q1, 0, 4),
+                e1z = __builtin_shufflevector(I.q1, J.q1, 1, 5);
+    const v2f_t e2x = __builtin_shufflevector(I.q1, J.q1, 2, 6), e2y = __builtin_shufflevector(I.q1, J.q1, 3, 7),
+                e2z = __builtin_shufflevector(I.q2, J.q2, 0, 2);
+    const v2f_t bx = ax + e1x, by = ay + e1y, bz = az + e1z;
+    const v2f_t cx = ax + e2x, cy = ay + e2y, cz = az + e2z;
+    const v2f_t nx = pk_fma(e1y, e2z, -(e1z * e2y)), ny = pk_fma(e1z, e2x, -(e1x * e2z)), nz = pk_fma(e1x, e2y, -(e1y * e2x));
+    const v2f_t aa = pk_fma(ax, ax, pk_fma(ay, ay, az * az));
+    const v2f_t bb = pk_fma(bx, bx, pk_fma(by, by, bz * bz));
+    const v2f_t cc = pk_fma(cx, cx, pk_fma(cy, cy, cz * cz));
+    const v2f_t ra = v2f_t{__builtin_amdgcn_rsqf(aa.x), __builtin_amdgcn_rsqf(aa.y)};
+    const v2f_t rb = v2f_t{__builtin_amdgcn_rsqf(bb.x), __builtin_amdgcn_rsqf(bb.y)};
+    const v2f_t rc = v2f_t{__builtin_amdgcn_rsqf(cc.x), __builtin_amdgcn_rsqf(cc.y)};
+    const v2f_t ab = pk_fma(ax, bx, pk_fma(ay, by, az * bz));
+    const v2f_t bc = pk_fma(bx, cx, pk_fma(by, cy, bz * cz));
+    const v2f_t ca = pk_fma(cx, ax, pk_fma(cy, ay, cz * az));
+    const v2f_t t = pk_fma(ax, nx, pk_fma(ay, ny, az * nz));
+    const v2f_t rab = ra * rb;
+    const v2f_t den = pk_fma(ab, rab, pk_fma(bc, rb * rc, pk_fma(ca, rc * ra, v2f_t{1.0f, 1.0f})));
+    const v2f_t num = __builtin_elementwise_abs(t) * (rab * rc);
+    float h0, h1;
+    if (__ballot(!(den.x > 0.0f && num.x <= 0.1f * den.x && den.y > 0.0f && num.y <= 0.1f * den.y)) == 0) {
+        // atan(z) = z - z^3/3 + z^5/5 - z^7/7 for z <= 0.1 (truncation z^8/9 < 1.2e-9)
+        const v2f_t z = num * v2f_t{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        const v2f_t sq = z * z;
+        const v2f_t p = pk_fma(sq, pk_fma(sq, v2f_t{-0.14285714f, -0.14285714f}, v2f_t{0.2f, 0.2f}),
+                               v2f_t{-0.33333334f, -0.33333334f});
+        const v2f_t h = pk_fma(z * sq, p, z);
+        h0 = h.x;
+        h1 = h.y;
+    } else {
+        h0 = atan2f(num.x, den.x);
+        h1 = atan2f(num.y, den.y);
+    }
+    const double v0 = (double)h0 * (double)I.q2.y, v1 = (double)h1 * (double)J.q2.y;
+    *ok0 = (h0 > 0.0f) & __builtin_amdgcn_class(v0, 0x1e0);
+    *ok1 = (h1 > 0.0f) & __builtin_amdgcn_class(v1, 0x1e0);
+    *w0 = *ok0 ? v0 : 0.0;
+    *w1 = *ok1 ? v1 : 0.0;
+}
+
 // The picked triangle's spherical triangle for Arvo's sampler: the same survival and sA as
 // light_weight_bf (lsum2 = 2 RadianceRGB::sum()), plus unit vectors in the reference's orientation (B, C swapped so that the
 // triangle winds counter-clockwise about n, Mylight.cpp:366-371; the test runs on the

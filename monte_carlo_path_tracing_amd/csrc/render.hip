@@ -76,6 +76,8 @@ struct DScene {
     const float4* lt_pk;      // NL*3: (p0.x, p1.x, p2.x, nl.x), (.. .y), (.. .z) -- packed cheap stages
     const float* lt_d;        // NL: float(nl . p0)
     const double2* lt_w;      // NL*5: p0, p1, p2 (fp64), 2 RadianceRGB::sum()
+    const float4* lt_f;       // NL*4: fp32 records of MCPT_RENDER_PRECISION_FP32 (LightF32: p0, p1, p2 with the
+                              // area normal in .w, then 2 RadianceRGB::sum() as fp64 bits)
     const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
     const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves), breadth-first node order
@@ -998,6 +1000,7 @@ __device__ inline int prep_stage_pk_bf(const DScene& S, int li, float4 X, float4
 // Light-table loads through buffer descriptors (32-bit offsets, immediate offsets per vertex row,
 // hardware bounds check returning 0 past the table, so no index clamp).
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 constexpr int kBufFlags = 0x00020000;  // gfx9 raw buffer descriptor word 3
 __device__ inline float4 u4f(v4u v) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
@@ -1027,6 +1030,35 @@ __device__ inline double prep_weight_buf(__amdgpu_buffer_rsrc_t rw, int li, d3 x
                            mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
                            mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1, ok);
 }
+// fp32 records (MCPT_RENDER_PRECISION_FP32, LightF32): 10 floats at a 64-B stride (a record never
+// straddles a cache line), the same padding and sentinels as lt_w
+constexpr int kLtF = 64;
+__device__ inline __amdgpu_buffer_rsrc_t light_record_f32_rsrc(const DScene& S, int ngroups4) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_f, kLtF, (ngroups4 * 256 + kSentinelPad) * kLtF, kBufFlags);
+}
+__device__ v2u struct_load_b64(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.ptr.buffer.load.v2i32");
+__device__ inline LightF32 load_light_f32(__amdgpu_buffer_rsrc_t rf, int li) {
+    const v4u a = struct_load_b128(rf, li, 0, 0, 0);
+    const v4u b = struct_load_b128(rf, li, 16, 0, 0);
+    const v2u c = struct_load_b64(rf, li, 32, 0, 0);
+    return LightF32{__builtin_bit_cast(v4f_t, a), __builtin_bit_cast(v4f_t, b), __builtin_bit_cast(v2f_t, c)};
+}
+// x1 split into float hi + lo per component (wave-uniform), for light_weight_f32x2
+struct NodeF32 {
+    v2f_t xh, yh, zh, xl, yl, zl;
+};
+__device__ inline NodeF32 node_f32(d3 x1) {
+    const float hx = (float)x1.x, hy = (float)x1.y, hz = (float)x1.z;
+    const float lx = (float)(x1.x - hx), ly = (float)(x1.y - hy), lz = (float)(x1.z - hz);
+    return NodeF32{v2f_t{hx, hx}, v2f_t{hy, hy}, v2f_t{hz, hz}, v2f_t{lx, lx}, v2f_t{ly, ly}, v2f_t{lz, lz}};
+}
+__device__ inline void prep_weight_f32x2(__amdgpu_buffer_rsrc_t rf, int li, int lj, const NodeF32& X, double* w0,
+                                         double* w1, bool* ok0, bool* ok1) {
+    light_weight_f32x2(load_light_f32(rf, li), load_light_f32(rf, lj), X.xh, X.yh, X.zh, X.xl, X.yl, X.zl, w0, w1, ok0,
+                       ok1);
+}
+
 __device__ inline int lane_rank(uint64_t m) {  // set bits of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
@@ -1069,7 +1101,7 @@ struct PrepCache {
 
 // inverse-CDF pick from the batch totals bt[0, nb) and candidate list lst (LDS or global): returns
 // weights_sum and the picked light (-1 if weights_sum < eps).  u_of() gives dim 1 when needed.
-template <class U>
+template <bool kF32 = false, class U>
 __device__ inline double prep_select(const double* bt, const unsigned short* lst, int nb, int ncand, int lane,
                                      __amdgpu_buffer_rsrc_t rw, d3 x1, U u_of, int* pick_out) {
     double wsum = 0;
@@ -1115,7 +1147,14 @@ __device__ inline double prep_select(const double* bt, const unsigned short* lst
         const bool act = k < ncand;
         const int lj = act ? (int)lst[k] : 0;
         bool ok;
-        double w = prep_weight_buf(rw, lj, x1, &ok);
+        double w;
+        if (kF32) {  // the same packed evaluation as the batch (both halves this candidate)
+            bool ok1;
+            double w1;
+            prep_weight_f32x2(rw, lj, lj, node_f32(x1), &w, &w1, &ok, &ok1);
+        } else {
+            w = prep_weight_buf(rw, lj, x1, &ok);
+        }
         ok = ok && act;
         w = act ? w : 0.0;
         const double sc = wave_incl_scan(w, lane);
@@ -1137,10 +1176,18 @@ constexpr int kChunkUnroll = 2;
 constexpr int kMaskLine = 8;  // words per 64-B line
 __host__ __device__ inline int mask_stride(int nchunks) { return (nchunks + kMaskLine - 1) / kMaskLine * kMaskLine; }
 // chunk splits of k_prep_cull_lanes over blockIdx.y (more waves in flight to hide the table's
-// scalar-load latency): 4, each a whole number of chunk pairs (measured with the tiled layout: 1 ->
-// 305, 2 -> 316, 3 -> 323, 4 -> 323, 6 -> 321, 8 -> 312 Msamples/s)
+// scalar-load latency), each a whole number of bursts: a lane keeps kCullBurst words in registers
+// and stores them back to back, so the node's 64-B line is written whole before L2 can evict it
+// (stored a pair at a time, lines were written back partially: 707 instead of ~400 B per node).
+// Same-box A/B (profiles/round2b_ab_cull_burst.txt): burst 2 / 4 splits 423.4, burst 4 428.1,
+// burst 8 with 6 splits 429.2, burst 8 with 3 splits 424.5 Msamples/s.
+#ifndef MCPT_CULL_BURST
+#define MCPT_CULL_BURST 8
+#endif
+constexpr int kCullBurst = MCPT_CULL_BURST;  // candidate words a cull lane stores back to back (even, <= kMaskLine)
+static_assert(kCullBurst % 2 == 0 && kMaskLine % kCullBurst == 0, "cull burst");
 #ifndef MCPT_CULL_SPLITS
-#define MCPT_CULL_SPLITS 4
+#define MCPT_CULL_SPLITS 6
 #endif
 inline int cull_splits(int nchunks) { return std::max(1, std::min(MCPT_CULL_SPLITS, nchunks / 4)); }
 // Phase A with a lane per shading node and the light table in scalar registers: each light pair
@@ -1272,28 +1319,36 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
     const uint64_t actm = __ballot(act);
     unsigned long long c1 = 0;
     const LightPair* __restrict__ T = S.lt_pair;
-    // blockIdx.y splits the chunks (whole pairs): more waves per SIMD to hide the scalar-load
-    // latency of the table.  Each pair of words is one 16-B store into the node's row.
-    const int pairs = (nchunks + 1) >> 1;
-    const int per = (pairs + gridDim.y - 1) / gridDim.y;
-    const int pb = blockIdx.y * per, pe = min(pairs, pb + per);
+    // blockIdx.y splits the chunks (whole bursts of kCullBurst words): more waves per SIMD to hide
+    // the scalar-load latency of the table.  A burst's words are stored back to back (16 B per
+    // store) into the node's row.
+    const int bursts = (nchunks + kCullBurst - 1) / kCullBurst;
+    const int per = (bursts + gridDim.y - 1) / gridDim.y;
+    const int pb = blockIdx.y * per, pe = min(bursts, pb + per);
     uint4* __restrict__ row = reinterpret_cast<uint4*>(masks + (size_t)nd * mask_stride(nchunks));
     for (int p = pb; p < pe; p++) {
-        const int c = 2 * p;
-        const uint64_t w0 = cull_chunk<kCountC1>(S, cl, T, c, err, actm, act, x1, nn, c1);
-        const uint64_t w1 = c + 1 < nchunks ? cull_chunk<kCountC1>(S, cl, T, c + 1, err, actm, act, x1, nn, c1) : 0ull;
-        if (act) row[p] = make_uint4((unsigned)w0, (unsigned)(w0 >> 32), (unsigned)w1, (unsigned)(w1 >> 32));
+        uint64_t w[kCullBurst];
+#pragma unroll
+        for (int i = 0; i < kCullBurst; i++) {
+            const int c = kCullBurst * p + i;
+            w[i] = c < nchunks ? cull_chunk<kCountC1>(S, cl, T, c, err, actm, act, x1, nn, c1) : 0ull;
+        }
+        if (act)
+#pragma unroll
+            for (int i = 0; i < kCullBurst; i += 2)
+                row[(kCullBurst * p + i) / 2] = make_uint4((unsigned)w[i], (unsigned)(w[i] >> 32), (unsigned)w[i + 1],
+                                                           (unsigned)(w[i + 1] >> 32));
     }
-    // zero words past nchunks up to the row's last whole line (k_prep_pk2 reads whole lines)
-    if (act && pe == pairs)
-        for (int p = pairs; p < mask_stride(nchunks) / 2; p++) row[p] = make_uint4(0, 0, 0, 0);
+    // zero words past the last burst up to the row's last whole line (k_prep_pk2 reads whole lines)
+    if (act && pe == bursts)
+        for (int p = bursts * kCullBurst / 2; p < mask_stride(nchunks) / 2; p++) row[p] = make_uint4(0, 0, 0, 0);
     // padding lights (index >= N_L, d = 1e30) were counted as light-side culled by every active lane
-    if (kCountC1 && pe == pairs) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
+    if (kCountC1 && pe == bursts) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
 
 constexpr int kMaskBatch = kMaskLine;  // candidate words per batch of scalar loads (k_prep_pk2): one line
-template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false>
+template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false, bool kF32 = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
@@ -1310,7 +1365,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
     const int ngroups4 = (nchunks + 3) / 4;
     const __amdgpu_buffer_rsrc_t rpk = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_pk, 0, ngroups4 * 4 * 3072, kBufFlags);
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)S.lt_d, 0, ngroups4 * 4 * 256, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rw = light_record_rsrc(S, ngroups4);
+    const __amdgpu_buffer_rsrc_t rw = kF32 ? light_record_f32_rsrc(S, ngroups4) : light_record_rsrc(S, ngroups4);
     // list padding: the entries [ncand, 64 nb) of the last batch name a sentinel record past the
     // table, which the full stage always culls, so a batch needs no k < ncand test
     const unsigned short sentinel = (unsigned short)(ngroups4 * 256);
@@ -1390,8 +1445,31 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         // branch on the exec mask that is almost never taken except for the padding, instead of a
         // ballot per batch; survivors = ncand - (culled lanes - padding).
         int nbad = 0;
+        const NodeF32 xf = node_f32(x1);
         for (int b0 = 0; b0 < nb; b0 += 4) {
             double w4[4];
+            if (kF32) {  // batches (b0, b0+1) and (b0+2, b0+3) as the two halves of packed fp32 evaluations
+#pragma unroll
+                for (int i = 0; i < 4; i += 2) {
+                    w4[i] = w4[i + 1] = 0.0;
+                    if (b0 + i < nb) {  // wave-uniform
+                        const int k0 = 64 * (b0 + i) + lane, k1 = k0 + 64;
+                        const bool has1 = b0 + i + 1 < nb;
+                        bool ok0, ok1;
+                        double w0, w1;
+                        prep_weight_f32x2(rw, (int)lst[k0], has1 ? (int)lst[k1] : (int)sentinel, xf, &w0, &w1, &ok0, &ok1);
+                        if (kBuild) {
+                            const size_t row = (size_t)(qpixel ? qpixel[node] : node) * C.lstride;
+                            if (k0 < ncand) C.w[row + k0] = ok0 ? w0 : -1.0;
+                            if (k1 < ncand) C.w[row + k1] = ok1 ? w1 : -1.0;
+                        }
+                        w4[i] = w0;
+                        w4[i + 1] = w1;
+                        if (!ok0) asm volatile("v_add_u32 %0, 1, %0" : "+v"(nbad));
+                        if (has1 && !ok1) asm volatile("v_add_u32 %0, 1, %0" : "+v"(nbad));
+                    }
+                }
+            } else {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 w4[i] = 0.0;
@@ -1403,6 +1481,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                     w4[i] = w;
                     if (!ok) asm volatile("v_add_u32 %0, 1, %0" : "+v"(nbad));  // a real branch (SALU only when no lane is culled)
                 }
+            }
             }
             const double t = batch_totals4(w4[0], w4[1], w4[2], w4[3]);
             if ((lane & 15) == 15 && b0 + (lane >> 4) < nb) bt[b0 + (lane >> 4)] = t;
@@ -1424,7 +1503,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             continue;
         }
         int pick;
-        const double wsum = prep_select(bt, lst, nb, ncand, lane, rw, x1, u_of, &pick);
+        const double wsum = prep_select<kF32>(bt, lst, nb, ncand, lane, rw, x1, u_of, &pick);
         if (lane == 0) {
             wsum_out[node] = wsum;
             pick_out[node] = pick;
@@ -2400,6 +2479,8 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     // fast path (|y| ~ 0, x ~ 4)
     std::vector<double2> lw(5 * (nl_pad + kSentinelPad), make_double2(0, 0));
     for (int l = nl_pad; l < nl_pad + kSentinelPad; l++) lw[5 * (size_t)l + 4] = make_double2(0.0, -1.0);
+    // fp32 records (same padding and sentinels: a zero record gives e1 = e2 = 0, so sA = 0, culled)
+    std::vector<float4> lf(4 * (nl_pad + kSentinelPad), make_float4(0, 0, 0, 0));
     for (int l = 0; l < s.NL; l++) {
         const float4 a = lv[3 * l], b = lv[3 * l + 1], c = lv[3 * l + 2];
         lpk[3 * l] = make_float4(a.x, b.x, c.x, a.w);
@@ -2411,6 +2492,12 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
         lw[5 * l + 2] = make_double2(b.y, b.z);
         lw[5 * l + 3] = make_double2(c.x, c.y);
         lw[5 * l + 4] = make_double2(c.z, 2.0 * ln[l].w);
+        // edges p1 - p0, p2 - p0 from the float vertices in fp64, rounded once (exact for nearby vertices)
+        const float e1[3] = {(float)((double)b.x - a.x), (float)((double)b.y - a.y), (float)((double)b.z - a.z)};
+        const float e2[3] = {(float)((double)c.x - a.x), (float)((double)c.y - a.y), (float)((double)c.z - a.z)};
+        lf[4 * (size_t)l] = make_float4(a.x, a.y, a.z, e1[0]);
+        lf[4 * (size_t)l + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
+        lf[4 * (size_t)l + 2] = make_float4(e2[2], (float)(2.0 * ln[l].w), 0, 0);
     }
     std::vector<LightPair> lpr(32 * (size_t)std::max(prep_chunks(s.NL), 1));
     for (size_t q = 0; q < lpr.size(); q++) {
@@ -2441,6 +2528,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, lpk, &d.lt_pk))) return rc;
     if ((rc = upload(*D, ld, &d.lt_d))) return rc;
     if ((rc = upload(*D, lw, &d.lt_w))) return rc;
+    if ((rc = upload(*D, lf, &d.lt_f))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
     std::vector<BvhNode4> b4 = bfs_order(collapse_bvh4(sc->bvh)), lb4 = bfs_order(collapse_bvh4(sc->lbvh));
     if ((rc = pack_leaf_codes(b4)) || (rc = pack_leaf_codes(lb4))) return rc;
@@ -2597,10 +2685,16 @@ constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 // form: needs the candidate-word scratch `masks`).  Auto: 9 for few lights, else 17 with masks, 8
 // without, 0 when the candidate list does not fit in LDS.  Cache builds run 8 or 17.
 // work: a device word, zeroed here before the launch (the kernel's dynamic node counter)
+// the fp32 variant's launch bound: 5 waves/SIMD (81 VGPRs; 6 forces 80: -0.8% same-box)
+#ifndef MCPT_PK2_F32_WAVES
+#define MCPT_PK2_F32_WAVES 5
+#endif
+constexpr int kPk2F32Waves = MCPT_PK2_F32_WAVES;
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
-                       const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr, bool count_c1 = true) {
+                       const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr, bool count_c1 = true,
+                       bool fp32 = false) {
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
@@ -2628,12 +2722,11 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
         else
             hipLaunchKernelGGL(k_prep_cull_lanes<false>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
                                n, qp, qn, masks, nchunks, stats);
-        if (cache.build)
-            hipLaunchKernelGGL((k_prep_pk2<5, true, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
-                               qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
-        else
-            hipLaunchKernelGGL((k_prep_pk2<5, false, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn,
-                               qpixel, qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache, masks);
+        // fp32: MCPT_RENDER_PRECISION_FP32's packed-fp32 full stage (light_weight_f32x2)
+        auto kern = cache.build ? (fp32 ? k_prep_pk2<kPk2F32Waves, true, true, true> : k_prep_pk2<5, true, true, false>)
+                                : (fp32 ? k_prep_pk2<kPk2F32Waves, false, true, true> : k_prep_pk2<5, false, true, false>);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample, qnode, u, wsum,
+                           pick, count, stats, nchunks, wb, work, cache, masks);
     } else if (cache.build) {
         hipLaunchKernelGGL((k_prep_pk2<5, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
@@ -2739,12 +2832,13 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
         return MCPT_E_SCENE;
     }
-    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_DEBUG_SPLIT_BRDF |
-                     MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL)) {
+    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
+                     MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
     const bool count_c1 = !(o->flags & MCPT_RENDER_NO_BACKFACE_STATS);
+    const bool fp32 = (o->flags & MCPT_RENDER_PRECISION_FP32) != 0;
     double prep_ms = 0, trace_ms = 0;
     uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0, trace_launches = 0;
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
@@ -2795,7 +2889,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
             HIP_OK(launch_prep(masks ? 17 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks, count_c1));
+                               nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks, count_c1, fp32));
             HIP_OK(hipEventRecord(D.evp1, st));
             HIP_OK(hipEventSynchronize(D.evp1));
             float ms = 0;
@@ -2918,7 +3012,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
                                        cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks,
-                                       count_c1));
+                                       count_c1, fp32));
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
@@ -2933,7 +3027,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
                                    cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks,
-                                   count_c1));
+                                   count_c1, fp32));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 timed = true;
             }

@@ -184,6 +184,32 @@ def test_mis_fresh_pdf_flag_vs_oracle(scene, oscene, W, H, spp):
     assert rel_l2(d[sub], g[sub]) > 1e-9
 
 
+@pytest.mark.parametrize("mode,W,H,spp", [("mis", 80, 60, 8), ("mis", 800, 600, 16), ("shade", 800, 600, 16)])
+def test_precision_fp32_vs_oracle(scene, oscene, mode, W, H, spp):
+    """MCPT_RENDER_PRECISION_FP32 (opt-in): packed-fp32 light weights,
+    summed in fp64.  Tolerance: frame relative L2 <= 1e-3 against the fp64 oracle (the north star's);
+    per pixel, a pick whose u * weights_sum lies within ~1e-6 of a CDF boundary may take the adjacent
+    light triangle (measured ~1e-4 of prep nodes), so <= 1% of pixels may exceed 1e-3 and none 0.5."""
+    cam = mcpt.Camera.reference(W, H)
+    g, _ = mcpt.render(scene, cam, spp, mode=mode, seed=SEED, flags=mcpt.RENDER_PRECISION_FP32)
+    d, _ = mcpt.render(scene, cam, spp, mode=mode, seed=SEED)
+    stride = 1 if W < 200 else 20
+    off = 0 if stride == 1 else 7
+    c, _ = oscene.render(po.reference_camera(W, H), OMODE[mode], SEED, spp, stride=stride, offset=off, nthreads=8)
+    sub = (slice(off, None, stride), slice(off, None, stride))
+    err, mx = rel_l2(g[sub], c[sub]), max_px_rel(g[sub], c[sub])
+    dn = np.linalg.norm((g[sub] - c[sub]).reshape(-1, 3), axis=1)
+    cn = np.linalg.norm(c[sub].reshape(-1, 3), axis=1)
+    frac = float(np.mean(dn > 1e-3 * np.maximum(cn, 1e-300)))
+    print("fp32 light prep %s %dx%dx%d: rel L2 vs oracle %.3e (fp64 GPU %.3e), max per-pixel %.3e, "
+          "pixels > 1e-3: %.4f; fp32 vs fp64 GPU frame %.3e" % (
+              mode, W, H, spp, err, rel_l2(d[sub], c[sub]), mx, frac, rel_l2(g, d)))
+    assert np.isfinite(g).all() and (g >= 0).all()
+    assert err <= L2_TOL
+    assert frac <= 0.01 and mx <= 0.5
+    assert rel_l2(g, d) > 0  # the flag changes the arithmetic
+
+
 def test_sample_range_split_is_invariant(scene):
     """Sharding by sample range (multi-GPU, sequential calls) gives the same frame up to fp64 order."""
     cam = mcpt.Camera.reference(64, 48)
