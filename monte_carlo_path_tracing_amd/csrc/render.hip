@@ -1347,6 +1347,11 @@ __global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const 
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
 
+// skip the list append of an all-zero candidate word by a scalar branch (same-box A/B:
+// 410.6 / 425.0 / 425.1 vs 423.8 / 415.8 / 421.9 Msamples/s, profiles/round2b_ab_zero_words.txt)
+#ifndef MCPT_SKIP_ZERO_WORDS
+#define MCPT_SKIP_ZERO_WORDS 1
+#endif
 constexpr int kMaskBatch = kMaskLine;  // candidate words per batch of scalar loads (k_prep_pk2): one line
 template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false, bool kF32 = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
@@ -1402,9 +1407,18 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
 #pragma unroll
                 for (int q = 0; q < kMaskBatch; q++) {
                     const uint64_t m = mw[q];
+                    (void)idx;
+#if MCPT_SKIP_ZERO_WORDS
+                    if (m != 0) {  // wave-uniform (SGPR word): an empty chunk costs no VALU
+                        append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_lst + 2u * (unsigned)ncand,
+                                      (unsigned)lane + 64u * (unsigned)(c0 + q));
+                        ncand += __popcll(m);
+                    }
+#else
                     append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_lst + 2u * (unsigned)ncand, idx);
                     ncand += __popcll(m);
                     idx += 64;
+#endif
                 }
             }
         } else {
