@@ -378,6 +378,9 @@ struct Queue {
     int cap;
 };
 
+#ifndef MCPT_ROOT_MINOR
+#define MCPT_ROOT_MINOR -1  // -1 auto (by acceleration-structure size), 0 sample-major, 1 sample-minor
+#endif
 struct Params {
     DScene S;
     uint64_t seed;
@@ -545,8 +548,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 }
 
 // roots: r in [0, nroots): pixel = r % npx, sample = s0 + r / npx
+// nminor > 0: sample-minor root order (the call's nminor samples of a pixel are consecutive roots,
+// so their rays leave one point: coherent traversal of a BVH that misses L2); else sample-major
 __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
-                                               int s0, long long rbase, int nroots, Queue q) {
+                                               int s0, long long rbase, int nroots, Queue q, int nminor) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int npx = cam.W * cam.H;
     bool active = r < nroots;
@@ -554,9 +559,9 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
     double beta = 0, gamma = 0;
     d3 wo = mk3(0, 0, 0);
     if (active) {
-        const long long rg = rbase + r;  // global root index: sample-major over the frame
-        pixel = (int)(rg % npx);
-        sample = s0 + (int)(rg / npx);
+        const long long rg = rbase + r;  // root index within the call
+        pixel = nminor > 0 ? (int)(rg / nminor) : (int)(rg % npx);
+        sample = s0 + (nminor > 0 ? (int)(rg % nminor) : (int)(rg / npx));
         f = hit_f[pixel];
         active = f >= 0;
         if (active) {
@@ -2801,6 +2806,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // is large until the final drain; roots are taken in global order r = (sample - s0) * npx +
     // pixel.  samples_per_launch (if set) sets target = samples_per_launch * npx.
     const long long R = (long long)(s1 - s0) * npx;
+    // root order: sample-minor when the acceleration structures exceed an XCD's 4 MiB L2 (the
+    // secondary rays of consecutive roots then share their origin and top-down paths: C5 +10%),
+    // sample-major otherwise (Veach: the root-point cache's per-pixel reads spread; -3% minor)
+    const uint64_t accel = (uint64_t)(D.d.nbvh4 + D.d.nlbvh4) * sizeof(BvhNode4) +
+                           (uint64_t)(sc->bvh.leaf_facets.size() + sc->lbvh.leaf_facets.size()) * 3 * sizeof(float4);
+    const int nminor = (MCPT_ROOT_MINOR > 0 || (MCPT_ROOT_MINOR < 0 && accel > (4ull << 20))) ? s1 - s0 : 0;
     const long long target_ll = o->samples_per_launch > 0 ? (long long)o->samples_per_launch * npx : (4ll << 20);
     if (target_ll > (1ll << 29)) {
         set_error("batch too large");
@@ -2992,7 +3003,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (rnext < R && n < (unsigned)fill) {  // refill with roots (appended through node_entry)
             const int m = (int)std::min<long long>((long long)fill - n, R - rnext);
             hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
-                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur);
+                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur, nminor);
             HIP_OK(hipGetLastError());
             rnext += m;
             if ((rc = read_count(&n))) return rc;

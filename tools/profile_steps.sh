@@ -11,6 +11,7 @@ exec tools/gpu_steps.sh \
  "300:bench_shade_area:python3 bench.py --mode shade_area --no-cpu" \
  "300:bench_cornell:python3 bench.py --scene cornell1m --no-cpu" \
  "300:bench_fresh:python3 bench.py --fresh-pdf --no-cpu" \
+ "300:bench_fp32:python3 bench.py --precision fp32 --no-cpu" \
  "300:bench_c4shard:python3 bench.py --width 1600 --height 1200 --steps 2 --no-cpu" \
  "300:bench_torchrun1:python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --no-cpu" \
  "300:prof:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T} -o run --output-format csv -- python3 bench.py --no-cpu" \
