@@ -279,7 +279,8 @@ def main():
             "bound": "valu_fp64", "kernel": "k_prep_cull_lanes+k_prep_pk2", "achieved": round(achieved, 3),
             "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": tsrc,
-            "valu_busy": busy("k_prep_cull_lanes<false>", "k_prep_pk2<5, false, true>"),
+            "valu_busy": busy("k_prep_cull_lanes<false>",
+                              "k_prep_pk2<5, false, true, %s>" % ("true" if args.precision == "fp32" else "false")),
             "valu_busy_source": pmc.get("source"),
             "hbm_frac_algorithmic": round(alg_gbs / HBM_PEAK_GBS, 5),
             "hbm_frac_measured": round(traffic / t_launch / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
