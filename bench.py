@@ -165,6 +165,9 @@ def main():
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
                     help="light-prep precision: fp64 (the reference's, the headline) or the opt-in FP32_STABLE mode "
                          "(MCPT_RENDER_PRECISION_FP32: packed-fp32 weights summed in fp64)")
+    ap.add_argument("--no-root-cache", action="store_true",
+                    help="disable the per-pixel root-point light-prep cache (MCPT_DEBUG_NO_ROOT_CACHE): every root runs "
+                         "the full O(N_L) prep, the regime of frames whose cache exceeds the HBM budget")
     ap.add_argument("--out", default="", help="optional .bmp of the rendered frame (rank 0)")
     args = ap.parse_args()
 
@@ -202,7 +205,8 @@ def main():
     scratch = torch.zeros_like(fb)
 
     mode_flags = (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0) | (
-        mcpt.RENDER_PRECISION_FP32 if args.precision == "fp32" else 0)
+        mcpt.RENDER_PRECISION_FP32 if args.precision == "fp32" else 0) | (
+        mcpt.DEBUG_NO_ROOT_CACHE if args.no_root_cache else 0)
     flags = mcpt.RENDER_NO_BACKFACE_STATS | mode_flags
     for k in range(args.warmup):  # warmup renders (same kernels and flags as the timed steps) go to scratch
         mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
@@ -340,7 +344,7 @@ def main():
         "config": {"workload": "%s %s %dx%d" % ("veach-mis" if args.scene == "veach" else "cornell-1M", args.mode.upper(), W, H),
                    "width": W, "height": H,
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
-                   "precision": args.precision,
+                   "precision": args.precision, "root_cache": not args.no_root_cache,
                    "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world},
         "roofline": roofline,
         "roofline_prep": roof_prep,

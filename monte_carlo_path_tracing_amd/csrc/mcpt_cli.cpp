@@ -6,11 +6,13 @@
 //
 //   mcpt_render --scene scenes/veach-mis/veach-mis [--width 1280 --height 720] [--spp 10]
 //               [--mode mis|brdf|shade|shade-area] [--seed 20240430] [--out test.bmp] [--hdr out.pfm] [--progress]
-//               [--grid] [--devices 0,1,2,3,4,5,6,7]
+//               [--grid] [--devices 0,1,2,3,4,5,6,7] [--precision fp64|fp32]
 //   --devices renders on several GPUs of this node: the sample range is split into one contiguous shard
 //   per listed device, rendered concurrently, and summed by ONE RCCL reduce into the first device
 //   (mcpt_render_opts.devices; the reference itself is single-threaded, README.md:418).
 //   --grid traverses the reference's uniform grid (Myobj.cpp:78-162, n0 = 100000) instead of the BVH.
+//   --precision fp32 selects the opt-in FP32_STABLE light prep (MCPT_RENDER_PRECISION_FP32); fp64 (the
+//   reference's, default) otherwise.
 //   --progress prints the share of camera samples dispatched (the reference prints per-row progress
 //   and updates its EasyX window, main.cpp:539-592) through mcpt_render_opts.progress.
 #include <chrono>
@@ -36,7 +38,7 @@ int print_progress(void* user, uint64_t done, uint64_t total) {
 }
 
 // render(scene, camera, spp, mode): main.cpp:547-588 lifted into a function.
-int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, bool progress, bool grid,
+int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_t seed, bool progress, bool grid, int flags,
            const std::vector<int32_t>& devices, std::vector<double>& hdr, mcpt_stats* st) {
     hdr.assign(3ull * cam.width * cam.height, 0.0);
     mcpt_render_opts o;
@@ -45,6 +47,7 @@ int render(mcpt_scene* scene, const mcpt_camera& cam, int spp, int mode, uint64_
     o.mode = mode;
     o.seed = seed;
     o.accel = grid ? MCPT_ACCEL_GRID : MCPT_ACCEL_BVH;
+    o.flags = flags;
     if (!devices.empty()) {  // one process, several GPUs: shards + one RCCL reduce
         o.num_devices = (int32_t)devices.size();
         o.devices = devices.data();
@@ -78,6 +81,7 @@ int main(int argc, char** argv) {
     double dist_scale = 2.0;
     uint64_t seed = 20240430;
     bool xml_cam = false, progress = false, grid = false;
+    int flags = 0;
     std::vector<int32_t> devices;
     for (int a = 1; a < argc; a++) {
         auto next = [&]() -> const char* {
@@ -109,6 +113,14 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[a], "--xml-camera")) xml_cam = true;
         else if (!std::strcmp(argv[a], "--progress")) progress = true;
         else if (!std::strcmp(argv[a], "--grid")) grid = true;
+        else if (!std::strcmp(argv[a], "--precision")) {
+            const char* v = next();
+            if (!std::strcmp(v, "fp32")) flags |= MCPT_RENDER_PRECISION_FP32;
+            else if (std::strcmp(v, "fp64")) {
+                std::fprintf(stderr, "--precision: fp64 or fp32, not %s\n", v);
+                return 2;
+            }
+        }
         else if (!std::strcmp(argv[a], "--devices")) {
             for (const char* p = next(); *p;) {
                 char* e = nullptr;
@@ -147,7 +159,7 @@ int main(int argc, char** argv) {
     std::vector<double> hdr;
     mcpt_stats st{};
     const auto t0 = std::chrono::steady_clock::now();
-    if (render(scene, cam, spp, mode, seed, progress, grid, devices, hdr, &st) != MCPT_OK) {
+    if (render(scene, cam, spp, mode, seed, progress, grid, flags, devices, hdr, &st) != MCPT_OK) {
         std::fprintf(stderr, "render failed: %s\n", mcpt_last_error());
         return 1;
     }

@@ -58,6 +58,18 @@ def test_cli_grid_and_progress(tmp_path):
     assert np.allclose(hdr, ref.astype(np.float32), rtol=1e-6, atol=1e-30)
 
 
+def test_cli_precision_fp32(tmp_path):
+    """--precision fp32 = MCPT_RENDER_PRECISION_FP32 (the opt-in FP32_STABLE light prep)"""
+    r, _, pfm = run_cli(tmp_path, "--width", "48", "--height", "36", "--spp", "4", "--mode", "mis", "--precision", "fp32")
+    assert r.returncode == 0, r.stderr
+    hdr = read_pfm(pfm)
+    scene = mcpt.Scene.load(SCENE_OBJ, SCENE_XML)
+    ref, _ = mcpt.render(scene, mcpt.Camera.reference(48, 36), 4, flags=mcpt.RENDER_PRECISION_FP32)
+    assert np.allclose(hdr, ref.astype(np.float32), rtol=1e-6, atol=1e-30)
+    r = subprocess.run([CLI, "--precision", "fp16"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+
+
 def test_cli_errors(tmp_path):
     r = subprocess.run([CLI, "--scene", str(tmp_path / "missing")], capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "scene load failed" in r.stderr
