@@ -71,6 +71,25 @@ def test_more_than_4096_candidates(tmp_path, mode, spp):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nx", [20, 32, 40, 60])
+def test_root_cache_pick_paths(tmp_path, nx):
+    """Light panels of 2 nx^2 triangles that every floor point sees: <= 16 (nx 20), <= 32 (32),
+    <= 64 (40) and > 64 (60) candidate batches per root, i.e. every batch-search path of k_prep_pick
+    (four roots per wave scan, two, one, sequential).  The root-point cache must give the frame the
+    full prep gives (MCPT_DEBUG_NO_ROOT_CACHE) up to fp64 accumulation order, and the oracle's."""
+    obj, xml = scenegen.light_panel(str(tmp_path), nx, nx)
+    s = mcpt.Scene.load(obj, xml)
+    g = s.camera()
+    g.width, g.height = 24, 18
+    a, sa = mcpt.render(s, g, 4, mode="mis", seed=SEED)
+    b, sb = mcpt.render(s, g, 4, mode="mis", seed=SEED, flags=mcpt.DEBUG_NO_ROOT_CACHE)
+    assert sa.prep_cached_nodes > 0 and sb.prep_cached_nodes == 0
+    assert a.sum() > 0 and rel_l2(a, b) <= 1e-12, rel_l2(a, b)
+    img, ref, _ = pair(obj, xml, 24, 18, 4, "mis")
+    assert rel_l2(img, ref) <= L2_TOL, rel_l2(img, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["mis", "shade"])
 def test_light_table_beyond_the_lds_list(tmp_path, mode):
     """N_L = 14160 > 7680: the LDS-queue prep variant, no root-point cache"""
