@@ -297,15 +297,19 @@ def main():
     tr_s, tr_n = totals.get("trace_seconds", 0.0), max(totals.get("trace_launches", 0), 1)
     visits, tests = totals.get("node_visits", 0), totals.get("tri_tests", 0)
     if tr_s > 0 and visits > 0:
-        kname = "k_extend_brdf" if args.mode == "brdf" else "k_mis_rays"
+        accel = scene.accel_bytes()
+        # the library traces MIS / shade rays with persistent refilling waves when the BVHs exceed an
+        # XCD's 4 MiB L2 (render.hip MCPT_RAYS_PERSISTENT), one ray per thread otherwise
+        pers = accel > (4 << 20)
+        kname = "k_extend_brdf" if args.mode == "brdf" else ("k_rays_persistent" if pers else "k_mis_rays")
         t_launch = tr_s / tr_n
         fl = (visits * FLOPS_NODE_VISIT + tests * FLOPS_TRI_TEST_FP64 * 2) / tr_n
         by = (visits * BYTES_NODE_VISIT + tests * BYTES_TRI_TEST) / tr_n
-        accel = scene.accel_bytes()
         _, level, mem_peak = next(g for g in GATHER_PEAKS if accel <= g[0])
         v_frac, h_frac = fl / t_launch / 1e12 / FP32_VECTOR_PEAK_TFLOPS, by / t_launch / 1e9 / mem_peak
         valu_bound = v_frac >= h_frac
-        pk_name = "k_extend_brdf<false>" if args.mode == "brdf" else "k_mis_rays<false, false>"
+        pk_name = ("k_extend_brdf<false>" if args.mode == "brdf" else
+                   "k_rays_persistent<false>" if pers else "k_mis_rays<false, false>")
         hbm_meas = pk.get(pk_name, {}).get("hbm_bytes_per_dispatch")
         roof_trace = {
             "bound": "valu" if valu_bound else level, "kernel": kname,

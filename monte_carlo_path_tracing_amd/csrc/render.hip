@@ -378,6 +378,14 @@ struct Queue {
     int cap;
 };
 
+// the ray sets of a generation: persistent waves with ray refill (k_rays_persistent) over the BVH,
+// one thread per ray (k_mis_rays) over the reference grid
+// (-1 auto: persistent when the acceleration structures exceed an XCD's 4 MiB L2 -- long, cache-
+// missing rays: Cornell-1M traversal -13%, the frame +9%; Veach's short L2-resident rays run 5%
+// faster one per thread at 8 waves/SIMD; profiles/round2b_ab_rays_persistent.txt)
+#ifndef MCPT_RAYS_PERSISTENT
+#define MCPT_RAYS_PERSISTENT -1
+#endif
 #ifndef MCPT_ROOT_MINOR
 #define MCPT_ROOT_MINOR -1  // -1 auto (by acceleration-structure size), 0 sample-major, 1 sample-minor
 #endif
@@ -1935,6 +1943,194 @@ __device__ inline int block_alloc_slot(const Slots& T, bool want) {
     return slot;
 }
 
+// The same three ray sets as k_mis_rays, traced by PERSISTENT waves that refill lanes whose ray has
+// finished with the next ray of a shared pool (Aila & Laine's persistent while-while with dynamic
+// ray fetch): a wave of one-ray-per-lane runs as long as its longest ray, and rays differ ~10x in
+// length (and a ray set's untraced nodes leave lanes idle from the start).  Pool item t = set-major
+// (t / n = set - first_set, t % n = node); a wave fetches items for all its idle lanes with one
+// atomic once at least kRefill lanes are idle; items whose set is not flagged for their node are
+// answered (-1) at once.  Each round is one iteration of trace4_ww's outer loop for every lane in
+// flight; the per-lane state (ray, stack pointer, LDS + private stack, best hit) lives across
+// rounds.  Hits are bit-identical to k_mis_rays (the closest hit, ties to the lower facet id, by the
+// same tests on conservatively pruned boxes); only the order of visits, and so their count, differs.
+constexpr int kRefill = 16;
+constexpr int kRayChunk = 256;  // pool items a wave takes per atomic
+template <bool kCount = false>
+#ifndef MCPT_RAYS_WAVES
+#define MCPT_RAYS_WAVES 6
+#endif
+__global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(DScene S, Queue cur, int n, Aux A, int first_set,
+                                                                  int nsets, unsigned* __restrict__ pool,
+                                                                  unsigned long long* cnt = nullptr) {
+    constexpr int kDone = 0x7fffffff;
+    __shared__ int stack[kRayTopLds * kRayBlock];
+    int* __restrict__ lds = stack + threadIdx.x;
+    constexpr int stride = kRayBlock;
+    const int lane = threadIdx.x & 63;
+    const unsigned total = (unsigned)nsets * (unsigned)n;
+    int spill[kStack - kRayTopLds];
+    unsigned visits = 0, tests = 0;
+    bool busy = false, exhausted = false;
+    unsigned wnext = 0, wend = 0;  // the wave's private range of pool items (wave-uniform)
+    int set = 0, ii = 0, excl = -1;
+    d3 ro = mk3(0, 0, 0), rd = mk3(0, 0, 0);
+    float ix = 0, iy = 0, iz = 0, oix = 0, oiy = 0, oiz = 0, tlimit = FLT_MAX;
+    int sp = 0, node = kDone, leaf = 0;
+    Hit best{-1, DBL_MAX, 0, 0};
+    auto push = [&](int v) {
+        if (sp < kRayTopLds) lds[sp * stride] = v;
+        else if (sp < kStack) spill[sp - kRayTopLds] = v;
+        sp = sp < kStack ? sp + 1 : sp;
+    };
+    auto pop = [&]() -> int {
+        if (sp == 0) return kDone;
+        --sp;
+        return sp < kRayTopLds ? lds[sp * stride] : spill[sp - kRayTopLds];
+    };
+    auto finish = [&]() {  // the lane's ray is done: store its hit
+        const size_t o = (size_t)set * A.cap + ii;
+        A.hf[o] = best.f;
+        if (set < 2) {
+            A.hbg[2 * o] = best.beta;
+            A.hbg[2 * o + 1] = best.gamma;
+        }
+        busy = false;
+    };
+    while (true) {
+        // refill the idle lanes (all of them at the start, then whenever kRefill are idle) from the
+        // wave's private chunk of kRayChunk consecutive items; one pool atomic per chunk (a single
+        // counter word saturates at ~88 atomics per us)
+        while (!exhausted) {
+            const uint64_t idle = __ballot(!busy);
+            if (idle == 0 || (__popcll(idle) < kRefill && __ballot(busy) != 0)) break;
+            if (wnext >= wend) {
+                unsigned base = 0;
+                if (lane == 0) base = atomicAdd(pool, (unsigned)kRayChunk);
+                base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+                if (base >= total) {
+                    exhausted = true;
+                    break;
+                }
+                wnext = base;
+                wend = min(base + (unsigned)kRayChunk, total);
+            }
+            const unsigned take = min((unsigned)__popcll(idle), wend - wnext);
+            const unsigned rk = (unsigned)lane_rank(idle);
+            const unsigned base = wnext;
+            wnext += take;
+            if (!busy && rk < take) {
+                const unsigned it = base + rk;
+                {
+                    set = first_set + (int)(it / (unsigned)n);
+                    ii = (int)(it % (unsigned)n);
+                    best = Hit{-1, DBL_MAX, 0, 0};
+                    if (A.flags[ii] & (1 << set)) {
+                        const double* d = set == 0 ? A.d1 : A.d2;
+                        ro = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
+                        rd = mk3(d[3 * ii], d[3 * ii + 1], d[3 * ii + 2]);
+                        excl = cur.f[ii];
+                        if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) {  // reference: UB (Myobj.cpp:463-468)
+                            finish();
+                        } else {
+                            auto inv = [](double v) {
+                                float f = (float)v;
+                                if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
+                                return 1.0f / f;
+                            };
+                            ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
+                            oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
+                            tlimit = FLT_MAX;
+                            sp = 0;
+                            node = 0;
+                            leaf = 0;
+                            busy = true;
+                        }
+                    } else {
+                        finish();  // this set is not traced for this node: no hit
+                    }
+                }
+            }
+        }
+        if (__ballot(busy) == 0) break;  // pool exhausted and no ray in flight
+        // one round of trace4_ww's outer loop on every lane in flight
+        if (busy) {
+            const BvhNode4* __restrict__ nodes = set == 2 ? S.lbvh4 : S.bvh4;
+            const float4* __restrict__ leafv = set == 2 ? S.lleaf_v : S.leaf_v;
+            while (node >= 0 && node != kDone) {
+                if (kCount) ++visits;
+                const BvhNode4* nd = nodes + node;
+                const float4 lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
+                             lz = *reinterpret_cast<const float4*>(nd->lo[2]);
+                const float4 hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
+                             hz = *reinterpret_cast<const float4*>(nd->hi[2]);
+                const int4 ch = *reinterpret_cast<const int4*>(nd->child);
+                const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, lys[4] = {ly.x, ly.y, ly.z, ly.w}, lzs[4] = {lz.x, lz.y, lz.z, lz.w};
+                const float hxs[4] = {hx.x, hx.y, hx.z, hx.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
+                const int chs[4] = {ch.x, ch.y, ch.z, ch.w};
+                float t[4];
+                int code[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float tx0 = fmaf(lxs[k], ix, -oix), tx1 = fmaf(hxs[k], ix, -oix);
+                    const float ty0 = fmaf(lys[k], iy, -oiy), ty1 = fmaf(hys[k], iy, -oiy);
+                    const float tz0 = fmaf(lzs[k], iz, -oiz), tz1 = fmaf(hzs[k], iz, -oiz);
+                    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+                    const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
+                    t[k] = h ? t0 : FLT_MAX;
+                    code[k] = h ? chs[k] : kDone;
+                }
+                auto cs = [&](int a, int b) {
+                    const bool sw = t[b] < t[a];
+                    const float ta = t[a], tb = t[b];
+                    const int ca = code[a], cb = code[b];
+                    t[a] = sw ? tb : ta, t[b] = sw ? ta : tb;
+                    code[a] = sw ? cb : ca, code[b] = sw ? ca : cb;
+                };
+                cs(0, 1), cs(2, 3), cs(0, 2), cs(1, 3), cs(1, 2);
+                if (code[3] != kDone) push(code[3]);
+                if (code[2] != kDone) push(code[2]);
+                if (code[1] != kDone) push(code[1]);
+                node = code[0] != kDone ? code[0] : pop();
+                if (node < 0 && leaf >= 0) {  // postpone the leaf, keep descending
+                    leaf = node;
+                    node = pop();
+                }
+                if (!__any(leaf >= 0)) break;
+            }
+            while (leaf < 0) {
+                const int packed = ~leaf, first = packed >> kLeafBits, cnt4 = packed & ((1 << kLeafBits) - 1);
+                for (int q = first; q < first + cnt4; q++) {
+                    const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
+                    const int fac = __float_as_int(a4.w);
+                    if (fac == excl) continue;
+                    if (kCount) ++tests;
+                    const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
+                    const double detA = det3(ab, ac, rd);
+                    if (fabs(detA) < MCPT_EPS) continue;
+                    const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
+                    const bool neg = detA < 0;
+                    if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
+                        continue;
+                    const double beta = nb / detA, gamma = ng / detA, tt = nt / detA;
+                    if (beta < 0 || gamma < 0 || beta + gamma > 1 || tt < 0 || fabs(tt) < MCPT_EPS) continue;
+                    if (tt < best.t || (tt == best.t && fac < best.f)) {
+                        best.f = fac;
+                        best.t = tt;
+                        best.beta = beta;
+                        best.gamma = gamma;
+                        tlimit = (float)tt * 1.0001f + 1e-5f;
+                    }
+                }
+                leaf = node;
+                if (node < 0) node = pop();
+            }
+            if (!(node != kDone || leaf < 0)) finish();
+        }
+    }
+    if (kCount) wave_count2(cnt, visits, cnt + 1, tests);
+}
+
 template <bool kStale>
 __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
@@ -2830,6 +3026,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // keeps the single kernel (one ray per node; measured faster).  A/B switches:
     const bool count_trav = (o->flags & MCPT_DEBUG_COUNT_TRAVERSAL) != 0;
 #define K_MIS_RAYS (grid ? k_mis_rays<true> : count_trav ? k_mis_rays<false, true> : k_mis_rays<false>)
+
     const bool split_brdf = (o->flags & MCPT_DEBUG_SPLIT_BRDF) != 0;
     // the O(N_L) light prep runs for shade_with_mis and for shade() with the spherical sampler
     const bool needs_prep = o->mode == MCPT_MODE_MIS || o->mode == MCPT_MODE_SHADE;
@@ -3061,12 +3258,29 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
         const dim3 g256((ni + 255) / 256), b256(256);
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
+    auto launch_rays = [&](int first_set, int nsets) {
+        const bool pers = MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
+        if (pers && !grid && kRayTop == 0) {
+            unsigned* pool = (unsigned*)D.work.p + 8;
+            (void)hipMemsetAsync(pool, 0, sizeof(unsigned), st);
+            const long long items = (long long)nsets * ni;
+            const int blocks = (int)std::max<long long>(1, std::min<long long>((items + kRayBlock - 1) / kRayBlock, 2048));
+            if (count_trav)
+                hipLaunchKernelGGL(k_rays_persistent<true>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux,
+                                   first_set, nsets, pool, tcnt);
+            else
+                hipLaunchKernelGGL(k_rays_persistent<false>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux,
+                                   first_set, nsets, pool, tcnt);
+        } else {
+            hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, nsets), dim3(kRayBlock), 0, st, D.d,
+                               *cur, ni, aux, first_set, tcnt);
+        }
+    };
         // trace_seconds: HIP events around the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf)
         if (!fused && o->mode == MCPT_MODE_MIS) {
             hipLaunchKernelGGL(stale ? k_mis_gen<true> : k_mis_gen<false>, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 3), dim3(kRayBlock), 0, st, D.d, *cur,
-                               ni, aux, 0, tcnt);
+            launch_rays(0, 3);
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(stale ? k_mis_combine<true> : k_mis_combine<false>, g256, b256, 0, st, P, *cur, ni, aux,
                                *nxt, T, rp);
@@ -3078,15 +3292,13 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         } else if (!fused && (o->mode == MCPT_MODE_SHADE || o->mode == MCPT_MODE_SHADE_AREA)) {
             hipLaunchKernelGGL(k_shade_gen, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 2), dim3(kRayBlock), 0, st, D.d, *cur,
-                               ni, aux, 0, tcnt);
+            launch_rays(0, 2);
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(k_shade_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else if (!fused) {
             hipLaunchKernelGGL(k_brdf_gen, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, 1), dim3(kRayBlock), 0, st, D.d, *cur,
-                               ni, aux, 1, tcnt);
+            launch_rays(1, 1);
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(k_brdf_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else {
