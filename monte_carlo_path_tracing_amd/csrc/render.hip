@@ -147,11 +147,15 @@ constexpr int kRayBlock = 256;
 constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB per 256 lanes)
 // k_mis_rays: the first kRayTop nodes of the traversed BVH4 (breadth-first numbering: its top
 // levels) staged in LDS per workgroup; 0 = off.  A/B builds: -DMCPT_RAY_TOP=N -DMCPT_RAY_LDS=M.
+// k_mis_rays stages the BVH's top four levels (1 + 4 + 16 + 64 = 85 nodes, 10.9 KB) in LDS per
+// block and reads them with ds_read when the whole wave is in them, with an 8-entry LDS stack per
+// lane (same-box A/B on Veach, profiles/round2b_ab_ray_top.txt: traversal 0.82-0.84 -> 0.735-0.745 ms
+// per launch; 21 nodes: 0.76; the earlier per-lane generic-pointer select: 0.79-0.84)
 #ifndef MCPT_RAY_TOP
-#define MCPT_RAY_TOP 0
+#define MCPT_RAY_TOP 85
 #endif
 #ifndef MCPT_RAY_LDS
-#define MCPT_RAY_LDS 16
+#define MCPT_RAY_LDS 8
 #endif
 constexpr int kRayTop = MCPT_RAY_TOP;
 constexpr int kRayTopLds = MCPT_RAY_LDS;
@@ -212,12 +216,19 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     while (node != kDone || leaf < 0) {
         while (node >= 0 && node != kDone) {
             if (kCount) ++*visits;
-            const BvhNode4* nd = (kTop > 0 && node < kTop) ? top + node : nodes + node;
-            const float4 lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
-                         lz = *reinterpret_cast<const float4*>(nd->lo[2]);
-            const float4 hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
-                         hz = *reinterpret_cast<const float4*>(nd->hi[2]);
-            const int4 ch = *reinterpret_cast<const int4*>(nd->child);
+            float4 lx, ly, lz, hx, hy, hz;
+            int4 ch;
+            auto fetch = [&](const BvhNode4* nd) {
+                lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
+                lz = *reinterpret_cast<const float4*>(nd->lo[2]);
+                hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
+                hz = *reinterpret_cast<const float4*>(nd->hi[2]);
+                ch = *reinterpret_cast<const int4*>(nd->child);
+            };
+            // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch,
+            // so each side reads one address space: ds_read from the LDS copy, global loads else)
+            if (kTop > 0 && __all(node < kTop)) fetch(top + node);
+            else fetch(nodes + node);
             const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, lys[4] = {ly.x, ly.y, ly.z, ly.w}, lzs[4] = {lz.x, lz.y, lz.z, lz.w};
             const float hxs[4] = {hx.x, hx.y, hx.z, hx.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
             const int chs[4] = {ch.x, ch.y, ch.z, ch.w};
@@ -1963,12 +1974,12 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                                                                   int nsets, unsigned* __restrict__ pool,
                                                                   unsigned long long* cnt = nullptr) {
     constexpr int kDone = 0x7fffffff;
-    __shared__ int stack[kRayTopLds * kRayBlock];
+    __shared__ int stack[kRayLds * kRayBlock];
     int* __restrict__ lds = stack + threadIdx.x;
     constexpr int stride = kRayBlock;
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)nsets * (unsigned)n;
-    int spill[kStack - kRayTopLds];
+    int spill[kStack - kRayLds];
     unsigned visits = 0, tests = 0;
     bool busy = false, exhausted = false;
     unsigned wnext = 0, wend = 0;  // the wave's private range of pool items (wave-uniform)
@@ -1978,14 +1989,14 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
     int sp = 0, node = kDone, leaf = 0;
     Hit best{-1, DBL_MAX, 0, 0};
     auto push = [&](int v) {
-        if (sp < kRayTopLds) lds[sp * stride] = v;
-        else if (sp < kStack) spill[sp - kRayTopLds] = v;
+        if (sp < kRayLds) lds[sp * stride] = v;
+        else if (sp < kStack) spill[sp - kRayLds] = v;
         sp = sp < kStack ? sp + 1 : sp;
     };
     auto pop = [&]() -> int {
         if (sp == 0) return kDone;
         --sp;
-        return sp < kRayTopLds ? lds[sp * stride] : spill[sp - kRayTopLds];
+        return sp < kRayLds ? lds[sp * stride] : spill[sp - kRayLds];
     };
     auto finish = [&]() {  // the lane's ray is done: store its hit
         const size_t o = (size_t)set * A.cap + ii;
@@ -2436,10 +2447,25 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
 }
 
 // one BRDF-only path vertex (main.cpp:385-396)
+// BRDF-only extension: 256-thread blocks with the BVH4's top levels in LDS (MCPT_BRDF_TOP nodes, 0 =
+// none: 128-thread blocks with a 16-entry stack)
+#ifndef MCPT_BRDF_TOP
+#define MCPT_BRDF_TOP 21
+#endif
+constexpr int kBrdfTop = MCPT_BRDF_TOP;
+constexpr int kBrdfBlock = kBrdfTop > 0 ? 256 : kTraceBlock;
+constexpr int kBrdfLds = kBrdfTop > 0 ? 8 : kRayLds;
 template <bool kCount = false>
-__global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
-    __shared__ int stack[kRayLds * kTraceBlock];
+__global__ __launch_bounds__(kBrdfBlock) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
+    __shared__ int stack[kBrdfLds * kBrdfBlock];
+    __shared__ BvhNode4 top[kBrdfTop > 0 ? kBrdfTop : 1];
     const DScene& S = P.S;
+    if (kBrdfTop > 0) {  // the tree's top levels into LDS (as k_mis_rays)
+        const int cnt4 = min(kBrdfTop, S.nbvh4) * (int)(sizeof(BvhNode4) / sizeof(float4));
+        for (int k = threadIdx.x; k < cnt4; k += blockDim.x)
+            reinterpret_cast<float4*>(top)[k] = reinterpret_cast<const float4*>(S.bvh4)[k];
+        __syncthreads();
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
     const int ii = active ? i : 0;
@@ -2462,7 +2488,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_brdf(Params P, Queue cur
         wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
         if (!(dot(wi, N) < 0)) {
             traced = 1;
-            h = trace4_ww<kRayLds, kCount>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kTraceBlock, &visits, &tests);
+            h = trace4_ww<kBrdfLds, kCount, kBrdfTop>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
+                                                      &tests, top);
             if (h.f >= 0) {
                 const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
                 tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
@@ -3260,7 +3287,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
     auto launch_rays = [&](int first_set, int nsets) {
         const bool pers = MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
-        if (pers && !grid && kRayTop == 0) {
+        if (pers && !grid) {
             unsigned* pool = (unsigned*)D.work.p + 8;
             (void)hipMemsetAsync(pool, 0, sizeof(unsigned), st);
             const long long items = (long long)nsets * ni;
@@ -3303,8 +3330,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             hipLaunchKernelGGL(k_brdf_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else {
             HIP_OK(hipEventRecord(D.evr0, st));
-            hipLaunchKernelGGL(count_trav ? k_extend_brdf<true> : k_extend_brdf<false>, dim3((ni + kTraceBlock - 1) / kTraceBlock),
-                               dim3(kTraceBlock), 0, st, P, *cur, ni, *nxt);
+            hipLaunchKernelGGL(count_trav ? k_extend_brdf<true> : k_extend_brdf<false>, dim3((ni + kBrdfBlock - 1) / kBrdfBlock),
+                               dim3(kBrdfBlock), 0, st, P, *cur, ni, *nxt);
             HIP_OK(hipEventRecord(D.evr1, st));
         }
         HIP_OK(hipGetLastError());
