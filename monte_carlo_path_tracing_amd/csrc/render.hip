@@ -397,6 +397,9 @@ struct Queue {
 #ifndef MCPT_RAYS_PERSISTENT
 #define MCPT_RAYS_PERSISTENT -1
 #endif
+#ifndef MCPT_ROOT_GROUP
+#define MCPT_ROOT_GROUP 2  // small scenes: consecutive roots take this many samples of a pixel (A/B: 1 / 2 / 4 / 8 -> 437 / 442 / 437 / 430)
+#endif
 #ifndef MCPT_ROOT_MINOR
 #define MCPT_ROOT_MINOR -1  // -1 auto (by acceleration-structure size), 0 sample-major, 1 sample-minor
 #endif
@@ -567,10 +570,12 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 }
 
 // roots: r in [0, nroots): pixel = r % npx, sample = s0 + r / npx
-// nminor > 0: sample-minor root order (the call's nminor samples of a pixel are consecutive roots,
-// so their rays leave one point: coherent traversal of a BVH that misses L2); else sample-major
+// root order: the call's nsamp samples in blocks of `group` consecutive samples; within a block,
+// pixel-major with the block's samples of a pixel consecutive (group 1 = sample-major over the frame,
+// group nsamp = fully sample-minor: a pixel's samples leave one point, coherent traversal of a BVH
+// that misses L2)
 __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
-                                               int s0, long long rbase, int nroots, Queue q, int nminor) {
+                                               int s0, long long rbase, int nroots, Queue q, int group, int nsamp) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int npx = cam.W * cam.H;
     bool active = r < nroots;
@@ -579,8 +584,17 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
     d3 wo = mk3(0, 0, 0);
     if (active) {
         const long long rg = rbase + r;  // root index within the call
-        pixel = nminor > 0 ? (int)(rg / nminor) : (int)(rg % npx);
-        sample = s0 + (nminor > 0 ? (int)(rg % nminor) : (int)(rg / npx));
+        const long long full = (long long)(nsamp / group) * group * npx;  // roots in whole blocks
+        if (rg < full) {
+            const long long blk = rg / ((long long)group * npx), idx = rg - blk * group * npx;
+            pixel = (int)(idx / group);
+            sample = s0 + (int)blk * group + (int)(idx % group);
+        } else {
+            const int gt = nsamp % group;
+            const long long idx = rg - full;
+            pixel = (int)(idx / gt);
+            sample = s0 + (nsamp / group) * group + (int)(idx % gt);
+        }
         f = hit_f[pixel];
         active = f >= 0;
         if (active) {
@@ -3034,7 +3048,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // sample-major otherwise (Veach: the root-point cache's per-pixel reads spread; -3% minor)
     const uint64_t accel = (uint64_t)(D.d.nbvh4 + D.d.nlbvh4) * sizeof(BvhNode4) +
                            (uint64_t)(sc->bvh.leaf_facets.size() + sc->lbvh.leaf_facets.size()) * 3 * sizeof(float4);
-    const int nminor = (MCPT_ROOT_MINOR > 0 || (MCPT_ROOT_MINOR < 0 && accel > (4ull << 20))) ? s1 - s0 : 0;
+    const int nminor = (MCPT_ROOT_MINOR > 0 || (MCPT_ROOT_MINOR < 0 && accel > (4ull << 20))) ? s1 - s0
+                                                                                              : std::min(MCPT_ROOT_GROUP, s1 - s0);
     const long long target_ll = o->samples_per_launch > 0 ? (long long)o->samples_per_launch * npx : (4ll << 20);
     if (target_ll > (1ll << 29)) {
         set_error("batch too large");
@@ -3227,7 +3242,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (rnext < R && n < (unsigned)fill) {  // refill with roots (appended through node_entry)
             const int m = (int)std::min<long long>((long long)fill - n, R - rnext);
             hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
-                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur, nminor);
+                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0);
             HIP_OK(hipGetLastError());
             rnext += m;
             if ((rc = read_count(&n))) return rc;
