@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--no-root-cache", action="store_true",
                     help="disable the per-pixel root-point light-prep cache (MCPT_DEBUG_NO_ROOT_CACHE): every root runs "
                          "the full O(N_L) prep, the regime of frames whose cache exceeds the HBM budget")
+    ap.add_argument("--debug-flags", type=lambda v: int(v, 0), default=0,
+                    help="extra mcpt_render_opts.flags bits of include/mcpt_debug.h (A/B experiments)")
     ap.add_argument("--out", default="", help="optional .bmp of the rendered frame (rank 0)")
     args = ap.parse_args()
 
@@ -206,7 +208,7 @@ def main():
 
     mode_flags = (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0) | (
         mcpt.RENDER_PRECISION_FP32 if args.precision == "fp32" else 0) | (
-        mcpt.DEBUG_NO_ROOT_CACHE if args.no_root_cache else 0)
+        mcpt.DEBUG_NO_ROOT_CACHE if args.no_root_cache else 0) | args.debug_flags
     flags = mcpt.RENDER_NO_BACKFACE_STATS | mode_flags
     for k in range(args.warmup):  # warmup renders (same kernels and flags as the timed steps) go to scratch
         mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,

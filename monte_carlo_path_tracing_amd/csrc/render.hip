@@ -2469,8 +2469,11 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
 constexpr int kBrdfTop = MCPT_BRDF_TOP;
 constexpr int kBrdfBlock = kBrdfTop > 0 ? 256 : kTraceBlock;
 constexpr int kBrdfLds = kBrdfTop > 0 ? 8 : kRayLds;
+#ifndef MCPT_BRDF_WAVES
+#define MCPT_BRDF_WAVES 5  // 96 VGPRs (10 spilled): 4 -> 5 waves/SIMD, +5% BRDF-only (profiles/round2b_ab_brdf.txt)
+#endif
 template <bool kCount = false>
-__global__ __launch_bounds__(kBrdfBlock) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
+__global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
     __shared__ int stack[kBrdfLds * kBrdfBlock];
     __shared__ BvhNode4 top[kBrdfTop > 0 ? kBrdfTop : 1];
     const DScene& S = P.S;
@@ -2502,13 +2505,13 @@ __global__ __launch_bounds__(kBrdfBlock) void k_extend_brdf(Params P, Queue cur,
         wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
         if (!(dot(wi, N) < 0)) {
             traced = 1;
+            // the child's throughput does not depend on the hit: computed before the traversal, so
+            // the shading state (N, wo, material, tp, pdf) is dead during it (fewer VGPRs)
+            const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
+            tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
             h = trace4_ww<kBrdfLds, kCount, kBrdfTop>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
                                                       &tests, top);
-            if (h.f >= 0) {
-                const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
-                tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
-                c = true;
-            }
+            c = h.f >= 0;
         }
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
