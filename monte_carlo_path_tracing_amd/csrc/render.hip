@@ -151,6 +151,29 @@ constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB p
 // block and reads them with ds_read when the whole wave is in them, with an 8-entry LDS stack per
 // lane (same-box A/B on Veach, profiles/round2b_ab_ray_top.txt: traversal 0.82-0.84 -> 0.735-0.745 ms
 // per launch; 21 nodes: 0.76; the earlier per-lane generic-pointer select: 0.79-0.84)
+// minimum waves per SIMD of the wavefront kernels' launch bounds (1 = the compiler's choice);
+// A/B in profiles/round2b_ab_launch_bounds.txt
+#ifndef MCPT_LB_CULL
+#define MCPT_LB_CULL 1
+#endif
+#ifndef MCPT_LB_PICK
+#define MCPT_LB_PICK 1
+#endif
+#ifndef MCPT_LB_GEN
+#define MCPT_LB_GEN 1
+#endif
+#ifndef MCPT_LB_RAYS
+#define MCPT_LB_RAYS 7
+#endif
+#ifndef MCPT_LB_COMBINE
+#define MCPT_LB_COMBINE 1
+#endif
+#ifndef MCPT_LB_COMPLETE
+#define MCPT_LB_COMPLETE 1
+#endif
+#ifndef MCPT_LB_SHADE_GEN
+#define MCPT_LB_SHADE_GEN 1
+#endif
 #ifndef MCPT_RAY_TOP
 #define MCPT_RAY_TOP 85
 #endif
@@ -1335,7 +1358,7 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
 }
 
 template <bool kCountC1>
-__global__ __launch_bounds__(256) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
+__global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
                                                          const double* __restrict__ qn, uint64_t* __restrict__ masks,
                                                          int nchunks, unsigned long long* stats) {
     const int node = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1581,7 +1604,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
 // issues each link for all of its nodes before waiting on any of them (the kernel is bound by
 // that latency, not by bandwidth).  No LDS.
 constexpr int kPickNodes = 4;
-__global__ __launch_bounds__(256) void k_prep_pick(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
+__global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                    double* __restrict__ wsum_out, int* __restrict__ pick_out,
                                                    unsigned long long* stats, int nchunks, PrepCache C) {
@@ -1822,7 +1845,7 @@ __device__ inline void mis_report(const Params& P, const Slots& T, bool act, int
 // kStale: the tree-reduction form (Slots) -- w1 / w2 hold the edges' BRDF values and s1 the light
 // edge's scalar, applied bottom-up; else w1 / w2 are forward throughputs (fresh-pdf path)
 template <bool kStale>
-__global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux A) {
+__global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cur, int n, Aux A) {
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1884,7 +1907,7 @@ __global__ __launch_bounds__(256) void k_mis_gen(Params P, Queue cur, int n, Aux
 // queue's shading points, excluding the origin facet
 // kCount: counts node visits / triangle tests into cnt[0] / cnt[1] (statistics replay only)
 template <bool kGrid, bool kCount = false>
-__global__ __launch_bounds__(kRayBlock, 8) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set,
+__global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set,
                                                           unsigned long long* cnt = nullptr) {
     constexpr int kTop = kGrid ? 0 : kRayTop;
     __shared__ int stack[kRayTopLds * kRayBlock];
@@ -2157,7 +2180,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
 }
 
 template <bool kStale>
-__global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
+__global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
@@ -2234,7 +2257,7 @@ __global__ __launch_bounds__(256) void k_mis_combine(Params P, Queue cur, int n,
 // node reports to its parent (ready list 1 - rp_in) -- one tree level per pass, in step with the
 // wavefront; grid-stride over the device-side count
 // grid: x blocks per shard, y = ready-list shard
-__global__ __launch_bounds__(256) void k_mis_complete(Params P, Slots T, int rp_in) {
+__global__ __launch_bounds__(256, MCPT_LB_COMPLETE) void k_mis_complete(Params P, Slots T, int rp_in) {
     const DScene& S = P.S;
     const unsigned n = T.ctrl[16 * blockIdx.y + 4 + rp_in];
     const int* ready = (rp_in ? T.ready1 : T.ready0) + (size_t)blockIdx.y * T.ready_cap;
@@ -2333,7 +2356,7 @@ __device__ inline int area_light_sample(const DScene& S, uint64_t key, d3* coord
     return j;
 }
 
-__global__ __launch_bounds__(256) void k_shade_gen(Params P, Queue cur, int n, Aux A) {
+__global__ __launch_bounds__(256, MCPT_LB_SHADE_GEN) void k_shade_gen(Params P, Queue cur, int n, Aux A) {
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
