@@ -287,4 +287,68 @@ std::vector<BvhNode4> collapse_bvh4(const Bvh& b) {
     return out;
 }
 
+namespace {
+float decode_plane(int q, int bexp, float org) {
+    uint32_t bits = (uint32_t)bexp << 23;
+    float sc;
+    std::memcpy(&sc, &bits, 4);
+    return std::fmaf((float)q, sc, org);  // the traversal's v_fma_f32 (correctly rounded on both sides)
+}
+}  // namespace
+
+std::vector<BvhNode4Q> quantize_bvh4(const std::vector<BvhNode4>& in) {
+    std::vector<BvhNode4Q> out(in.size());
+    for (size_t i = 0; i < in.size(); i++) {
+        const BvhNode4& n = in[i];
+        BvhNode4Q& o = out[i];
+        std::memset(&o, 0, sizeof(o));
+        bool used[4];
+        for (int k = 0; k < 4; k++) {
+            o.child[k] = n.child[k];
+            used[k] = n.child[k] != kBvh4Empty && n.lo[0][k] <= n.hi[0][k];
+        }
+        for (int a = 0; a < 3; a++) {
+            float lo = FLT_MAX, hi = -FLT_MAX;
+            for (int k = 0; k < 4; k++)
+                if (used[k]) {
+                    lo = std::min(lo, n.lo[a][k]);
+                    hi = std::max(hi, n.hi[a][k]);
+                }
+            if (lo > hi) lo = hi = 0.0f;  // no child: any planes (the traversal skips kBvh4Empty)
+            o.org[a] = lo;
+            // smallest scale 2^(b - 127) whose 255 steps from org reach hi in the decode arithmetic
+            const double ext = (double)hi - (double)lo;
+            int b = ext > 0 ? std::max(1, std::min(254, (int)std::ceil(std::log2(ext / 255.0)) + 127 - 1)) : 1;
+            uint32_t qlo = 0, qhi = 0;
+            for (;; b++) {
+                if (b > 254) b = 254;
+                bool ok = decode_plane(255, b, lo) >= hi || b == 254;
+                qlo = qhi = 0;
+                for (int k = 0; ok && k < 4; k++) {
+                    if (!used[k]) {
+                        qlo |= 255u << (8 * k);  // empty slot: lo > hi
+                        continue;
+                    }
+                    const double scale = std::ldexp(1.0, b - 127);
+                    int ql = std::max(0, std::min(255, (int)std::floor(((double)n.lo[a][k] - lo) / scale)));
+                    while (ql > 0 && decode_plane(ql, b, lo) > n.lo[a][k]) ql--;
+                    int qh = std::max(0, std::min(255, (int)std::ceil(((double)n.hi[a][k] - lo) / scale)));
+                    while (qh < 255 && decode_plane(qh, b, lo) < n.hi[a][k]) qh++;
+                    if (decode_plane(ql, b, lo) > n.lo[a][k] || decode_plane(qh, b, lo) < n.hi[a][k]) {
+                        ok = false;  // needs a coarser scale
+                        break;
+                    }
+                    qlo |= (uint32_t)ql << (8 * k);
+                    qhi |= (uint32_t)qh << (8 * k);
+                }
+                if (ok || b == 254) break;
+            }
+            o.ex |= (uint32_t)b << (8 * a);
+            o.q[2 * a] = qlo;
+            o.q[2 * a + 1] = qhi;
+        }
+    }
+    return out;
+}
+
 }  // namespace mcpt

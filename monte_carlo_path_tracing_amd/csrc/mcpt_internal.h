@@ -65,6 +65,21 @@ struct BvhNode4 {
     int32_t child[4];  // >= 0: inner node; < 0: leaf ~first slot; kBvh4Empty: no child
     int32_t count[4];
 };
+// compressed 4-wide node (64 B, half a cache line): per axis the children's union minimum `org` and
+// a power-of-two scale 2^(ex_a - 127); each child plane is a byte q with plane = fma(q, scale, org)
+// in fp32, rounded outward at build time against that exact fp32 expression, so every decoded box
+// contains its BvhNode4 box (conservative: the traversal only prunes with it).  Loaded as four
+// dwordx4: (org, ex), (q lo.x, hi.x, lo.y, hi.y), (q lo.z, hi.z, -, -), children.
+struct BvhNode4Q {
+    float org[3];
+    uint32_t ex;       // byte a: biased fp32 exponent of axis a's scale
+    uint32_t q[6];     // q[2a] lo planes, q[2a + 1] hi planes of axis a; byte k = child k
+    uint32_t pad[2];
+    int32_t child[4];  // as BvhNode4 (leaf codes already packed)
+};
+static_assert(sizeof(BvhNode4Q) == 64, "BvhNode4Q must be 64 B");
+std::vector<BvhNode4Q> quantize_bvh4(const std::vector<BvhNode4>& in);
+
 // collapses a binary BVH into a 4-wide one (greedy: expand the largest-area inner child until
 // four children); leaves and leaf slots are shared with the binary tree
 std::vector<BvhNode4> collapse_bvh4(const Bvh& b);

@@ -82,6 +82,8 @@ struct DScene {
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
     const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves), breadth-first node order
     const BvhNode4* lbvh4;
+    const BvhNode4Q* bvh4q;   // the same trees as 64-B compressed nodes (k_rays_persistent)
+    const BvhNode4Q* lbvh4q;
     int nbvh4, nlbvh4;        // node counts
     const float4* lleaf_v;
     // select_a_point_from_lights (MCPT_MODE_SHADE_AREA): the lightsRadiance map in name order --
@@ -189,6 +191,44 @@ struct Hit {
     double t, beta, gamma;
 };
 
+// one node visit's loads: the four children's boxes (lo[axis][child], hi) and child codes
+__device__ inline void load_node(const BvhNode4* nd, float (&lo)[3][4], float (&hi)[3][4], int (&ch)[4]) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float4 l = *reinterpret_cast<const float4*>(nd->lo[a]), h = *reinterpret_cast<const float4*>(nd->hi[a]);
+        lo[a][0] = l.x, lo[a][1] = l.y, lo[a][2] = l.z, lo[a][3] = l.w;
+        hi[a][0] = h.x, hi[a][1] = h.y, hi[a][2] = h.z, hi[a][3] = h.w;
+    }
+    const int4 c = *reinterpret_cast<const int4*>(nd->child);
+    ch[0] = c.x, ch[1] = c.y, ch[2] = c.z, ch[3] = c.w;
+}
+// compressed node (k_rays_persistent): the slab distances of the 24 planes directly,
+//   t = fma(byte, 2^(ex - 127) * inv, fma(org, inv, -o * inv))
+// -- the same plane (org + byte * scale, quantize_bvh4 rounds it outward) with a few more fp32
+// roundings, each ~1 ulp of |plane - origin| * |inv|, far inside the boxes' 1e-5-of-the-scene
+// margins; 2 VALU per plane (v_cvt_f32_ubyteN + v_fma_f32) plus 2 per axis
+__device__ inline void node_tplanes(const BvhNode4Q* nd, const float (&inv)[3], const float (&oi)[3], float (&tl)[3][4],
+                                    float (&th)[3][4], int (&ch)[4]) {
+    const float4 v0 = *reinterpret_cast<const float4*>(nd->org);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(nd->q);
+    const uint2 v2 = *reinterpret_cast<const uint2*>(nd->q + 4);
+    const int4 c = *reinterpret_cast<const int4*>(nd->child);
+    const unsigned ex = __float_as_uint(v0.w);
+    const float org[3] = {v0.x, v0.y, v0.z};
+    const unsigned ql[3] = {v1.x, v1.z, v2.x}, qh[3] = {v1.y, v1.w, v2.y};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float m = __uint_as_float(((ex >> (8 * a)) & 0xffu) << 23) * inv[a];
+        const float b = fmaf(org[a], inv[a], -oi[a]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            tl[a][k] = fmaf((float)((ql[a] >> (8 * k)) & 0xffu), m, b);
+            th[a][k] = fmaf((float)((qh[a] >> (8 * k)) & 0xffu), m, b);
+        }
+    }
+    ch[0] = c.x, ch[1] = c.y, ch[2] = c.z, ch[3] = c.w;
+}
+
 // Closest hit over the 4-wide BVH (Myobj::closet_ray_intersect semantics without the grid):
 //  * Aila & Laine's "while-while" loop: a lane descends through inner nodes until it holds a leaf
 //    (postponed), and the wave tests triangles only once every active lane has one (or ran out of
@@ -239,22 +279,13 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     while (node != kDone || leaf < 0) {
         while (node >= 0 && node != kDone) {
             if (kCount) ++*visits;
-            float4 lx, ly, lz, hx, hy, hz;
-            int4 ch;
-            auto fetch = [&](const BvhNode4* nd) {
-                lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
-                lz = *reinterpret_cast<const float4*>(nd->lo[2]);
-                hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
-                hz = *reinterpret_cast<const float4*>(nd->hi[2]);
-                ch = *reinterpret_cast<const int4*>(nd->child);
-            };
+            float lo[3][4], hi[3][4];
+            int chs[4];
             // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch,
             // so each side reads one address space: ds_read from the LDS copy, global loads else)
-            if (kTop > 0 && __all(node < kTop)) fetch(top + node);
-            else fetch(nodes + node);
-            const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, lys[4] = {ly.x, ly.y, ly.z, ly.w}, lzs[4] = {lz.x, lz.y, lz.z, lz.w};
-            const float hxs[4] = {hx.x, hx.y, hx.z, hx.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
-            const int chs[4] = {ch.x, ch.y, ch.z, ch.w};
+            if (kTop > 0 && __all(node < kTop)) load_node(top + node, lo, hi, chs);
+            else load_node(nodes + node, lo, hi, chs);
+            const float* lxs = lo[0], *lys = lo[1], *lzs = lo[2], *hxs = hi[0], *hys = hi[1], *hzs = hi[2];
             float t[4];
             int code[4];
 #pragma unroll
@@ -419,6 +450,12 @@ struct Queue {
 // faster one per thread at 8 waves/SIMD; profiles/round2b_ab_rays_persistent.txt)
 #ifndef MCPT_RAYS_PERSISTENT
 #define MCPT_RAYS_PERSISTENT -1
+#endif
+// k_rays_persistent reads the 64-B compressed nodes (BvhNode4Q): Cornell-1M traversal -6%; the
+// L2-resident kernels keep the 128-B fp32 nodes (their decode VALU costs more than the lines save:
+// Veach MIS -1.5%, BRDF -5%; profiles/round2b_ab_bvh_quant.txt)
+#ifndef MCPT_PERSIST_QUANT
+#define MCPT_PERSIST_QUANT 1
 #endif
 #ifndef MCPT_WORKING_SET
 #define MCPT_WORKING_SET (32 << 20)  // default wavefront working set (nodes per generation)
@@ -2105,26 +2142,33 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
         if (__ballot(busy) == 0) break;  // pool exhausted and no ray in flight
         // one round of trace4_ww's outer loop on every lane in flight
         if (busy) {
+#if MCPT_PERSIST_QUANT
+            const BvhNode4Q* __restrict__ nodes = set == 2 ? S.lbvh4q : S.bvh4q;
+#else
             const BvhNode4* __restrict__ nodes = set == 2 ? S.lbvh4 : S.bvh4;
+#endif
             const float4* __restrict__ leafv = set == 2 ? S.lleaf_v : S.leaf_v;
+            const float inv3[3] = {ix, iy, iz}, oi3[3] = {oix, oiy, oiz};
             while (node >= 0 && node != kDone) {
                 if (kCount) ++visits;
-                const BvhNode4* nd = nodes + node;
-                const float4 lx = *reinterpret_cast<const float4*>(nd->lo[0]), ly = *reinterpret_cast<const float4*>(nd->lo[1]),
-                             lz = *reinterpret_cast<const float4*>(nd->lo[2]);
-                const float4 hx = *reinterpret_cast<const float4*>(nd->hi[0]), hy = *reinterpret_cast<const float4*>(nd->hi[1]),
-                             hz = *reinterpret_cast<const float4*>(nd->hi[2]);
-                const int4 ch = *reinterpret_cast<const int4*>(nd->child);
-                const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, lys[4] = {ly.x, ly.y, ly.z, ly.w}, lzs[4] = {lz.x, lz.y, lz.z, lz.w};
-                const float hxs[4] = {hx.x, hx.y, hx.z, hx.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
-                const int chs[4] = {ch.x, ch.y, ch.z, ch.w};
+                float tl[3][4], th[3][4];
+                int chs[4];
+#if MCPT_PERSIST_QUANT
+                node_tplanes(nodes + node, inv3, oi3, tl, th, chs);
+#else
+                load_node(nodes + node, tl, th, chs);
+#pragma unroll
+                for (int a = 0; a < 3; a++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) tl[a][k] = fmaf(tl[a][k], inv3[a], -oi3[a]), th[a][k] = fmaf(th[a][k], inv3[a], -oi3[a]);
+#endif
                 float t[4];
                 int code[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const float tx0 = fmaf(lxs[k], ix, -oix), tx1 = fmaf(hxs[k], ix, -oix);
-                    const float ty0 = fmaf(lys[k], iy, -oiy), ty1 = fmaf(hys[k], iy, -oiy);
-                    const float tz0 = fmaf(lzs[k], iz, -oiz), tz1 = fmaf(hzs[k], iz, -oiz);
+                    const float tx0 = tl[0][k], tx1 = th[0][k];
+                    const float ty0 = tl[1][k], ty1 = th[1][k];
+                    const float tz0 = tl[2][k], tz1 = th[2][k];
                     const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
                     const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
                     const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
@@ -2821,6 +2865,8 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     d.nlbvh4 = (int)lb4.size();
     if ((rc = upload(*D, b4, &d.bvh4))) return rc;
     if ((rc = upload(*D, lb4, &d.lbvh4))) return rc;
+    if ((rc = upload(*D, quantize_bvh4(b4), &d.bvh4q))) return rc;
+    if ((rc = upload(*D, quantize_bvh4(lb4), &d.lbvh4q))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc(&D->pinned_count, 64 + kCtrlBytes));
