@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Benchmark: Msamples/s of the MI355X path tracer on the Veach-MIS stand-in (BASELINE.json).
 
-Workload (BASELINE.json configs[2]): MIS (light + BRDF sampling), 800x600, frame of
-steps x gpus x spp_per_step samples per pixel (default 4 x 1 x 256 = 1024 spp).  A "step" is one
-pass of the hot path over one batch: spp_per_step samples of every pixel of the 800x600 frame,
-rendered by one mcpt_render_device call (wavefront kernels, fp64 framebuffer resident in HBM).
+Workload (BASELINE.json configs[2]): MIS (light + BRDF sampling), 800x600 at 1024 spp.  A "step"
+is one pass of the hot path over one batch: spp_per_step samples of every pixel of the 800x600
+frame (default 1024: each step renders the whole 1024-spp frame of BASELINE.json), by one
+mcpt_render_device call (wavefront kernels, fp64 framebuffer resident in HBM); the run accumulates
+steps x gpus x spp_per_step samples per pixel.
 Each call computes everything it uses, including its root-point light-prep cache;
 nothing is carried from one step to the next except the framebuffer.
 
@@ -146,12 +147,13 @@ def cpu_baseline(scene_name, W, H, mode, seed, target_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     # samples per render call: every call rebuilds its root-point cache and drains its wavefront
-    # queue, so larger calls amortise more (measured 64 -> 360, 128 -> 379, 256 -> 391, 1024 -> 399
-    # Msamples/s); 4 x 256 is the 1024-spp frame of BASELINE.json in four calls
-    ap.add_argument("--spp-per-step", type=int, default=256)
+    # queue, so larger calls amortise more (round 1: 64 -> 360, 128 -> 379, 256 -> 391, 1024 -> 399
+    # Msamples/s; round 2e: 256 -> 467-468, 1024 -> 480-481); the default step is the whole
+    # 1024-spp frame of BASELINE.json in one call, as the reference renders it
+    ap.add_argument("--spp-per-step", type=int, default=1024)
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--mode", default="mis", choices=["mis", "brdf", "shade", "shade_area"])
