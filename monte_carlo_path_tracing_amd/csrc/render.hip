@@ -1643,7 +1643,10 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
 // is a chain of three dependent loads (pixel -> batch totals -> one batch of weights), so the wave
 // issues each link for all of its nodes before waiting on any of them (the kernel is bound by
 // that latency, not by bandwidth).  No LDS.
-constexpr int kPickNodes = 4;
+#ifndef MCPT_PICK_NODES
+#define MCPT_PICK_NODES 4
+#endif
+constexpr int kPickNodes = MCPT_PICK_NODES;
 __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                    double* __restrict__ wsum_out, int* __restrict__ pick_out,
