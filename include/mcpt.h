@@ -100,7 +100,7 @@ typedef struct {
     uint64_t seed;          /* counter-RNG seed (reference default 20240430 in bench/tests) */
     int32_t samples_per_launch; /* wavefront working set: the node queue is refilled with camera samples
                                  * up to samples_per_launch x width x height nodes per generation
-                                 * (0 = auto: 32 Mi nodes, at most the call's camera samples and at
+                                 * (0 = auto: 48 Mi nodes, at most the call's camera samples and at
                                  * most half the free HBM) */
     int32_t queue_factor;   /* wavefront queue capacity = factor * batch roots (0 = 2); a generation with
                              * more nodes than the children buffer can take is processed in slices, the

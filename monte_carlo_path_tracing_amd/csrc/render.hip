@@ -458,7 +458,7 @@ struct Queue {
 #define MCPT_PERSIST_QUANT 1
 #endif
 #ifndef MCPT_WORKING_SET
-#define MCPT_WORKING_SET (32 << 20)  // default wavefront working set (nodes per generation)
+#define MCPT_WORKING_SET (48 << 20)  // default wavefront working set (nodes per generation)
 #endif
 #ifndef MCPT_ROOT_GROUP
 #define MCPT_ROOT_GROUP 2  // small scenes: consecutive roots take this many samples of a pixel (A/B: 1 / 2 / 4 / 8 -> 437 / 442 / 437 / 430)
@@ -3129,8 +3129,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int nminor = (MCPT_ROOT_MINOR > 0 || (MCPT_ROOT_MINOR < 0 && accel > (4ull << 20))) ? s1 - s0
                                                                                               : std::min(MCPT_ROOT_GROUP, s1 - s0);
     const int qf = o->queue_factor > 0 ? o->queue_factor : 2;
-    // default working set: MCPT_WORKING_SET nodes (32 Mi: fewer, larger generations amortise each
-    // launch's tail -- measured +5% Veach, +18% Cornell-1M over 4 Mi), but no more than the call's
+    // default working set: MCPT_WORKING_SET nodes (48 Mi: fewer, larger generations amortise each
+    // launch's tail -- measured +6% Veach, +21% Cornell-1M over 4 Mi), but no more than the call's
     // camera samples (a small render holds all its roots at once) and no more than half the free
     // HBM (the other half is left to the root-point cache and the caller)
     size_t ws_held = D.masks.bytes, ws_free = 0, ws_total = 0;
