@@ -2044,7 +2044,10 @@ __device__ inline int block_alloc_slot(const Slots& T, bool want) {
 // flight; the per-lane state (ray, stack pointer, LDS + private stack, best hit) lives across
 // rounds.  Hits are bit-identical to k_mis_rays (the closest hit, ties to the lower facet id, by the
 // same tests on conservatively pruned boxes); only the order of visits, and so their count, differs.
-constexpr int kRefill = 16;
+#ifndef MCPT_RAYS_REFILL
+#define MCPT_RAYS_REFILL 8  // A/B on Cornell-1M: 16 -> 1220, 8 -> 1231-1237, 4 -> 1203, 32 -> 1179 (profiles/round2b_ab_rays_persistent.txt)
+#endif
+constexpr int kRefill = MCPT_RAYS_REFILL;
 constexpr int kRayChunk = 256;  // pool items a wave takes per atomic
 template <bool kCount = false>
 #ifndef MCPT_RAYS_WAVES
