@@ -2048,7 +2048,14 @@ __device__ inline int block_alloc_slot(const Slots& T, bool want) {
 #define MCPT_RAYS_REFILL 8  // A/B on Cornell-1M: 16 -> 1220, 8 -> 1231-1237, 4 -> 1203, 32 -> 1179 (profiles/round2b_ab_rays_persistent.txt)
 #endif
 constexpr int kRefill = MCPT_RAYS_REFILL;
-constexpr int kRayChunk = 256;  // pool items a wave takes per atomic
+#ifndef MCPT_PERSIST_LDS
+#define MCPT_PERSIST_LDS 16  // LDS stack entries per lane of k_rays_persistent (private stack beyond)
+#endif
+constexpr int kPersistLds = MCPT_PERSIST_LDS;
+#ifndef MCPT_RAY_CHUNK
+#define MCPT_RAY_CHUNK 256
+#endif
+constexpr int kRayChunk = MCPT_RAY_CHUNK;  // pool items a wave takes per atomic
 template <bool kCount = false>
 #ifndef MCPT_RAYS_WAVES
 #define MCPT_RAYS_WAVES 6
@@ -2057,12 +2064,12 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                                                                   int nsets, unsigned* __restrict__ pool,
                                                                   unsigned long long* cnt = nullptr) {
     constexpr int kDone = 0x7fffffff;
-    __shared__ int stack[kRayLds * kRayBlock];
+    __shared__ int stack[kPersistLds * kRayBlock];
     int* __restrict__ lds = stack + threadIdx.x;
     constexpr int stride = kRayBlock;
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)nsets * (unsigned)n;
-    int spill[kStack - kRayLds];
+    int spill[kStack - kPersistLds];
     unsigned visits = 0, tests = 0;
     bool busy = false, exhausted = false;
     unsigned wnext = 0, wend = 0;  // the wave's private range of pool items (wave-uniform)
@@ -2072,14 +2079,14 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
     int sp = 0, node = kDone, leaf = 0;
     Hit best{-1, DBL_MAX, 0, 0};
     auto push = [&](int v) {
-        if (sp < kRayLds) lds[sp * stride] = v;
-        else if (sp < kStack) spill[sp - kRayLds] = v;
+        if (sp < kPersistLds) lds[sp * stride] = v;
+        else if (sp < kStack) spill[sp - kPersistLds] = v;
         sp = sp < kStack ? sp + 1 : sp;
     };
     auto pop = [&]() -> int {
         if (sp == 0) return kDone;
         --sp;
-        return sp < kRayLds ? lds[sp * stride] : spill[sp - kRayLds];
+        return sp < kPersistLds ? lds[sp * stride] : spill[sp - kPersistLds];
     };
     auto finish = [&]() {  // the lane's ray is done: store its hit
         const size_t o = (size_t)set * A.cap + ii;
