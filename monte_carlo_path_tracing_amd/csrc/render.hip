@@ -1356,8 +1356,9 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
         const LightPair* __restrict__ Th = T + 32 * c + 16 * h;
         unsigned w = 0, c1w = 0;
         float amin = __builtin_inff();  // min over the 32 lights of min(|s|, |min(s, max t)|)
-#pragma unroll 2
-        for (int q = 0; q < 16; q++) {
+        // pairs holding real lights (the table's last chunk is partial: N_L = 3012 leaves 4 of 64)
+        const int qend = kCountC1 ? 16 : min(16, max(0, (S.NL - (64 * c + 32 * h) + 1) >> 1));
+        auto pair = [&](int q) {
             v2f s1, t[3];
             cl.eval(Th[q], &s1, t);
 #pragma unroll
@@ -1369,6 +1370,13 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
                 if (kCountC1) c1w += __popcll(__ballot(sv < -err) & actm);  // statistic only
                 w = shift_in(w, __ballot(mn > err));
             }
+        };
+        if (qend == 16) {
+#pragma unroll 2
+            for (int q = 0; q < 16; q++) pair(q);
+        } else {  // the padding lights' bits stay clear; light j's bit back at 31 - j
+            for (int q = 0; q < qend; q++) pair(q);
+            w = qend == 0 ? 0u : w << (32 - 2 * qend);
         }
         if (__ballot(amin <= err) & actm) {  // rare: the reference's exact fp64 stages for the ambiguous (node, light) pairs
             for (int q = 0; q < 16; q++) {
