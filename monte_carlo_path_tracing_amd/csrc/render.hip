@@ -229,6 +229,80 @@ __device__ inline void node_tplanes(const BvhNode4Q* nd, const float (&inv)[3], 
     ch[0] = c.x, ch[1] = c.y, ch[2] = c.z, ch[3] = c.w;
 }
 
+// fp32 pre-test of the reference's triangle test (Myobj.cpp:165-192) with a rigorous error bound.
+// The four determinants (detA, nb, ng, nt of tri_hit) are evaluated in fp32 as triple products
+// sharing two cross products, p = ac x rd and q = ab x ar:
+//   detA = ab.p, nb = ar.p, ng = rd.q, nt = -(ac.q)
+// -- the same exact values as tri_hit's det3 forms (cyclic permutations).  Each fp32 value is
+// within E = 16 * 6 * u32 * Wx * Wy * Wz of the fp64 one, W = max |component| of the operand (a
+// triple product has 6 terms of at most Wx Wy Wz; the fma evaluation rounds <= 6 u32 of their sum,
+// the inputs carry <= u32 relative error -- ab, ac: fp32 differences of the fp32 vertices, rd: its
+// fp32 rounding -- and ar = a - (float)ro carries <= 2 u32 (|ar| + |ro|), so W_ar = M_ar + M_ro;
+// the fp64 evaluation's own error is ~1e-16 of the same sum).  Verdicts:
+//   0: tri_hit rejects for sure: a numerator of the opposite sign to detA beyond its bound, beta +
+//      gamma > 1 beyond the bounds, |detA| < 1e-8 for sure, or t above `tlim` for sure (tlim is at
+//      least the t of a triangle tri_hit accepts: this one cannot be the closest hit);
+//   2: tri_hit accepts for sure, *tup >= its t;
+//   1: undecided -- the fp64 test decides.
+// Nothing tri_hit would accept as the closest hit is rejected, so hits stay bit-identical.
+struct RayF {
+    float ox, oy, oz, dx, dy, dz;
+    float mo;  // max |ro| component (rounded up)
+    float kd;  // 96 u32 * max |rd| component
+};
+__device__ inline RayF ray_f(d3 ro, d3 rd) {
+    RayF r;
+    r.ox = (float)ro.x, r.oy = (float)ro.y, r.oz = (float)ro.z;
+    r.dx = (float)rd.x, r.dy = (float)rd.y, r.dz = (float)rd.z;
+    r.mo = fmaxf(fmaxf(fabsf(r.ox), fabsf(r.oy)), fabsf(r.oz)) * 1.0000002f;
+    r.kd = 96.0f * 5.9604645e-8f * 1.0001f * fmaxf(fmaxf(fabsf(r.dx), fabsf(r.dy)), fabsf(r.dz));
+    return r;
+}
+__device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const RayF& r, float tlim, float* tup) {
+    const float abx = a4.x - b4.x, aby = a4.y - b4.y, abz = a4.z - b4.z;
+    const float acx = a4.x - c4.x, acy = a4.y - c4.y, acz = a4.z - c4.z;
+    const float arx = a4.x - r.ox, ary = a4.y - r.oy, arz = a4.z - r.oz;
+    const float px = fmaf(acy, r.dz, -acz * r.dy), py = fmaf(acz, r.dx, -acx * r.dz), pz = fmaf(acx, r.dy, -acy * r.dx);
+    const float qx = fmaf(aby, arz, -abz * ary), qy = fmaf(abz, arx, -abx * arz), qz = fmaf(abx, ary, -aby * arx);
+    const float dA = fmaf(abx, px, fmaf(aby, py, abz * pz));
+    const float nb = fmaf(arx, px, fmaf(ary, py, arz * pz));
+    const float ng = fmaf(r.dx, qx, fmaf(r.dy, qy, r.dz * qz));
+    const float nt = -fmaf(acx, qx, fmaf(acy, qy, acz * qz));
+    const float wab = fmaxf(fmaxf(fabsf(abx), fabsf(aby)), fabsf(abz));
+    const float wac = fmaxf(fmaxf(fabsf(acx), fabsf(acy)), fabsf(acz));
+    const float war = fmaxf(fmaxf(fabsf(arx), fabsf(ary)), fabsf(arz)) + r.mo;
+    // bounds (+1e-30 keeps them positive under flush-to-zero; the products round well inside the x16)
+    const float eA = fmaf(wab * wac, r.kd, 1e-30f);
+    const float eB = fmaf(war * wac, r.kd, 1e-30f);
+    const float eG = fmaf(wab * war, r.kd, 1e-30f);
+    const float eT = fmaf(wab * wac * war, 96.0f * 5.9604645e-8f * 1.0001f, 1e-30f);
+    const float aA = fabsf(dA);
+    if (aA <= eA) return aA + eA < 0.999f * (float)MCPT_EPS ? 0 : 1;  // sign of detA unknown
+    const float sb = dA < 0 ? -nb : nb, sg = dA < 0 ? -ng : ng, st = dA < 0 ? -nt : nt;  // numerators over |detA|
+    if (sb < -eB || sg < -eG || st < -eT) return 0;  // beta, gamma or t < 0 for sure
+    const float over = (sb + sg) - aA, eover = (eB + eG + eA) * 1.0001f + 1e-6f * aA;
+    if (over > eover) return 0;                                         // beta + gamma > 1 for sure
+    if ((aA + eA) * 1.000001f < (float)MCPT_EPS) return 0;              // |detA| < 1e-8 for sure
+    if ((st - eT) * 0.999999f > tlim * (aA + eA) * 1.000001f) return 0;  // farther than a sure hit
+    const float lo = aA - eA;
+    if (sb > eB && sg > eG && -over > eover && (st - eT) * 0.999999f > (float)MCPT_EPS * 1.001f * (aA + eA) &&
+        lo > 1.001f * (float)MCPT_EPS) {
+        *tup = (st + eT) * 1.000001f / (lo * 0.999999f);
+        return 2;
+    }
+    return 1;
+}
+// trace4_ww's fp32 pre-filter with deferred fp64 tests (kFilter), per kernel.  Same-box A/B
+// (profiles/round2h_ab_tri_filter.txt): BRDF-only traversal (k_extend_brdf) 2.19 -> 2.10 ms per
+// launch (+3% C2); k_mis_rays 4.62 -> 4.64 ms (+-0: its light rays mostly end on the light they aim
+// at, so the deferred fp64 slots run in nearly every wave, and the slots cost registers at 7 waves)
+#ifndef MCPT_FILTER_MIS
+#define MCPT_FILTER_MIS 0
+#endif
+#ifndef MCPT_FILTER_BRDF
+#define MCPT_FILTER_BRDF 1
+#endif
+
 // Closest hit over the 4-wide BVH (Myobj::closet_ray_intersect semantics without the grid):
 //  * Aila & Laine's "while-while" loop: a lane descends through inner nodes until it holds a leaf
 //    (postponed), and the wave tests triangles only once every active lane has one (or ran out of
@@ -242,12 +316,15 @@ __device__ inline void node_tplanes(const BvhNode4Q* nd, const float (&inv)[3], 
 //    a sign pre-test that rejects beta < 0, gamma < 0 and t < 0 before the three divisions (a
 //    nonzero quotient has the sign of its operands; the divisions of the surviving candidates are
 //    exactly tri_hit's, so accepted hits are bit-identical); origin facet excluded, t > 1e-8, ties
-//    to the lower facet id.
+//    to the lower facet id (a total order on (t, facet): the result does not depend on test order);
+//  * kFilter: tri_filter's fp32 pre-test first; triangles it cannot reject wait in two per-lane
+//    slots and get the fp64 test after the traversal, wave-wide (a third survivor is tested at
+//    once); a sure hit lowers tlimit by its fp32 upper bound.
 // kCount: also count node visits and triangle tests into *visits / *tests (the traversal roofline's
 // events; only the untimed statistics replay instantiates it)
 // kTop > 0: nodes [0, kTop) are read from `top` (an LDS copy of the tree's top levels) through a
 // generic pointer, the rest from `nodes`
-template <int kLds, bool kCount = false, int kTop = 0>
+template <int kLds, bool kCount = false, int kTop = 0, bool kFilter = true>
 __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
                                 int exclude, int* __restrict__ lds, int stride, unsigned* visits = nullptr,
                                 unsigned* tests = nullptr, const BvhNode4* top = nullptr) {
@@ -263,6 +340,30 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
     const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
     float tlimit = FLT_MAX;
+    // the reference's fp64 test of leaf triangle q (the facet is not `exclude`): a sign pre-test
+    // rejects beta < 0, gamma < 0 and t < 0 before the three divisions, which are tri_hit's
+    auto exact = [&](int q) {
+        const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
+        const int fac = __float_as_int(a4.w);
+        const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
+        const double detA = det3(ab, ac, rd);
+        if (fabs(detA) < MCPT_EPS) return;
+        const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
+        const bool neg = detA < 0;
+        if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
+            return;
+        const double beta = nb / detA, gamma = ng / detA, tt = nt / detA;
+        if (beta < 0 || gamma < 0 || beta + gamma > 1 || tt < 0 || fabs(tt) < MCPT_EPS) return;
+        if (tt < best.t || (tt == best.t && fac < best.f)) {
+            best.f = fac;
+            best.t = tt;
+            best.beta = beta;
+            best.gamma = gamma;
+            tlimit = fminf(tlimit, (float)tt * 1.0001f + 1e-5f);
+        }
+    };
+    const RayF rf = kFilter ? ray_f(ro, rd) : RayF{};
+    int pend0 = -1, pend1 = -1;
     int sp = 0;
     auto push = [&](int v) {
         if (sp < kLds) lds[sp * stride] = v;
@@ -325,27 +426,26 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                 const int fac = __float_as_int(a4.w);
                 if (fac == exclude) continue;
                 if (kCount) ++*tests;
-                const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
-                const double detA = det3(ab, ac, rd);
-                if (fabs(detA) < MCPT_EPS) continue;
-                const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
-                const bool neg = detA < 0;
-                if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg)))
-                    continue;
-                const double beta = nb / detA, gamma = ng / detA, tt = nt / detA;
-                if (beta < 0 || gamma < 0 || beta + gamma > 1 || tt < 0 || fabs(tt) < MCPT_EPS) continue;
-                if (tt < best.t || (tt == best.t && fac < best.f)) {
-                    best.f = fac;
-                    best.t = tt;
-                    best.beta = beta;
-                    best.gamma = gamma;
-                    tlimit = (float)tt * 1.0001f + 1e-5f;
+                if (kFilter) {
+                    // fp32 pre-test; survivors wait in two slots for the fp64 test (run wave-wide at
+                    // the end, or at once for a third survivor), so the fp64 work has few idle lanes
+                    float tup;
+                    const int v = tri_filter(a4, b4, c4, rf, tlimit, &tup);
+                    if (v == 0) continue;
+                    if (v == 2) tlimit = fminf(tlimit, tup * 1.0001f + 1e-5f);
+                    if (pend0 < 0) pend0 = q;
+                    else if (pend1 < 0) pend1 = q;
+                    else exact(q);
+                } else {
+                    exact(q);
                 }
             }
             leaf = node;
             if (node < 0) node = pop();
         }
     }
+    if (kFilter && pend0 >= 0) exact(pend0);
+    if (kFilter && pend1 >= 0) exact(pend1);
     return best;
 }
 
@@ -1986,7 +2086,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
         if (kGrid)
             h = grid_trace(S, ro, rd, cur.f[i], set == 2);
         else
-            h = trace4_ww<kRayTopLds, kCount, kTop>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
+            h = trace4_ww<kRayTopLds, kCount, kTop, MCPT_FILTER_MIS>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
                                                     stack + threadIdx.x, kRayBlock, &visits, &tests, top);
         f = h.f;
         beta = h.beta;
@@ -2600,7 +2700,7 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
             // the shading state (N, wo, material, tp, pdf) is dead during it (fewer VGPRs)
             const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
             tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
-            h = trace4_ww<kBrdfLds, kCount, kBrdfTop>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
+            h = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
                                                       &tests, top);
             c = h.f >= 0;
         }

@@ -107,6 +107,40 @@ def test_random_rays_vs_reference(scene, light_only, name):
     print("%d/%d rays hit the reference grid's bbox crack; GPU == brute force there" % (crack.sum(), len(rin)))
 
 
+@pytest.mark.parametrize("light_only", [False, True])
+def test_edge_and_vertex_rays_vs_brute_force(scene, light_only):
+    """Rays aimed exactly at triangle vertices, edge points and points a few ulps off the edges
+    (from near and far origins, including grazing ones): the traversal's fp32 triangle pre-test
+    (tri_filter, render.hip) only skips triangles the reference's fp64 test (Myobj.cpp:165-192)
+    surely rejects, so the closest hit equals the fp64 brute force over every facet, bit for bit."""
+    arr = scene.arrays()
+    P = arr["positions"].astype(np.float64).reshape(-1, 3, 3)
+    rng = np.random.default_rng(7)
+    n = 3000
+    tri = rng.integers(0, len(P), n)
+    if light_only:
+        tri = np.asarray(arr["light_facet"])[rng.integers(0, len(arr["light_facet"]), n)]
+    kind = rng.integers(0, 3, n)
+    w = rng.random((n, 3))
+    w[kind == 0] = np.eye(3)[rng.integers(0, 3, (kind == 0).sum())]  # a vertex
+    e = rng.integers(0, 3, n)
+    w[(kind == 1), e[kind == 1]] = 0.0  # a point on an edge
+    w /= w.sum(axis=1, keepdims=True)
+    target = np.einsum("nk,nkc->nc", w, P[tri])
+    target *= 1.0 + rng.choice([0.0, 1e-15, -1e-15, 1e-12, -1e-12], (n, 1))
+    lo, hi = P.reshape(-1, 3).min(axis=0), P.reshape(-1, 3).max(axis=0)
+    ro = lo + rng.random((n, 3)) * (hi - lo)
+    near = rng.random(n) < 0.3
+    ro[near] = target[near] + rng.normal(0, 0.05, (near.sum(), 3))
+    rd = target - ro
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    ex = np.where(rng.random(n) < 0.2, tri, -1).astype(np.int32)
+    f, _ = mcpt.closest_hit(scene, ro, rd, ex, light_only)
+    bf = brute_force_hits(arr, np.concatenate([ro, rd, ex[:, None]], axis=1), light_only)
+    assert np.array_equal(f, bf)
+    print("%d/%d edge/vertex rays hit" % ((f >= 0).sum(), n))
+
+
 def test_light_prep_vs_reference_and_oracle(scene, oscene):
     pin, pout = np.load(GOLDEN / "prep_in.npy"), np.load(GOLDEN / "prep_out.npy")
     u = np.array([rng.counter_uniform(SEED, k, 0, 1, 1) for k in range(len(pin))])
