@@ -293,7 +293,7 @@ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const RayF& r,
     return 1;
 }
 // trace4_ww's fp32 pre-filter with deferred fp64 tests (kFilter), per kernel.  Same-box A/B
-// (profiles/round2h_ab_tri_filter.txt): BRDF-only traversal (k_extend_brdf) 2.19 -> 2.10 ms per
+// (profiles/round2h_ab_traversal.txt): BRDF-only traversal (k_extend_brdf) 2.19 -> 2.10 ms per
 // launch (+3% C2); k_mis_rays 4.62 -> 4.64 ms (+-0: its light rays mostly end on the light they aim
 // at, so the deferred fp64 slots run in nearly every wave, and the slots cost registers at 7 waves)
 #ifndef MCPT_FILTER_MIS
@@ -327,7 +327,7 @@ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const RayF& r,
 template <int kLds, bool kCount = false, int kTop = 0, bool kFilter = true>
 __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
                                 int exclude, int* __restrict__ lds, int stride, unsigned* visits = nullptr,
-                                unsigned* tests = nullptr, const BvhNode4* top = nullptr) {
+                                unsigned* tests = nullptr, const BvhNode4* top = nullptr, float tlimit0 = FLT_MAX) {
     constexpr int kDone = 0x7fffffff;
     Hit best{-1, DBL_MAX, 0, 0};
     if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
@@ -339,7 +339,9 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     };
     const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
     const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
-    float tlimit = FLT_MAX;
+    // tlimit0: at least the t of a triangle tri_hit accepts (or FLT_MAX) -- boxes beyond it hold no
+    // closest hit
+    float tlimit = tlimit0;
     // the reference's fp64 test of leaf triangle q (the facet is not `exclude`): a sign pre-test
     // rejects beta < 0, gamma < 0 and t < 0 before the three divisions, which are tri_hit's
     auto exact = [&](int q) {
@@ -1993,6 +1995,19 @@ __device__ inline void mis_report(const Params& P, const Slots& T, bool act, int
     if (ready) (rp ? T.ready1 : T.ready0)[(size_t)sh * T.ready_cap + q] = ps;
 }
 
+// The seed of a light ray (p, wl) aimed at light facet fac: tri_hit's t for that facet (a hit the
+// closest-hit query must accept unless it is the origin facet), else -1.  Written by the generation
+// kernels into the set-0 hit slot A.hbg[2 i], read by k_mis_rays before it overwrites the slot.
+// (A/B: -DMCPT_SEED_LIGHT=0)
+#ifndef MCPT_SEED_LIGHT
+#define MCPT_SEED_LIGHT 1
+#endif
+__device__ inline double seed_light_t(const DScene& S, int fac, int origin, d3 p, d3 wl) {
+    if (!MCPT_SEED_LIGHT || fac < 0 || fac == origin) return -1;
+    const TriHit h = tri_hit(f3(S.tri_v[3 * fac]), f3(S.tri_v[3 * fac + 1]), f3(S.tri_v[3 * fac + 2]), p, wl);
+    return h.hit ? h.t : -1;
+}
+
 // kStale: the tree-reduction form (Slots) -- w1 / w2 hold the edges' BRDF values and s1 the light
 // edge's scalar, applied bottom-up; else w1 / w2 are forward throughputs (fresh-pdf path)
 template <bool kStale>
@@ -2031,6 +2046,7 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
     double s1 = 0;
     if (dot(wl, N) > 0) {
         flags |= 1;
+        A.hbg[2 * (size_t)i] = seed_light_t(S, pick >= 0 ? S.light_facet[pick] : -1, f, p, wl);
         const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
         const double pp = phong_pdf(N, wl, wo, kd, ks, sh);
         s1 = dot(wl, N) / (lprob + pp) / MCPT_P_RR;
@@ -2059,7 +2075,7 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
 // kCount: counts node visits / triangle tests into cnt[0] / cnt[1] (statistics replay only)
 template <bool kGrid, bool kCount = false>
 __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set,
-                                                          unsigned long long* cnt = nullptr) {
+                                                          unsigned long long* cnt = nullptr, int seeded = 0) {
     constexpr int kTop = kGrid ? 0 : kRayTop;
     __shared__ int stack[kRayTopLds * kRayBlock];
     __shared__ BvhNode4 top[kTop > 0 ? kTop : 1];
@@ -2085,9 +2101,18 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
         Hit h;
         if (kGrid)
             h = grid_trace(S, ro, rd, cur.f[i], set == 2);
-        else
+        else {
+            // set 0 aims at a sampled light triangle: the generation kernel left that triangle's
+            // exact t along the ray in the set-0 hit slot (seed_light_t), so boxes behind the light
+            // are pruned from the start
+            float tl0 = FLT_MAX;
+            if (set == 0 && seeded) {
+                const double t0 = A.hbg[2 * (size_t)i];
+                if (t0 > 0) tl0 = (float)t0 * 1.0001f + 1e-5f;
+            }
             h = trace4_ww<kRayTopLds, kCount, kTop, MCPT_FILTER_MIS>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
-                                                    stack + threadIdx.x, kRayBlock, &visits, &tests, top);
+                                                    stack + threadIdx.x, kRayBlock, &visits, &tests, top, tl0);
+        }
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
@@ -2565,6 +2590,7 @@ __global__ __launch_bounds__(256, MCPT_LB_SHADE_GEN) void k_shade_gen(Params P, 
     const d3 wl = normalized(sub(coord, p));
     if (pick >= 0 && dot(wl, N) > 0 && dot(mul(wl, -1), n1) > 0) {
         flags |= 1;
+        A.hbg[2 * (size_t)i] = seed_light_t(S, S.light_facet[pick], f, p, wl);
         const d3 b = brdf_phong(N, wl, wo, kd, ks, sh);
         const d3 d = sub(coord, p);
         const d3 I = mk3(S.light_rad[3 * pick], S.light_rad[3 * pick + 1], S.light_rad[3 * pick + 2]);
@@ -3510,7 +3536,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
         const dim3 g256((ni + 255) / 256), b256(256);
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
-    auto launch_rays = [&](int first_set, int nsets) {
+    auto launch_rays = [&](int first_set, int nsets, int seeded) {
         const bool pers = MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
         if (pers && !grid) {
             unsigned* pool = (unsigned*)D.work.p + 8;
@@ -3525,14 +3551,14 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                                    first_set, nsets, pool, tcnt);
         } else {
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, nsets), dim3(kRayBlock), 0, st, D.d,
-                               *cur, ni, aux, first_set, tcnt);
+                               *cur, ni, aux, first_set, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
         }
     };
         // trace_seconds: HIP events around the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf)
         if (!fused && o->mode == MCPT_MODE_MIS) {
             hipLaunchKernelGGL(stale ? k_mis_gen<true> : k_mis_gen<false>, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            launch_rays(0, 3);
+            launch_rays(0, 3, 1);
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(stale ? k_mis_combine<true> : k_mis_combine<false>, g256, b256, 0, st, P, *cur, ni, aux,
                                *nxt, T, rp);
@@ -3544,13 +3570,13 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         } else if (!fused && (o->mode == MCPT_MODE_SHADE || o->mode == MCPT_MODE_SHADE_AREA)) {
             hipLaunchKernelGGL(k_shade_gen, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            launch_rays(0, 2);
+            launch_rays(0, 2, 1);
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(k_shade_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else if (!fused) {
             hipLaunchKernelGGL(k_brdf_gen, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            launch_rays(1, 1);
+            launch_rays(1, 1, 0);
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(k_brdf_combine, g256, b256, 0, st, P, *cur, ni, aux, *nxt);
         } else {
