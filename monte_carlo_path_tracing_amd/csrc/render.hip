@@ -2195,7 +2195,7 @@ template <bool kCount = false>
 #endif
 __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(DScene S, Queue cur, int n, Aux A, int first_set,
                                                                   int nsets, unsigned* __restrict__ pool,
-                                                                  unsigned long long* cnt = nullptr) {
+                                                                  unsigned long long* cnt = nullptr, int seeded = 0) {
     constexpr int kDone = 0x7fffffff;
     __shared__ int stack[kPersistLds * kRayBlock];
     int* __restrict__ lds = stack + threadIdx.x;
@@ -2274,6 +2274,10 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                             ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
                             oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
                             tlimit = FLT_MAX;
+                            if (set == 0 && seeded) {  // the light triangle's exact t (seed_light_t)
+                                const double t0 = A.hbg[2 * (size_t)ii];
+                                if (t0 > 0) tlimit = (float)t0 * 1.0001f + 1e-5f;
+                            }
                             sp = 0;
                             node = 0;
                             leaf = 0;
@@ -2360,7 +2364,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                         best.t = tt;
                         best.beta = beta;
                         best.gamma = gamma;
-                        tlimit = (float)tt * 1.0001f + 1e-5f;
+                        tlimit = fminf(tlimit, (float)tt * 1.0001f + 1e-5f);
                     }
                 }
                 leaf = node;
@@ -3545,10 +3549,10 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             const int blocks = (int)std::max<long long>(1, std::min<long long>((items + kRayBlock - 1) / kRayBlock, 2048));
             if (count_trav)
                 hipLaunchKernelGGL(k_rays_persistent<true>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux,
-                                   first_set, nsets, pool, tcnt);
+                                   first_set, nsets, pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
             else
                 hipLaunchKernelGGL(k_rays_persistent<false>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux,
-                                   first_set, nsets, pool, tcnt);
+                                   first_set, nsets, pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
         } else {
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, nsets), dim3(kRayBlock), 0, st, D.d,
                                *cur, ni, aux, first_set, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
