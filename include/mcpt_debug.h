@@ -27,6 +27,14 @@ enum { MCPT_DEBUG_SPLIT_BRDF = 1 << 16, MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17, MCPT
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 
+/* diagnostics (host only, no GPU): the traversal's fp32 triangle pre-test (tri_filter in render.hip)
+ * on n (triangle, ray) pairs -- tri: 9 floats per triangle (a, b, c), ro / rd: 3 doubles per ray,
+ * tlim: the traversal's current limit per pair (FLT_MAX: none).  verdict: 0 the reference's fp64 test
+ * (Myobj.cpp:165-192) surely rejects, or the hit lies surely beyond tlim; 2 it surely accepts, with
+ * tup >= its t; 1 undecided.  Lets a CPU test check the bound's soundness against the fp64 test. */
+int mcpt_debug_tri_filter(int32_t n, const float* tri, const double* ro, const double* rd, const float* tlim,
+                          int32_t* verdict, float* tup);
+
 #ifdef __cplusplus
 }
 #endif

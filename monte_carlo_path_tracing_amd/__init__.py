@@ -91,7 +91,7 @@ EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_cre
            "mcpt_render_opts_init", "mcpt_render", "mcpt_render_device",
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
-DEBUG_EXPORTS = ["mcpt_debug_prep_bench"]  # include/mcpt_debug.h
+DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter"]  # include/mcpt_debug.h
 
 
 def lib():
@@ -135,6 +135,7 @@ def lib():
         L.mcpt_light_prep.argtypes = [P, I, dp, dp, dp, dp, ip, ip]
         L.mcpt_primary_hits.argtypes = [P, C.POINTER(Camera), ip, dp]
         L.mcpt_debug_prep_bench.argtypes = [P, I, dp, dp, dp, I, I, C.POINTER(C.c_double), dp, ip]
+        L.mcpt_debug_tri_filter.argtypes = [I, fp, dp, dp, fp, ip, fp]
         L.mcpt_tone_map.argtypes = [dp, I, I, D, D, u8]
         L.mcpt_write_bmp.argtypes = [C.c_char_p, u8, I, I]
         L.mcpt_comm_unique_id.argtypes = [C.c_char_p]
@@ -324,6 +325,19 @@ def light_prep(scene, x1, normal, u):
     ws, cnt, pick = np.zeros(n), np.zeros(n, np.int32), np.zeros(n, np.int32)
     _check(lib().mcpt_light_prep(scene.h, n, x1, normal, u, ws, cnt, pick))
     return ws, cnt, pick
+
+
+def debug_tri_filter(tri, ro, rd, tlim=None):
+    """Diagnostics (host only): the traversal's fp32 triangle pre-test on (triangle, ray) pairs.
+    Returns (verdict, tup): 0 = the fp64 test surely rejects (or the hit is surely beyond tlim),
+    2 = it surely accepts with t <= tup, 1 = undecided (include/mcpt_debug.h)."""
+    tri = np.ascontiguousarray(tri, np.float32).reshape(-1, 9)
+    n = tri.shape[0]
+    ro, rd = _d(ro, (-1, 3)), _d(rd, (-1, 3))
+    tl = np.full(n, np.finfo(np.float32).max, np.float32) if tlim is None else np.ascontiguousarray(tlim, np.float32)
+    verdict, tup = np.zeros(n, np.int32), np.zeros(n, np.float32)
+    _check(lib().mcpt_debug_tri_filter(n, tri, ro, rd, tl, verdict, tup))
+    return verdict, tup
 
 
 def debug_prep_bench(scene, x1, normal, u, variant=-1, iters=5):

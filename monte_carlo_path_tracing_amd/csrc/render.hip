@@ -250,7 +250,7 @@ struct RayF {
     float mo;  // max |ro| component (rounded up)
     float kd;  // 96 u32 * max |rd| component
 };
-__device__ inline RayF ray_f(d3 ro, d3 rd) {
+__host__ __device__ inline RayF ray_f(d3 ro, d3 rd) {
     RayF r;
     r.ox = (float)ro.x, r.oy = (float)ro.y, r.oz = (float)ro.z;
     r.dx = (float)rd.x, r.dy = (float)rd.y, r.dz = (float)rd.z;
@@ -258,7 +258,7 @@ __device__ inline RayF ray_f(d3 ro, d3 rd) {
     r.kd = 96.0f * 5.9604645e-8f * 1.0001f * fmaxf(fmaxf(fabsf(r.dx), fabsf(r.dy)), fabsf(r.dz));
     return r;
 }
-__device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const RayF& r, float tlim, float* tup) {
+__host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const RayF& r, float tlim, float* tup) {
     const float abx = a4.x - b4.x, aby = a4.y - b4.y, abz = a4.z - b4.z;
     const float acx = a4.x - c4.x, acy = a4.y - c4.y, acz = a4.z - c4.z;
     const float arx = a4.x - r.ox, ary = a4.y - r.oy, arz = a4.z - r.oz;
@@ -4265,6 +4265,20 @@ int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* n
     for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
     void* bufs[] = {dp, dn, du, dw, dc, dk, dm};
     for (void* b : bufs) (void)hipFree(b);
+    return MCPT_OK;
+}
+
+int mcpt_debug_tri_filter(int32_t n, const float* tri, const double* ro, const double* rd, const float* tlim,
+                          int32_t* verdict, float* tup) {
+    if (n < 0 || (n > 0 && (!tri || !ro || !rd || !tlim || !verdict || !tup))) return MCPT_E_INVALID;
+    for (int32_t k = 0; k < n; k++) {
+        const float* v = tri + 9 * (size_t)k;
+        const RayF r = ray_f(mk3(ro[3 * k], ro[3 * k + 1], ro[3 * k + 2]), mk3(rd[3 * k], rd[3 * k + 1], rd[3 * k + 2]));
+        float t = 0;
+        verdict[k] = tri_filter(make_float4(v[0], v[1], v[2], 0), make_float4(v[3], v[4], v[5], 0),
+                                make_float4(v[6], v[7], v[8], 0), r, tlim[k], &t);
+        tup[k] = t;
+    }
     return MCPT_OK;
 }
 
