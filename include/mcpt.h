@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 20000 /* 2.0.0: mcpt_render_opts carries struct_size (checked first), a device list
+#define MCPT_VERSION 20100 /* 2.1.0: mcpt_stats gains prep_exact_nodes and cache_build_seconds (appended);
+                               * 2.0.0: mcpt_render_opts carries struct_size (checked first), a device list
                                * and a multi-process communicator; debug entry points moved to mcpt_debug.h */
 
 enum {
@@ -175,6 +176,10 @@ typedef struct {
     uint64_t trace_launches;
     uint64_t node_visits;   /* BVH node visits and ray/triangle tests of that kernel -- counted only when */
     uint64_t tri_tests;     /* the render sets MCPT_DEBUG_COUNT_TRAVERSAL (mcpt_debug.h), else 0 */
+    uint64_t prep_exact_nodes; /* light preps whose pick lay within the rounding band of a cumulative-weight
+                                * boundary and were redone with the reference's literal formulas and
+                                * summation order (Mylight.cpp:335-438), so the pick is the reference's */
+    double cache_build_seconds; /* device time building the per-pixel root-point cache (in prep_seconds) */
 } mcpt_stats;
 /* With several devices, `seconds` is the wall time of the whole call (shards + reduce), counts are
  * summed over devices and prep_seconds is summed device time. */

@@ -27,6 +27,19 @@ enum { MCPT_DEBUG_SPLIT_BRDF = 1 << 16, MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17, MCPT
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 
+/* diagnostics: mcpt_light_prep with every point through the exact fallback alone (k_prep_exact: the
+ * reference's literal cull chain and weights, Mylight.cpp:335-413, summed in index order, and the
+ * counter-RNG pick over those sums) -- the arithmetic the renderer uses for picks inside the
+ * ambiguity band.  Scenes with more than 64 light triangles (else MCPT_E_INVALID). */
+int mcpt_debug_light_prep_exact(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
+                                double* weights_sum, int32_t* count, int32_t* pick);
+
+/* diagnostics: the reference's literal cull chain (Mylight.cpp:335-413, light_tri_stage) for every light
+ * at one point, 20 doubles per light: stage (0 survives, 1/2 cheap culls, 3 full-stage cull), A, B, C
+ * (after the orientation swap), a, b, c, alpha, beta, gamma, alpha+beta+gamma-pi, w (-1 if culled),
+ * alpha's acos argument, B.C.  For checking the GPU's fp64 sqrt / division / acos against the host's. */
+int mcpt_debug_light_literal(mcpt_scene* scene, const double x1[3], const double normal[3], double* out20);
+
 /* diagnostics (host only, no GPU): the traversal's fp32 triangle pre-test (tri_filter in render.hip)
  * on n (triangle, ray) pairs -- tri: 9 floats per triangle (a, b, c), ro / rd: 3 doubles per ray,
  * tlim: the traversal's current limit per pair (FLT_MAX: none).  verdict: 0 the reference's fp64 test

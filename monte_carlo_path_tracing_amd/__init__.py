@@ -26,7 +26,7 @@ MODES = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE, "shade_area": 
 ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
 HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
 DEFAULT_SEED = 20240430
-MCPT_VERSION = 20000  # include/mcpt.h MCPT_VERSION this mirror is written against
+MCPT_VERSION = 20100  # include/mcpt.h MCPT_VERSION this mirror is written against
 COMM_ID_BYTES = 128  # MCPT_COMM_ID_BYTES
 
 
@@ -77,7 +77,7 @@ class Stats(C.Structure):
                 ("prep_full_nodes", C.c_uint64), ("prep_cached_nodes", C.c_uint64), ("prep_cache_points", C.c_uint64),
                 ("spilled_nodes", C.c_uint64), ("reduce_seconds", C.c_double), ("devices_used", C.c_int32),
                 ("trace_seconds", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
-                ("tri_tests", C.c_uint64)]
+                ("tri_tests", C.c_uint64), ("prep_exact_nodes", C.c_uint64), ("cache_build_seconds", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -91,7 +91,7 @@ EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_cre
            "mcpt_render_opts_init", "mcpt_render", "mcpt_render_device",
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
-DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter"]  # include/mcpt_debug.h
+DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter", "mcpt_debug_light_prep_exact", "mcpt_debug_light_literal"]  # include/mcpt_debug.h
 
 
 def lib():
@@ -136,6 +136,8 @@ def lib():
         L.mcpt_primary_hits.argtypes = [P, C.POINTER(Camera), ip, dp]
         L.mcpt_debug_prep_bench.argtypes = [P, I, dp, dp, dp, I, I, C.POINTER(C.c_double), dp, ip]
         L.mcpt_debug_tri_filter.argtypes = [I, fp, dp, dp, fp, ip, fp]
+        L.mcpt_debug_light_prep_exact.argtypes = [P, I, dp, dp, dp, dp, ip, ip]
+        L.mcpt_debug_light_literal.argtypes = [P, dp, dp, dp]
         L.mcpt_tone_map.argtypes = [dp, I, I, D, D, u8]
         L.mcpt_write_bmp.argtypes = [C.c_char_p, u8, I, I]
         L.mcpt_comm_unique_id.argtypes = [C.c_char_p]
@@ -325,6 +327,23 @@ def light_prep(scene, x1, normal, u):
     ws, cnt, pick = np.zeros(n), np.zeros(n, np.int32), np.zeros(n, np.int32)
     _check(lib().mcpt_light_prep(scene.h, n, x1, normal, u, ws, cnt, pick))
     return ws, cnt, pick
+
+
+def debug_light_prep_exact(scene, x1, normal, u):
+    """Diagnostics: light_prep with every point through the exact fallback alone (the reference's
+    literal cull chain and weights, summed in index order; include/mcpt_debug.h)."""
+    x1, normal, u = _d(x1, (-1, 3)), _d(normal, (-1, 3)), _d(u, (-1,))
+    n = x1.shape[0]
+    ws, cnt, pick = np.zeros(n), np.zeros(n, np.int32), np.zeros(n, np.int32)
+    _check(lib().mcpt_debug_light_prep_exact(scene.h, n, x1, normal, u, ws, cnt, pick))
+    return ws, cnt, pick
+
+
+def debug_light_literal(scene, x1, normal):
+    """Diagnostics: the literal cull chain's intermediates for every light at one point (N_L x 20)."""
+    out = np.zeros((scene.nlights, 20))
+    _check(lib().mcpt_debug_light_literal(scene.h, _d(x1, (3,)), _d(normal, (3,)), out.reshape(-1)))
+    return out
 
 
 def debug_tri_filter(tri, ro, rd, tlim=None):

@@ -351,6 +351,8 @@ struct SphEx {
     d3 A, B, C;     // unit vectors towards p0, p1, p2 (reference vertex order)
     double ab;      // A.B
     double half;    // sA / 2
+    double num;     // |A.(B x C)|
+    double den;     // 1 + A.B + B.C + C.A = 4 - (the three edges' 1 - cos)
     bool edges_ok;  // A.B, B.C, C.A < 1
 };
 template <bool kPrepBatch = false>
@@ -363,6 +365,8 @@ __device__ inline SphEx sph_excess(d3 a, d3 b, d3 c) {
     e.ab = ab;
     e.edges_ok = (ab < 1.0) & (bc < 1.0) & (ca < 1.0);
     const double num = fabs(fdot(e.A, fcross(e.B, e.C))), den = 1.0 + ab + bc + ca;
+    e.num = num;
+    e.den = den;
     e.half = kPrepBatch ? atan2_pos_prep(num, den) : atan2_pos_wave(num, den);
     return e;
 }
@@ -379,6 +383,37 @@ __device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum2, d3 x
     const bool good = e.edges_ok & (e.half > 0) & __builtin_amdgcn_class(w, 0x1e0);
     *ok = good;
     return good ? w : 0.0;
+}
+// ---- exact pick: light_weight_bf plus the error bookkeeping of the pick band ----
+// The reference's weight (alpha + beta + gamma - pi from six acos, Mylight.cpp:375-396) differs from
+// this one by its own rounding, ~u / (edge angle) for ordinary triangles and ~u sqrt(2x) / num for
+// slivers (a spherical triangle seen nearly edge-on: an angle near 0 or pi, where acos is
+// ill-conditioned).  Slivers -- 4 - den > kBandTau num, i.e. the sum of 1/sin of the angles above
+// ~2 kBandTau -- are flagged here (one FMA and one compare per candidate) and carry their error term
+// into the band; the others are covered by the per-chunk bound.
+#ifndef MCPT_BAND_TAU
+#define MCPT_BAND_TAU 1000.0
+#endif
+struct WeightBx {
+    double w;     // weight (0 if culled)
+    double num;   // |A.(B x C)|
+    double den;   // 1 + A.B + B.C + C.A
+    bool ok;      // survives the full stage
+    bool sliver;  // 4 - den > kBandTau num
+};
+template <bool kPrepBatch = false>
+__device__ inline WeightBx light_weight_bx(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1) {
+    const SphEx e = sph_excess<kPrepBatch>(sub(p0, x1), sub(p1, x1), sub(p2, x1));
+    const double w = e.half * lsum2;
+    const bool good = e.edges_ok & (e.half > 0) & __builtin_amdgcn_class(w, 0x1e0);
+    return WeightBx{good ? w : 0.0, e.num, e.den, good, fma(MCPT_BAND_TAU, e.num, e.den) < 4.0};
+}
+// the sliver's error term (without the factor u lsum2 / 2 applied by the caller): sqrt(2x) / num,
+// x = 4 - den, from the hardware rsqrt / rcp estimates (~1e-7 relative), rounded up by 1% (a bound
+// only; no IEEE sqrt / division sequence and its constants in the prep's hot loop)
+__device__ inline double sliver_term(double num, double den) {
+    const double x2 = fmax(2.0 * (4.0 - den), 1e-300);
+    return x2 * __builtin_amdgcn_rsq(x2) * __builtin_amdgcn_rcp(num) * 1.01;
 }
 __device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, double* w_out) {
     bool ok;

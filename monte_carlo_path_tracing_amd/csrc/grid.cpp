@@ -33,12 +33,17 @@ Grid build_grid(const HostScene& s, const double eye[3], int n0) {
     double len[3];
     for (int i = 0; i < 3; i++) len[i] = g.mx[i] - g.mn[i];
     g.d = std::fmax(std::fmax(len[0], len[1]), len[2]) / std::pow((double)n0, 1.0 / 3);
+    // a box of zero or non-finite extent (no facets, a single point, inf coordinates) has no cell
+    // size; the reference would divide by it (Myobj.cpp:119).  Refused (g.ok stays false) -- found
+    // by the sanitizer build (`make sanitize`), as was the cell-count cap below
+    if (!(g.d > 0) || !std::isfinite(g.d) || !std::isfinite(len[0] + len[1] + len[2])) return g;
     g.inv_d = 1.0 / g.d;
     for (int i = 0; i < 3; i++) {
         g.lim[i] = (int)std::floor(len[i] / g.d) + 2;
         g.gd[i] = g.lim[i] + 1;
     }
     const size_t ncell = (size_t)g.gd[0] * g.gd[1] * g.gd[2];
+    if (ncell > (size_t)1 << 31) return g;  // n0 beyond any sane grid
     // per facet: its cell range per axis (the facet's own box)
     std::vector<int> rng(6 * (size_t)s.F);
     for (int f = 0; f < s.F; f++) {
@@ -49,8 +54,10 @@ Grid build_grid(const HostScene& s, const double eye[3], int n0) {
                 lo = std::fmin(lo, v);
                 hi = std::fmax(hi, v);
             }
-            rng[6 * f + 2 * i] = (int)std::floor((lo - g.mn[i]) / g.d);
-            rng[6 * f + 2 * i + 1] = (int)std::floor((hi - g.mn[i]) / g.d);
+            // a facet with a non-finite coordinate is listed nowhere (fmin / fmax skip its NaNs)
+            const bool fin = std::isfinite(lo) && std::isfinite(hi);
+            rng[6 * f + 2 * i] = fin ? (int)std::floor((lo - g.mn[i]) / g.d) : 1;
+            rng[6 * f + 2 * i + 1] = fin ? (int)std::floor((hi - g.mn[i]) / g.d) : 0;
         }
     }
     // counting pass, prefix sum, fill pass (CSR: cell -> facets in facet order)

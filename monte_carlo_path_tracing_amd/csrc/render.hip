@@ -79,6 +79,11 @@ struct DScene {
     const float4* lt_f;       // NL*4: fp32 records of MCPT_RENDER_PRECISION_FP32 (LightF32: p0, p1, p2 with the
                               // area normal in .w, then 2 RadianceRGB::sum() as fp64 bits)
     const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
+    // exact-pick band: per 64-light chunk a bounding sphere (centre, radius) of its
+    // vertices and (max sum L, max sum L / shortest edge) of its lights; the same over the whole table
+    const float4* chunk_sph;  // nchunks
+    const float2* chunk_sk;   // nchunks
+    double band_ctr[3], band_R, band_S, band_K;
     const float4* leaf_v;     // per leaf slot: 3 float4 (w of the first = facet id bits)
     const BvhNode4* bvh4;     // 4-wide collapse of bvh (same leaves), breadth-first node order
     const BvhNode4* lbvh4;
@@ -819,9 +824,10 @@ __global__ __launch_bounds__(256) void k_root_points(DScene S, CamFrame cam, con
 
 // Light prep for scenes with few light triangles (N_L <= kSmallNL, e.g. the 2-triangle Cornell
 // light): lane per node, a sequential loop over the light table in index order -- exactly the
-// oracle's loop (exact fp64 cheap stages, light_weight_bf for the full stage), the sum in index
+// oracle's loop (the reference's literal cull chain and weight, light_tri_stage), the sum in index
 // order and the pick "first survivor whose running sum >= u * weights_sum" (last survivor on
-// rounding).  A wave per node would leave 62 of 64 lanes idle here.
+// rounding): exact by construction, no ambiguity band needed.  A wave per node would leave 62 of 64
+// lanes idle here.
 constexpr int kSmallNL = 64;
 __device__ inline unsigned long long wave_sum_u64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -851,17 +857,17 @@ __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int 
     if (active) {
         const d3 x1 = mk3(qp[3 * i], qp[3 * i + 1], qp[3 * i + 2]);
         const d3 nn = mk3(qn[3 * i], qn[3 * i + 1], qn[3 * i + 2]);
+        // the reference's literal chain (light_tri_stage: Mylight.cpp:335-413, six acos), so weights,
+        // weights_sum (summed in index order below) and the pick are the reference's bit for bit
         auto eval = [&](int li, bool* ok) -> double {
             const double2* w = S.lt_w + 5 * li;
             const double2 a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
             const d3 p0 = mk3(a.x, a.y, b.x), p1 = mk3(b.y, c.x, c.y), p2 = mk3(d.x, d.y, e.x);
             const double4 ln = S.lt_n[li];
-            const int st = light_cheap_stage(p0, p1, p2, mk3(ln.x, ln.y, ln.z), x1, nn);
-            if (st != 0) {
-                *ok = false;
-                return st;  // 1 or 2: the culling stage
-            }
-            return light_weight_bf(p0, p1, p2, e.y, x1, ok);
+            SphTri o;
+            const int st = light_tri_stage(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
+            *ok = st == 0;
+            return st == 0 ? o.w : (double)st;  // culled: 1 or 2 = the cheap stage, 3 = the full stage
         };
         double wsum = 0;
         for (int li = 0; li < S.NL; li++) {
@@ -986,6 +992,65 @@ __device__ inline double batch_totals4(double a, double b, double c, double d) {
     return r;
 }
 
+// ---- exact pick: the ambiguity band ------------------------------------------
+// The GPU's weights differ from the reference's (oracle's) by rounding, so a pick whose target u W
+// lies within that difference of a cumulative-weight boundary may differ.  Each pick therefore
+// computes its margin -- the distance of the target from the two boundaries around the picked
+// candidate -- and compares it with a band that bounds the prefix sums' difference (calibrated with
+// tools/prep_error_study.py: the band is >= 4x the largest difference measured over 60 000 shading
+// points): kappa u sqrt(sum_c n_c m_c^2) over the 64-light chunks (m_c = S_c + K_c (|x1 - c_c| + R_c),
+// the chunk's largest sum L and sum L / shortest edge, scaled by the distance bound) + the flagged
+// slivers' own terms + the GPU's summation-order rounding.  A node inside the band goes to the exact
+// fallback (k_prep_exact: the reference's literal formulas, summed in the reference's order).
+#ifndef MCPT_BAND_KAPPA
+#define MCPT_BAND_KAPPA 8.0
+#endif
+#ifndef MCPT_BAND_SLIVER
+#define MCPT_BAND_SLIVER 0.25
+#endif
+constexpr double kU53 = 0x1.0p-53;
+constexpr int kExactHead = 16;  // exact list: [0] count, entries from [kExactHead]
+// rounding of the GPU's own sums (batch trees instead of a sequential sum) and of its formulas
+__device__ inline double band_round(int ncand, double wsum) { return (2.0 * ncand + 4096.0) * kU53 * fabs(wsum); }
+// the slivers' terms: sum over flagged candidates of lsum2 sqrt(2x)/num (sliver_term), to band units
+__device__ inline double band_sliver(double acc) { return MCPT_BAND_SLIVER * 0.5 * kU53 * acc; }
+// upper bound of band_base over the whole table (scene sphere and maxima, at most N_L candidates)
+__device__ inline double band_base_upper(const DScene& S, d3 x1) {
+    const double dx = x1.x - S.band_ctr[0], dy = x1.y - S.band_ctr[1], dz = x1.z - S.band_ctr[2];
+    const double m = S.band_S + S.band_K * (sqrt(dx * dx + dy * dy + dz * dz) + S.band_R);
+    return MCPT_BAND_KAPPA * kU53 * sqrt((double)S.NL) * m * 1.0001;
+}
+// the per-chunk term of the band for one node (this lane): n_c = set bits of the node's candidate word c
+// (mrow), or 64 without words
+__device__ inline double band_base(const DScene& S, d3 x1, const uint64_t* mrow, int nchunks) {
+    double b2 = 0;
+    for (int c = 0; c < nchunks; c++) {
+        const int nc = mrow ? __popcll(mrow[c]) : 64;
+        if (nc == 0) continue;
+        const float4 sp = S.chunk_sph[c];
+        const float2 sk = S.chunk_sk[c];
+        const double dx = x1.x - sp.x, dy = x1.y - sp.y, dz = x1.z - sp.z;
+        const double m = (double)sk.x + (double)sk.y * (sqrt(dx * dx + dy * dy + dz * dz) + (double)sp.w);
+        b2 += (double)nc * m * m;
+    }
+    return MCPT_BAND_KAPPA * kU53 * sqrt(b2) * 1.0001;
+}
+// distance of target = u W from the boundaries around the picked candidate (lane pl of the batch whose
+// exclusive prefix is base; sc = this lane's inclusive in-batch scan): below, the cumulative weight
+// before it (none if that is 0: no earlier weight); above, the cumulative weight including it
+__device__ inline double pick_margin(double base, double sc, int pl, double target) {
+    const double c_hi = base + __shfl(sc, pl);
+    const double c_lo = pl > 0 ? base + __shfl(sc, pl > 0 ? pl - 1 : 0) : base;
+    const double m_lo = c_lo == 0.0 ? INFINITY : target - c_lo;
+    return fmin(m_lo, c_hi - target);
+}
+// the room a pick leaves for the band: its margin, and the distance of weights_sum from the empty-set
+// threshold 1e-8 (Mylight.cpp:427); a pick is exact if its slack exceeds the band (NaN: not exact)
+__device__ inline double pick_slack(double margin, double wsum) {
+    const double s = fmin(margin, fabs(fabs(wsum) - MCPT_EPS));
+    return s == s ? s : -INFINITY;
+}
+
 struct PrepLight {
     d3 p0, p1, p2, nl;
     double lsum2;  // 2 RadianceRGB::sum()
@@ -1038,7 +1103,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
                                               const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                               const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                               int* __restrict__ pick_out, int* __restrict__ count_out,
-                                              unsigned long long* stats, int nchunks, unsigned* __restrict__ work) {
+                                              unsigned long long* stats, int nchunks, unsigned* __restrict__ work,
+                                              double* __restrict__ slack, int exact_off, int exact_counts) {
     extern __shared__ double prep_lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
@@ -1063,6 +1129,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
         const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
         const NodeF nf = node_f(x1, nn, S.light_bound);
         int qcnt = 0, nb = 0, survivors = 0, candidates = 0, culled1 = 0;
+        double sacc = 0;  // flagged slivers' band terms (exact pick)
+        bool degen = false;
         // ---- pass 1 ----
         for (int c = 0; c < nchunks; c++) {
             const int li = c * 64 + lane;
@@ -1082,8 +1150,15 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
                 bool ok = false;
                 if (act) {
                     const PrepLight L = load_light(S, lj);
-                    ok = light_weight(L.p0, L.p1, L.p2, L.lsum2, x1, &w);
-                    if (!ok) w = 0;
+                    const WeightBx r = light_weight_bx(L.p0, L.p1, L.p2, L.lsum2, x1);
+                    ok = r.ok;
+                    w = r.w;
+                    if (ok && r.sliver) {
+                        const double t = sliver_term(r.num, r.den) * L.lsum2;
+                        sacc += t;
+                        degen |= 2.0 * w < 64.0 * kU53 * t;
+                    }
+                    degen |= !ok;
                 }
                 const double sc = wave_incl_scan(w, lane);
                 survivors += __popcll(__ballot(ok));
@@ -1101,6 +1176,7 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
         for (int b = 0; b < nb; b++) wsum += bt[b];
         // ---- pass 2: inverse-CDF pick ----
         int pick = -1;
+        double margin = INFINITY;
         if (!(fabs(wsum) < MCPT_EPS)) {
             double u;
             if (u_override) u = u_override[node];
@@ -1159,12 +1235,21 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
             int pl = -1;
             if (candm) pl = __ffsll((unsigned long long)candm) - 1;
             else if (okm) pl = 63 - __clzll((long long)okm);
-            if (pl >= 0) pick = __shfl(lj, pl);
+            if (pl >= 0) {
+                pick = __shfl(lj, pl);
+                margin = pick_margin(base, sc, pl, target);
+            }
         }
         if (lane == 0) {
             wsum_out[node] = wsum;
             pick_out[node] = pick;
             if (count_out) count_out[node] = survivors;
+        }
+        if (slack) {  // exact pick (k_prep_band: no candidate words here, every chunk counts as full)
+            double sl = pick_slack(margin, wsum) - (band_sliver(__shfl(wave_incl_scan(sacc, lane), 63)) +
+                                                    band_round(candidates, wsum));
+            if (exact_counts && __ballot(degen)) sl = -INFINITY;
+            if (lane == 0) slack[exact_off + node] = sl;
         }
         surv_acc += survivors;
         cand_acc += candidates;
@@ -1235,6 +1320,18 @@ __device__ inline double prep_weight_buf(__amdgpu_buffer_rsrc_t rw, int li, d3 x
                            mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
                            mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1, ok);
 }
+// prep_weight_buf with the exact-pick bookkeeping (light_weight_bx); *lsum2 = the record's 2 sum L
+__device__ inline WeightBx prep_weight_buf_bx(__amdgpu_buffer_rsrc_t rw, int li, d3 x1, double* lsum2) {
+    const v4u a = struct_load_b128(rw, li, 0, 0, 0);
+    const v4u b = struct_load_b128(rw, li, 16, 0, 0);
+    const v4u c = struct_load_b128(rw, li, 32, 0, 0);
+    const v4u d = struct_load_b128(rw, li, 48, 0, 0);
+    const v4u e = struct_load_b128(rw, li, 64, 0, 0);
+    *lsum2 = u2d(e.z, e.w);
+    return light_weight_bx<true>(mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y)),
+                                 mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
+                                 mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1);
+}
 // fp32 records (MCPT_RENDER_PRECISION_FP32, LightF32): 10 floats at a 64-B stride (a record never
 // straddles a cache line), the same padding and sentinels as lt_w
 constexpr int kLtF = 64;
@@ -1302,13 +1399,22 @@ struct PrepCache {
     int lstride;
     int build;            // this launch builds entries of pixel qpixel[node] (qpixel == nullptr: node)
     int use;              // host side: root nodes go to k_prep_pick
+    // exact pick: the pick's slack -- its margin less the band's terms known here
+    // (flagged slivers, summation rounding; k_prep_pick: the whole band, so +-inf) -- goes to
+    // slack[exact_off + node] for k_prep_band; null: no band (the opt-in fp32 precision, benches of
+    // the prep alone).  exact_counts: -inf also for nodes whose survivor count may differ (a candidate
+    // the full stage culls, a near-degenerate sliver) -- the mcpt_light_prep entry reports counts.
+    double* slack;
+    int exact_off;
+    int exact_counts;
 };
 
 // inverse-CDF pick from the batch totals bt[0, nb) and candidate list lst (LDS or global): returns
-// weights_sum and the picked light (-1 if weights_sum < eps).  u_of() gives dim 1 when needed.
+// weights_sum and the picked light (-1 if weights_sum < eps) and the pick's margin (pick_margin; +inf
+// without a pick).  u_of() gives dim 1 when needed.
 template <bool kF32 = false, class U>
 __device__ inline double prep_select(const double* bt, const unsigned short* lst, int nb, int ncand, int lane,
-                                     __amdgpu_buffer_rsrc_t rw, d3 x1, U u_of, int* pick_out) {
+                                     __amdgpu_buffer_rsrc_t rw, d3 x1, U u_of, int* pick_out, double* margin_out) {
     double wsum = 0;
     int pick = -1;
     int kb = -1;
@@ -1347,6 +1453,7 @@ __device__ inline double prep_select(const double* bt, const unsigned short* lst
             }
         }
     }
+    double margin = INFINITY;
     if (kb >= 0) {
         const int k = 64 * kb + lane;
         const bool act = k < ncand;
@@ -1368,9 +1475,13 @@ __device__ inline double prep_select(const double* bt, const unsigned short* lst
         int pl = -1;
         if (candm) pl = __ffsll((unsigned long long)candm) - 1;
         else if (okm) pl = 63 - __clzll((long long)okm);
-        if (pl >= 0) pick = __shfl(lj, pl);
+        if (pl >= 0) {
+            pick = __shfl(lj, pl);
+            margin = pick_margin(base, sc, pl, target);
+        }
     }
     *pick_out = pick;
+    *margin_out = margin;
     return wsum;
 }
 
@@ -1606,12 +1717,12 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                               : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
         };
         int ncand = 0, nb = 0, survivors = 0, culled1 = 0;
+        const uint64_t* __restrict__ mrow = kMaskIn ? masks + (size_t)node * mask_stride(nchunks) : nullptr;
         if (kMaskIn) {  // phase A done by k_prep_cull_lanes: rebuild the list from the candidate words
             // The node's words are wave-uniform: scalar loads of whole 64-B lines (s_load_dwordx16,
             // kMaskBatch words each, the row zero-padded to whole lines) put them straight into SGPRs,
             // so a word costs 3 VALU (2 v_mbcnt + 1 v_lshl_add) + 1 v_add for the index.
             const unsigned lds_lst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lst);  // LDS offset (low half of the flat address)
-            const uint64_t* __restrict__ mrow = masks + (size_t)node * mask_stride(nchunks);
             unsigned idx = (unsigned)lane;
             for (int c0 = 0; c0 < nchunks; c0 += kMaskBatch) {
                 uint64_t mw[kMaskBatch];
@@ -1672,6 +1783,8 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         // branch on the exec mask that is almost never taken except for the padding, instead of a
         // ballot per batch; survivors = ncand - (culled lanes - padding).
         int nbad = 0;
+        double sacc = 0;  // flagged slivers' error terms (this lane's candidates)
+        int ndeg = 0;     // near-degenerate slivers (this lane's)
         const NodeF32 xf = node_f32(x1);
         for (int b0 = 0; b0 < nb; b0 += 4) {
             double w4[4];
@@ -1702,11 +1815,22 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                 w4[i] = 0.0;
                 if (b0 + i < nb) {  // wave-uniform
                     const int k = 64 * (b0 + i) + lane;
-                    bool ok;
-                    const double w = prep_weight_buf(rw, (int)lst[k], x1, &ok);  // 0 if culled
-                    if (kBuild && k < ncand) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = ok ? w : -1.0;
-                    w4[i] = w;
-                    if (!ok) asm volatile("v_add_u32 %0, 1, %0" : "+v"(nbad));  // a real branch (SALU only when no lane is culled)
+                    double l2;
+                    const WeightBx r = prep_weight_buf_bx(rw, (int)lst[k], x1, &l2);  // w = 0 if culled
+                    if (kBuild && k < ncand) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = r.ok ? r.w : -1.0;
+                    w4[i] = r.w;
+                    // a real branch (SALU only when no lane is culled or a sliver): culled lanes (the
+                    // padding included) are counted, slivers add their term to the band
+                    if (!r.ok | r.sliver) {
+                        if (!r.ok) {
+                            asm volatile("v_add_u32 %0, 1, %0" : "+v"(nbad));
+                        } else {
+                            const double t = sliver_term(r.num, r.den) * l2;
+                            sacc += t;
+                            if (2.0 * r.w < 64.0 * kU53 * t)  // sA within the reference's error of 0
+                                asm volatile("v_add_u32 %0, 1, %0" : "+v"(ndeg));
+                        }
+                    }
                 }
             }
             }
@@ -1721,20 +1845,34 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         full_acc++;
         cand_acc += ncand;
         c1_acc += culled1;
-        if (kBuild) {  // store the entry of this pixel (C.build)
+        // the flagged slivers' band term (wave-uniform; almost always 0 without a wave reduction)
+        double band_sl = 0;
+        if (!kF32 && __ballot(sacc > 0.0)) band_sl = band_sliver(__shfl(wave_incl_scan(sacc, lane), 63));
+        if (kBuild) {  // store the entry of this pixel (C.build), with the node's band for k_prep_pick
             const int px = qpixel ? qpixel[node] : node;
             for (int b = lane; b < nb; b += 64) C.bt[(size_t)px * nchunks + b] = bt[b];
             for (int k = lane; k < ncand; k += 64) C.lst[(size_t)px * C.lstride + k] = lst[k];
-            if (lane == 0) C.info[px] = make_int4(nb, ncand, survivors, 0);
+            if (lane == 0) {
+                const double band = kF32 ? 0.0 : band_sl + band_base(S, x1, mrow, nchunks);
+                C.info[px] = make_int4(nb, ncand, survivors, __float_as_int((float)band * 1.001f));
+            }
             wave_lds_sync();
             continue;
         }
         int pick;
-        const double wsum = prep_select<kF32>(bt, lst, nb, ncand, lane, rw, x1, u_of, &pick);
+        double margin;
+        const double wsum = prep_select<kF32>(bt, lst, nb, ncand, lane, rw, x1, u_of, &pick, &margin);
         if (lane == 0) {
             wsum_out[node] = wsum;
             pick_out[node] = pick;
             if (count_out) count_out[node] = survivors;
+        }
+        if (!kF32 && C.slack) {  // exact pick: k_prep_band compares the slack with the per-chunk term
+            double sl = pick_slack(margin, wsum) - (band_sl + band_round(ncand, wsum));
+            // survivor counts: a candidate the full stage culls (the reference may keep it) or a
+            // near-degenerate sliver (the reference may cull it) -- survivors < ncand without padding
+            if (C.exact_counts && (survivors < ncand || __ballot(ndeg != 0))) sl = -INFINITY;
+            if (lane == 0) C.slack[C.exact_off + node] = sl;
         }
         wave_lds_sync();
     }
@@ -1863,9 +2001,11 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
         // the picked lane's light index only (one uniform load per root, issued for all roots
         // before waiting) instead of the batch's 64 list entries
         int pls[kPickNodes];
+        double margin[kPickNodes];
 #pragma unroll
         for (int k = 0; k < kPickNodes; k++) {
             pls[k] = -1;
+            margin[k] = INFINITY;
             if (kb[k] >= 0) {
                 const bool ok = wc[k] >= 0;
                 const double sc = wave_incl_scan(ok ? wc[k] : 0.0, lane);
@@ -1873,6 +2013,14 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
                 const uint64_t okm = __ballot(ok);
                 if (candm) pls[k] = __ffsll((unsigned long long)candm) - 1;
                 else if (okm) pls[k] = 63 - __clzll((long long)okm);
+                if (pls[k] >= 0) margin[k] = pick_margin(base[k], sc, pls[k], target[k]);
+            }
+        }
+        if (C.slack) {  // exact pick: the band stored by the cache build (same weights) + this sum's rounding
+#pragma unroll
+            for (int k = 0; k < kPickNodes; k++) {
+                const double band = (double)__int_as_float(inf[k].w) + band_round(inf[k].y, wsum[k]);
+                if (lane == 0 && n0 + k < n) C.slack[C.exact_off + n0 + k] = pick_slack(margin[k], wsum[k]) > band ? INFINITY : -INFINITY;
             }
         }
         int pk[kPickNodes];
@@ -1891,6 +2039,163 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
     }
     if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
 }
+
+// Exact pick, the band test's second half (lane per node): the per-chunk term of the
+// band against the slack the prep kernels left (k_prep_pk2 / k_prep: margin less the slivers' and the
+// rounding terms; k_prep_pick: +-inf, its cached band is complete).  The whole-table upper bound decides
+// almost every node; the node's candidate words are read only when it does not.  Nodes inside the band
+// are appended to the exact list (count in list[0], wave-aggregated).
+__global__ __launch_bounds__(256) void k_prep_band(DScene S, int n, const double* __restrict__ slack,
+                                                  const double* __restrict__ qp, const uint64_t* __restrict__ masks,
+                                                  int nchunks, int* __restrict__ list) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool amb = false;
+    if (i < n) {
+        const double sl = slack[i];
+        if (sl != INFINITY) {
+            if (!(sl > 0.0)) {
+                amb = true;
+            } else {
+                const d3 x1 = mk3(qp[3 * i], qp[3 * i + 1], qp[3 * i + 2]);
+                if (!(sl > band_base_upper(S, x1)))
+                    amb = !(sl > band_base(S, x1, masks ? masks + (size_t)i * mask_stride(nchunks) : nullptr, nchunks));
+            }
+        }
+    }
+    const int q = wave_append(reinterpret_cast<unsigned*>(list), amb);
+    if (amb) list[kExactHead + q] = i;
+}
+
+// Exact fallback of the light prep's pick.  For the nodes the prep kernels put on
+// the exact list (list[kExactHead + j] = node index, count in list[0]): the reference's own arithmetic
+// end to end -- the cheap culls (light_cheap_stage, Mylight.cpp:340-357), the literal full stage
+// (light_tri_stage: sqrt / division unit vectors, six acos, alpha + beta + gamma - pi,
+// Mylight.cpp:360-413), weights_sum summed candidate by candidate in index order (Mylight.cpp:415-418)
+// and the pick "first survivor whose running sum >= u weights_sum, else the last survivor" -- so
+// weights_sum, the survivor count and the pick are the oracle's bit for bit (up to libm's acos: ocml
+// vs glibc).  One wave per node: the candidate list and weights go to this wave's scratch slab;
+// the running sum is sequential (each lane adds the same broadcast weight in order, lane q keeps the
+// sum after candidate q), the pick a ballot search over the stored running sums.
+constexpr int kExactBlock = 256;
+constexpr int kExactBlocks = 256;  // grid-stride; the list is short (~1e-3 of the prep nodes)
+__global__ __launch_bounds__(kExactBlock) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
+                                                         const double* __restrict__ qp, const double* __restrict__ qn,
+                                                         const int* __restrict__ qpixel, const int* __restrict__ qsample,
+                                                         const uint64_t* __restrict__ qnode,
+                                                         const double* __restrict__ u_override, double* __restrict__ wsum_out,
+                                                         int* __restrict__ pick_out, int* __restrict__ count_out,
+                                                         unsigned long long* stats, double* __restrict__ scratch) {
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * (kExactBlock / 64);
+    const int gw = blockIdx.x * (kExactBlock / 64) + (threadIdx.x >> 6);
+    const int nlp = (S.NL + 63) & ~63;
+    double* wsc = scratch + (size_t)gw * nlp;                  // candidates' weights, then running sums
+    int* lst = reinterpret_cast<int*>(scratch + (size_t)waves * nlp) + (size_t)gw * nlp;  // candidate list
+    const int cnt = list[0];
+    if (gw == 0 && lane == 0 && stats && cnt) atomicAdd(stats + 10, (unsigned long long)cnt);
+    for (int j = gw; j < cnt; j += waves) {
+        const int node = list[kExactHead + j];
+        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        int ncand = 0;
+        for (int c = 0; c < S.NL; c += 64) {  // cheap stages, candidates compacted in index order
+            const int li = c + lane;
+            bool cand = false;
+            if (li < S.NL) {
+                const double4 ln = S.lt_n[li];
+                cand = light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                         mk3(ln.x, ln.y, ln.z), x1, nn) == 0;
+            }
+            const uint64_t m = __ballot(cand);
+            if (cand) lst[ncand + lane_rank(m)] = li;
+            ncand += __popcll(m);
+        }
+        wave_lds_sync();
+        for (int k0 = 0; k0 < ncand; k0 += 64) {  // the literal full stage, 64 candidates at a time
+            const int k = k0 + lane;
+            if (k < ncand) {
+                const int li = lst[k];
+                const double4 ln = S.lt_n[li];
+                SphTri o;
+                const int st = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                               mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
+                wsc[k] = st == 0 ? o.w : -1.0;
+            }
+        }
+        wave_lds_sync();
+        double run = 0;  // the reference's weights_sum, in its order
+        int surv = 0;
+        for (int k0 = 0; k0 < ncand; k0 += 64) {
+            const bool in = k0 + lane < ncand;
+            const double wv = in ? wsc[k0 + lane] : -1.0;
+            const int nk = min(64, ncand - k0);
+            double mine = -1.0;
+            for (int q = 0; q < nk; q++) {
+                const double wq = __shfl(wv, q);
+                run += fmax(wq, 0.0);  // a culled candidate (-1) adds +0, leaving the sum unchanged
+                mine = lane == q ? (wq >= 0.0 ? run : -1.0) : mine;
+            }
+            surv += __popcll(__ballot(in && wv >= 0.0));
+            if (in) wsc[k0 + lane] = mine;  // running sum after this survivor, -1 if culled
+        }
+        wave_lds_sync();
+        int pick = -1;
+        if (!(fabs(run) < MCPT_EPS)) {
+            const double u = u_override ? u_override[node]
+                                        : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+            const double target = u * run;
+            int found = -1, last = -1;
+            for (int k0 = 0; k0 < ncand && found < 0; k0 += 64) {
+                const bool in = k0 + lane < ncand;
+                const double rv = in ? wsc[k0 + lane] : -1.0;
+                const uint64_t hm = __ballot(rv >= 0.0 && rv >= target);
+                const uint64_t sm = __ballot(rv >= 0.0);
+                if (hm) found = k0 + __ffsll((unsigned long long)hm) - 1;
+                if (sm) last = k0 + 63 - __clzll((long long)sm);
+            }
+            const int at = found >= 0 ? found : last;
+            if (at >= 0) pick = lst[at];
+        }
+        if (lane == 0) {
+            wsum_out[node] = run;
+            pick_out[node] = pick;
+            if (count_out) count_out[node] = surv;
+        }
+        wave_lds_sync();
+    }
+}
+// diagnostics (mcpt_debug_light_literal): the literal chain's intermediates for every light at one point,
+// 20 doubles per light: stage, A, B, C (after the orientation swap), a, b, c, alpha, beta, gamma, sA, w
+__global__ void k_light_literal(DScene S, d3 x1, d3 nn, double* out) {
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= S.NL) return;
+    const double4 ln = S.lt_n[li];
+    const d3 p0 = f3(S.lt_v[3 * li]), p1 = f3(S.lt_v[3 * li + 1]), p2 = f3(S.lt_v[3 * li + 2]);
+    double* o = out + 20 * (size_t)li;
+    for (int k = 0; k < 20; k++) o[k] = 0;
+    SphTri t;
+    o[0] = light_tri_stage(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &t);
+    // recompute the angles the same way (light_tri_stage keeps only alpha, c)
+    d3 A = normalized(sub(p0, x1)), B = normalized(sub(p1, x1)), C = normalized(sub(p2, x1));
+    if (dot(cross(normalized(sub(C, A)), normalized(sub(B, A))), nn) < 0) {
+        const d3 tt = B;
+        B = C;
+        C = tt;
+    }
+    o[1] = A.x, o[2] = A.y, o[3] = A.z, o[4] = B.x, o[5] = B.y, o[6] = B.z, o[7] = C.x, o[8] = C.y, o[9] = C.z;
+    o[10] = acos(fmax(-1.0, fmin(1.0, dot(B, C))));
+    o[11] = acos(fmax(-1.0, fmin(1.0, dot(A, C))));
+    o[12] = acos(fmax(-1.0, fmin(1.0, dot(A, B))));
+    o[13] = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(B, A)), normalized(cross(A, C))))));
+    o[14] = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(C, B)), normalized(cross(B, A))))));
+    o[15] = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(A, C)), normalized(cross(C, B))))));
+    o[16] = o[13] + o[14] + o[15] - MCPT_PI;
+    o[17] = o[0] == 0 ? t.w : -1.0;
+    o[18] = -dot(normalized(cross(B, A)), normalized(cross(A, C)));  // alpha's acos argument
+    o[19] = dot(B, C);
+}
+// scratch doubles k_prep_exact needs (per wave: weights + list)
+inline size_t exact_scratch_doubles(int NL) { return (size_t)kExactBlocks * (kExactBlock / 64) * 2 * (size_t)((NL + 63) & ~63); }
 
 // ---- MIS node split into three kernels (ray generation / traversal / combination) -------------
 // (one MIS node per lane with three inlined traversals measured 152 VGPRs, 3 waves/SIMD.)  Split,
@@ -2786,6 +3091,7 @@ struct DeviceState {
     hipStream_t stream = nullptr;
     // reusable work buffers
     DevBuf hit_f, hit_tbg, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[9], sl[13], cache_bt, cache_lst, cache_info, cache_w, masks;
+    DevBuf exact, exact_scr, slack;  // exact pick: list, k_prep_exact's scratch, per-node slack
     int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
@@ -3007,6 +3313,58 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
         }
     }
     if ((rc = upload(*D, lpr, &d.lt_pair))) return rc;
+    {  // exact-pick band tables: the chunk spheres are conservative (radius rounded up by 1e-6 relative)
+        const int nch = prep_chunks(s.NL);
+        std::vector<float4> sph(nch, make_float4(0, 0, 0, 0));
+        std::vector<float2> sk(nch, make_float2(0, 0));
+        double lo_s[3] = {1e300, 1e300, 1e300}, hi_s[3] = {-1e300, -1e300, -1e300};
+        double smax = 0, kmax = 0;
+        for (int c = 0; c < nch; c++) {
+            double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+            const int l0 = 64 * c, l1 = std::min(s.NL, 64 * c + 64);
+            for (int l = l0; l < l1; l++)
+                for (int k = 0; k < 3; k++) {
+                    const double p[3] = {lv[3 * l + k].x, lv[3 * l + k].y, lv[3 * l + k].z};
+                    for (int a = 0; a < 3; a++) {
+                        lo[a] = std::min(lo[a], p[a]);
+                        hi[a] = std::max(hi[a], p[a]);
+                        lo_s[a] = std::min(lo_s[a], p[a]);
+                        hi_s[a] = std::max(hi_s[a], p[a]);
+                    }
+                }
+            if (l1 <= l0) continue;
+            // the centre as stored (float), so R bounds the distances from the centre the kernels read
+            const double ctr[3] = {(double)(float)(0.5 * (lo[0] + hi[0])), (double)(float)(0.5 * (lo[1] + hi[1])),
+                                   (double)(float)(0.5 * (lo[2] + hi[2]))};
+            double R = 0, S = 0, K = 0;
+            for (int l = l0; l < l1; l++) {
+                double lmin = 1e300;
+                for (int k = 0; k < 3; k++) {
+                    const float4 a = lv[3 * l + k], b = lv[3 * l + (k + 1) % 3];
+                    const double dx = (double)a.x - ctr[0], dy = (double)a.y - ctr[1], dz = (double)a.z - ctr[2];
+                    R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz));
+                    const double ex = (double)b.x - a.x, ey = (double)b.y - a.y, ez = (double)b.z - a.z;
+                    lmin = std::min(lmin, std::sqrt(ex * ex + ey * ey + ez * ez));
+                }
+                S = std::max(S, s.light_sum[l]);
+                K = std::max(K, lmin > 0 ? s.light_sum[l] / lmin : 1e30);
+            }
+            sph[c] = make_float4((float)ctr[0], (float)ctr[1], (float)ctr[2], (float)(R * (1 + 1e-6) + 1e-6));
+            sk[c] = make_float2((float)(S * (1 + 1e-6)), (float)std::min(K * (1 + 1e-6), 1e30));
+            smax = std::max(smax, S);
+            kmax = std::max(kmax, K);
+        }
+        double Rs = 0;
+        for (int a = 0; a < 3; a++) d.band_ctr[a] = s.NL > 0 ? 0.5 * (lo_s[a] + hi_s[a]) : 0.0;
+        for (int c = 0; c < nch; c++) {  // the scene sphere contains every chunk sphere
+            const double dx = sph[c].x - d.band_ctr[0], dy = sph[c].y - d.band_ctr[1], dz = sph[c].z - d.band_ctr[2];
+            Rs = std::max(Rs, std::sqrt(dx * dx + dy * dy + dz * dz) + sph[c].w);
+        }
+        d.band_R = Rs * (1 + 1e-6) + 1e-6;
+        d.band_S = smax * (1 + 1e-6);
+        d.band_K = std::min(kmax * (1 + 1e-6), 1e30);
+        if ((rc = upload(*D, sph, &d.chunk_sph)) || (rc = upload(*D, sk, &d.chunk_sk))) return rc;
+    }
     if ((rc = upload(*D, lpk, &d.lt_pk))) return rc;
     if ((rc = upload(*D, ld, &d.lt_d))) return rc;
     if ((rc = upload(*D, lw, &d.lt_w))) return rc;
@@ -3198,7 +3556,8 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     if (e != hipSuccess) return e;
     if (variant == 0) {
         hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
-                           qsample, qnode, u, wsum, pick, count, stats, nchunks, work);
+                           qsample, qnode, u, wsum, pick, count, stats, nchunks, work, cache.slack, cache.exact_off,
+                           cache.exact_counts);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
         if (count_c1 || !stats)
             hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
@@ -3221,13 +3580,27 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     return hipGetLastError();
 }
 
-// builds the scene's uniform grid for (eye, n0) unless it already is, and brings D's copy up to date
-int use_grid(mcpt_scene* sc, DeviceState& D, const double eye[3], int n0) {
+// builds the scene's uniform grid for (eye, n0) unless it already is (host side; NOT thread-safe:
+// render_multi calls it on the calling thread before its device workers start, so the workers only
+// find an up-to-date grid and read it)
+int ensure_host_grid(mcpt_scene* sc, const double eye[3], int n0) {
     Grid& g = sc->grid;
     if (!g.ok || g.n0 != n0 || g.eye[0] != eye[0] || g.eye[1] != eye[1] || g.eye[2] != eye[2]) {
         g = build_grid(sc->host, eye, n0);
         sc->grid_version++;
     }
+    if (!g.ok) {
+        set_error("the scene's bounding box has zero or non-finite extent: no uniform grid (Myobj.cpp:110-162)");
+        return MCPT_E_SCENE;
+    }
+    return MCPT_OK;
+}
+
+// ensure_host_grid, then brings D's copy up to date
+int use_grid(mcpt_scene* sc, DeviceState& D, const double eye[3], int n0) {
+    int rg;
+    if ((rg = ensure_host_grid(sc, eye, n0))) return rg;
+    const Grid& g = sc->grid;
     if (D.grid_version != sc->grid_version) {
         int rc;
         if ((rc = ensure(D.g_start, g.cell_start.size() * 4)) || (rc = ensure(D.g_tri, g.cell_tri.size() * 4))) return rc;
@@ -3345,13 +3718,26 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     }
     const bool count_c1 = !(o->flags & MCPT_RENDER_NO_BACKFACE_STATS);
     const bool fp32 = (o->flags & MCPT_RENDER_PRECISION_FP32) != 0;
-    double prep_ms = 0, trace_ms = 0;
+    double prep_ms = 0, trace_ms = 0, cache_ms = 0;
     uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0, trace_launches = 0;
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
     if (needs_prep && D.d.NL > kSmallNL) {
         if ((rc = ensure(D.masks, (size_t)std::max(cap, npx) * mask_stride(nchunks) * 8))) return rc;
         masks = (uint64_t*)D.masks.p;
+    }
+    // exact pick: nodes inside the ambiguity band go to k_prep_exact; the opt-in fp32
+    // precision makes no exactness claim, and the small-table prep (k_prep_lane) is exact by construction
+    const bool exact_pick = needs_prep && !fp32 && D.d.NL > kSmallNL;
+    int* exact_list = nullptr;
+    double *exact_scr = nullptr, *slack = nullptr;
+    if (exact_pick) {
+        if ((rc = ensure(D.exact, 4ull * ((size_t)cap + kExactHead))) ||
+            (rc = ensure(D.exact_scr, 8 * exact_scratch_doubles(D.d.NL))) || (rc = ensure(D.slack, 8ull * cap)))
+            return rc;
+        exact_list = (int*)D.exact.p;
+        exact_scr = (double*)D.exact_scr.p;
+        slack = (double*)D.slack.p;
     }
     // root-point cache (see PrepCache): built here when the call has >= 2 samples per pixel and the
     // entries fit in the free HBM less a 16 GiB reserve (800x600 with N_L = 3012: 15 GB; 1600x1200:
@@ -3401,6 +3787,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             float ms = 0;
             HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
             prep_ms += ms;
+            cache_ms = ms;
             prep_launches++;
             cache_points = (uint64_t)nr;
         }
@@ -3512,32 +3899,46 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         // prep_seconds / prep_launches time the full light-prep kernel (k_prep_pk2) launches only
         bool timed = false;
         if (needs_prep) {
+            PrepCache cx{};  // the children's full prep: no cache, the picks' slack
+            cx.slack = slack;
+            if (exact_pick) HIP_OK(hipMemsetAsync(exact_list, 0, 4, st));
             if (pc.use) {  // children: full prep; roots: pick from the root-point cache
                 const int nc = (int)n_children, nr = ni - nc;
                 if (nc > 0) {
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks,
+                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
                                        count_c1, fp32));
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
                 if (nr > 0) {
+                    PrepCache pr = pc;
+                    pr.slack = slack;
+                    pr.exact_off = nc;
                     const int blocks = std::max(1, std::min((nr + 4 * kPickNodes - 1) / (4 * kPickNodes), 8192));
                     hipLaunchKernelGGL(k_prep_pick, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
                                        cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats, nchunks,
-                                       pc);
+                                       pr);
                     HIP_OK(hipGetLastError());
                 }
             } else {
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
-                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, PrepCache{}, masks,
+                                   cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
                                    count_c1, fp32));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 timed = true;
             }
             prep_launches += timed;
+            if (exact_pick) {  // the band's nodes: the reference's literal prep and pick
+                hipLaunchKernelGGL(k_prep_band, dim3((ni + 255) / 256), dim3(256), 0, st, D.d, ni, slack, cur->p, masks,
+                                   nchunks, exact_list);
+                hipLaunchKernelGGL(k_prep_exact, dim3(kExactBlocks), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
+                                   cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
+                                   nullptr, P.stats, exact_scr);
+                HIP_OK(hipGetLastError());
+            }
         }
         HIP_OK(hipMemsetAsync(nxt->count, 0, 4, st));
         const dim3 g256((ni + 255) / 256), b256(256);
@@ -3656,6 +4057,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->devices_used = 1;
         stats->prep_seconds = prep_ms * 1e-3;
         stats->prep_launches = prep_launches;
+        stats->prep_exact_nodes = hs[10];
+        stats->cache_build_seconds = cache_ms * 1e-3;
     }
     return MCPT_OK;
 }
@@ -3738,6 +4141,8 @@ void add_stats(mcpt_stats& t, const mcpt_stats& x) {
     t.trace_launches += x.trace_launches;
     t.node_visits += x.node_visits;
     t.tri_tests += x.tri_tests;
+    t.prep_exact_nodes += x.prep_exact_nodes;
+    t.cache_build_seconds += x.cache_build_seconds;
 }
 
 // progress of a multi-device call: the shards' dispatched counts are summed and the caller's callback
@@ -3928,6 +4333,75 @@ int render_rank(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mc
         stats->reduce_seconds = ms * 1e-3;
         stats->devices_used = 1;
     }
+    return MCPT_OK;
+}
+
+// mcpt_light_prep (all_exact = false: the renderer's prep kernels, the band's nodes redone by
+// k_prep_exact, which also takes the nodes whose survivor count may differ) and
+// mcpt_debug_light_prep_exact (all_exact: every node through k_prep_exact alone)
+int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* nrm, const double* u, double* wsum,
+                     int32_t* count, int32_t* pick, bool all_exact) {
+    if (!sc || n < 0 || (n && (!x1 || !nrm || !u || !wsum || !count || !pick))) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    if (n == 0) return MCPT_OK;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    DeviceState* D;
+    int rc;
+    if ((rc = get_device_state(sc, -1, &D))) return rc;
+    const bool exact = D->d.NL > kSmallNL;  // k_prep_lane is exact by construction
+    if (all_exact && !exact) {
+        set_error("the exact prep applies to scenes with more than %d light triangles", kSmallNL);
+        return MCPT_E_INVALID;
+    }
+    void *dp, *dn, *du, *dw, *dc, *dk, *dm, *dl = nullptr, *ds = nullptr, *dsl = nullptr;
+    HIP_OK(hipMalloc(&dm, 8ull * n * mask_stride(prep_chunks(D->d.NL))));  // candidate words of the split prep (variant 17)
+    HIP_OK(hipMalloc(&dp, 24ull * n));
+    HIP_OK(hipMalloc(&dn, 24ull * n));
+    HIP_OK(hipMalloc(&du, 8ull * n));
+    HIP_OK(hipMalloc(&dw, 8ull * n));
+    HIP_OK(hipMalloc(&dc, 4ull * n));
+    HIP_OK(hipMalloc(&dk, 4ull * n));
+    if (exact) {
+        HIP_OK(hipMalloc(&dl, 4ull * (n + kExactHead)));
+        HIP_OK(hipMalloc(&ds, 8 * exact_scratch_doubles(D->d.NL)));
+        HIP_OK(hipMalloc(&dsl, 8ull * n));
+        HIP_OK(hipMemset(dl, 0, 4));
+    }
+    HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
+    if ((rc = ensure(D->work, 256))) return rc;
+    if (all_exact) {
+        std::vector<int> all(n + kExactHead, 0);
+        all[0] = n;
+        for (int k = 0; k < n; k++) all[kExactHead + k] = k;
+        HIP_OK(hipMemcpy(dl, all.data(), 4ull * all.size(), hipMemcpyHostToDevice));
+    } else {
+        PrepCache cx{};
+        cx.slack = (double*)dsl;
+        cx.exact_counts = 1;
+        HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+                           (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream,
+                           cx, (uint64_t*)dm));
+        if (exact)
+            hipLaunchKernelGGL(k_prep_band, dim3((n + 255) / 256), dim3(256), 0, D->stream, D->d, n, (const double*)dsl,
+                               (const double*)dp, (const uint64_t*)dm, prep_chunks(D->d.NL), (int*)dl);
+    }
+    if (exact)
+        hipLaunchKernelGGL(k_prep_exact, dim3(kExactBlocks), dim3(kExactBlock), 0, D->stream, D->d, (uint64_t)0,
+                           (const int*)dl, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+                           (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (double*)ds);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(D->stream));
+    HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(count, dc, 4ull * n, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
+    for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
+    void* bufs[] = {dp, dn, du, dw, dc, dk, dm, dl, ds, dsl};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
     return MCPT_OK;
 }
 
@@ -4168,6 +4642,10 @@ int mcpt_scene_meshing(mcpt_scene* sc, const double eye[3], int32_t n0) {
     std::lock_guard<std::mutex> lk(sc->mu);
     sc->grid = build_grid(sc->host, eye, n0);
     sc->grid_version++;
+    if (!sc->grid.ok) {
+        set_error("the scene's bounding box has zero or non-finite extent: no uniform grid (Myobj.cpp:110-162)");
+        return MCPT_E_SCENE;
+    }
     return MCPT_OK;
 }
 
@@ -4234,37 +4712,33 @@ int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* 
 
 int mcpt_light_prep(mcpt_scene* sc, int32_t n, const double* x1, const double* nrm, const double* u, double* wsum,
                     int32_t* count, int32_t* pick) {
-    if (!sc || n < 0 || (n && (!x1 || !nrm || !u || !wsum || !count || !pick))) {
+    return light_prep_query(sc, n, x1, nrm, u, wsum, count, pick, false);
+}
+
+int mcpt_debug_light_prep_exact(mcpt_scene* sc, int32_t n, const double* x1, const double* nrm, const double* u,
+                                double* wsum, int32_t* count, int32_t* pick) {
+    return light_prep_query(sc, n, x1, nrm, u, wsum, count, pick, true);
+}
+
+int mcpt_debug_light_literal(mcpt_scene* sc, const double* x1, const double* nrm, double* out) {
+    if (!sc || !x1 || !nrm || !out) {
         set_error("invalid argument");
         return MCPT_E_INVALID;
     }
-    if (n == 0) return MCPT_OK;
     std::lock_guard<std::mutex> lk(sc->mu);
     DeviceState* D;
     int rc;
     if ((rc = get_device_state(sc, -1, &D))) return rc;
-    void *dp, *dn, *du, *dw, *dc, *dk, *dm;
-    HIP_OK(hipMalloc(&dm, 8ull * n * mask_stride(prep_chunks(D->d.NL))));  // candidate words of the split prep (variant 17)
-    HIP_OK(hipMalloc(&dp, 24ull * n));
-    HIP_OK(hipMalloc(&dn, 24ull * n));
-    HIP_OK(hipMalloc(&du, 8ull * n));
-    HIP_OK(hipMalloc(&dw, 8ull * n));
-    HIP_OK(hipMalloc(&dc, 4ull * n));
-    HIP_OK(hipMalloc(&dk, 4ull * n));
-    HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
-    if ((rc = ensure(D->work, 256))) return rc;
-    HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
-                       (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream,
-                       PrepCache{}, (uint64_t*)dm));
+    const int NL = D->d.NL;
+    if (NL == 0) return MCPT_OK;
+    void* dout;
+    HIP_OK(hipMalloc(&dout, 160ull * NL));
+    hipLaunchKernelGGL(k_light_literal, dim3((NL + 255) / 256), dim3(256), 0, D->stream, D->d, mk3(x1[0], x1[1], x1[2]),
+                       mk3(nrm[0], nrm[1], nrm[2]), (double*)dout);
+    HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
-    HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(count, dc, 4ull * n, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
-    for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
-    void* bufs[] = {dp, dn, du, dw, dc, dk, dm};
-    for (void* b : bufs) (void)hipFree(b);
+    HIP_OK(hipMemcpy(out, dout, 160ull * NL, hipMemcpyDeviceToHost));
+    (void)hipFree(dout);
     return MCPT_OK;
 }
 

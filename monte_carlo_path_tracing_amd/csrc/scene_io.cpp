@@ -209,6 +209,12 @@ bool load_obj_mtl(const std::string& obj_path, HostScene& s, std::string& err) {
                     err = obj_path + ": face without a vertex normal (the reference reads normal_index >= 0)";
                     return false;
                 }
+                // an index past the vertices / normals read so far (found by the sanitizer build:
+                // it was read out of bounds)
+                if ((size_t)va >= V.size() / 3 || (size_t)na >= N.size() / 3) {
+                    err = obj_path + ": face index out of range";
+                    return false;
+                }
                 vi.push_back(va);
                 ni.push_back(na);
             }

@@ -12,6 +12,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <sys/stat.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -179,14 +180,18 @@ static float tobj_real(const char** tok, double dflt) {
     return (float)val;
 }
 
+/* whole file + "\n\0"; NULL if it cannot be read as a regular file (a directory opens but has no
+ * size: found by the sanitizer build, `make -C monte_carlo_path_tracing_amd/csrc sanitize`).  Embedded
+ * NUL bytes end the text there (the line loops below stop at the first NUL). */
 static char* read_file(const char* path, size_t* len) {
     FILE* f = fopen(path, "rb");
     if (!f) return NULL;
-    fseek(f, 0, SEEK_END);
+    struct stat st;
+    if (fstat(fileno(f), &st) != 0 || !S_ISREG(st.st_mode) || fseek(f, 0, SEEK_END) != 0) { fclose(f); return NULL; }
     long n = ftell(f);
-    fseek(f, 0, SEEK_SET);
+    if (n < 0 || fseek(f, 0, SEEK_SET) != 0) { fclose(f); return NULL; }
     char* b = (char*)malloc((size_t)n + 2);
-    if (n > 0 && fread(b, 1, (size_t)n, f) != (size_t)n) { fclose(f); free(b); return NULL; }
+    if (!b || (n > 0 && fread(b, 1, (size_t)n, f) != (size_t)n)) { fclose(f); free(b); return NULL; }
     fclose(f);
     b[n] = '\n';
     b[n + 1] = 0;
@@ -215,6 +220,7 @@ static int load_mtl(const char* path, vecbuf* mats) {
     int have = 0;
     for (char* line = buf; *line;) {
         char* nl = strchr(line, '\n');
+        if (!nl) break; /* an embedded NUL ends the text */
         *nl = 0;
         const char* t = line + strspn(line, " \t");
         if (!strncmp(t, "newmtl", 6) && (t[6] == ' ' || t[6] == '\t')) {
@@ -269,6 +275,7 @@ static int load_obj(orc_scene* s, const char* path) {
     int cur_mat = -1, ok = 1;
     for (char* line = buf; *line && ok;) {
         char* nl = strchr(line, '\n');
+        if (!nl) break; /* an embedded NUL ends the text */
         *nl = 0;
         const char* t = line + strspn(line, " \t");
         if (t[0] == 'v' && (t[1] == ' ' || t[1] == '\t')) {
@@ -299,6 +306,11 @@ static int load_obj(orc_scene* s, const char* path) {
                 t += strcspn(t, " \t\r");
                 if (!fix_index(a, (long)V.n, &vi[nv]) || c == 0 || !fix_index(c, (long)N.n, &ni[nv])) {
                     set_err("%s: face without vertex normal (the reference needs normal_index >= 0)", path);
+                    ok = 0;
+                    break;
+                }
+                if (vi[nv] < 0 || vi[nv] >= (long)V.n || ni[nv] < 0 || ni[nv] >= (long)N.n) { /* sanitizer build */
+                    set_err("%s: face index out of range", path);
                     ok = 0;
                     break;
                 }
@@ -589,6 +601,10 @@ void orc_grid_build(orc_scene* s, const double cam[3], int n0) {
     double len[3];
     for (int i = 0; i < 3; i++) len[i] = s->mm[i][1] - s->mm[i][0];
     double d = fmax(fmax(len[0], len[1]), len[2]) / pow(n0, 1.0 / 3);
+    /* a box of zero or non-finite extent has no cell size (the reference divides by it): no grid,
+     * queries fail (found by the sanitizer build, like grid.cpp's guard) */
+    s->grid_ok = 0;
+    if (!(d > 0) || !isfinite(d) || !isfinite(len[0] + len[1] + len[2])) return;
     s->d = d;
     s->inv_d = 1.0 / d;
     for (int i = 0; i < 3; i++) {
@@ -596,6 +612,7 @@ void orc_grid_build(orc_scene* s, const double cam[3], int n0) {
         s->gd[i] = s->lim[i] + 1;
     }
     size_t ncell = (size_t)s->gd[0] * s->gd[1] * s->gd[2];
+    if (ncell > ((size_t)1 << 31)) return;
     free(s->cell_start);
     free(s->cell_tri);
     s->cell_start = (int*)calloc(ncell + 1, sizeof(int));
@@ -618,8 +635,9 @@ void orc_grid_build(orc_scene* s, const double cam[3], int n0) {
                         xyz[i][1] = fmax(xyz[i][1], (double)s->v[9 * f + 3 * v + i]);
                     }
                 for (int k = 0; k < 3; k++) {
-                    rng[f][k][0] = (int)floor((xyz[k][0] - s->mm[k][0]) / d);
-                    rng[f][k][1] = (int)floor((xyz[k][1] - s->mm[k][0]) / d);
+                    const int fin = isfinite(xyz[k][0]) && isfinite(xyz[k][1]); /* else listed nowhere */
+                    rng[f][k][0] = fin ? (int)floor((xyz[k][0] - s->mm[k][0]) / d) : 1;
+                    rng[f][k][1] = fin ? (int)floor((xyz[k][1] - s->mm[k][0]) / d) : 0;
                 }
             }
             for (int i = rng[f][0][0]; i <= rng[f][0][1]; i++)
@@ -660,6 +678,7 @@ static inline hitrec tri_hit(const orc_scene* s, v3 ro, v3 rd, int f) {
 /* light_only: Myobj.cpp:476-622 (skip non-light triangles; step every tied axis) */
 static int grid_trace(const orc_scene* s, v3 ro, v3 rd, int exclude, int light_only, hitrec* out) {
     out->hit = 0;
+    if (!s->grid_ok) return -1;
     if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return -1;  /* reference: UB (Myobj.cpp:463-468) */
     const double mn[3] = {s->mm[0][0], s->mm[1][0], s->mm[2][0]};
     v3 x0v = vmul(vsub(ro, mk(mn[0], mn[1], mn[2])), s->inv_d);

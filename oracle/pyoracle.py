@@ -8,7 +8,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("MCPT_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")  # override: the sanitizer build
 
 MODE_MIS, MODE_BRDF, MODE_SHADE, MODE_SHADE_AREA = 0, 1, 2, 3  # ORC_MODE_* (mcpt_oracle.h)
 FLAG_FRESH_PDF = 0x200  # ORC_FLAG_FRESH_PDF: or into MODE_MIS for the node's own light pdf instead of the reference's stale one

@@ -1,4 +1,4 @@
-"""Host-side mirror of the library's multi-GPU partitioning of a frame.
+"""Test helper: host-side mirror of the library's multi-GPU partitioning of a frame.
 
 Every (pixel, sample) is independent (main.cpp:557-588) and the RNG is keyed by the GLOBAL sample
 index, so a frame shards by sample range with no data-path exchange.  The library

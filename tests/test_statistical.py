@@ -7,8 +7,9 @@ sampler: the spherical one of main.cpp:297 and select_a_point_from_lights of mai
 shade_with_brdf at 65536 spp (its tiny bright lights make it heavy-tailed).  The GPU renders the
 same frame at 64x-1024x more samples, so its mean is the estimator's expectation to well below the
 reference's standard error; the test then checks, per integrator:
-  * whole-frame z = (sum ref - sum gpu) / sqrt(sum var_ref / n) within +-4 (this also bounds the
-    effect of the stale-pdf quirk the counter path removes, SURVEY.md §0 item 5);
+  * whole-frame z = (sum ref - sum gpu) / sqrt(sum var_ref / n) within +-4 (the counter path
+    reproduces the stale-pdf quirk of SURVEY.md §0 item 5 -- the bottom-up reduction of DESIGN.md
+    §4.6 -- so only the RNG differs between the two);
   * per-pixel median |z| <= 1.0 (0.674 for a normal; heavy tails widen it a little);
   * pixels with zero reference variance (emitters seen directly) equal.
 The BRDF-only and MIS expectations differ by ~15% on this scene: the reference's sample_from_phong
