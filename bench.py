@@ -9,7 +9,9 @@ steps x gpus x spp_per_step samples per pixel.
 Each call computes everything it uses, including its root-point light-prep cache (DESIGN.md §4.4);
 nothing is carried from one step to the next except the framebuffer.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling by sample-range sharding.  Every rank joins
+Multi-GPU (torchrun, one process per GPU): sample-range sharding -- weak scaling for --config c3 (each
+rank S samples per step), strong scaling for --config c4 (1600x1200, one 4096-spp frame per step split
+over the ranks, BASELINE.json configs[3]).  Every rank joins
 the library's own RCCL communicator (mcpt_comm: rank 0's ncclUniqueId is broadcast over
 torch.distributed, then mcpt_comm_init_rank); step k is the job [k*G*S, (k+1)*G*S) of global sample
 indices, which the library splits into one S-sample shard per rank and ends with ONE ncclReduce(sum)
@@ -53,8 +55,14 @@ FP32_VECTOR_PEAK_TFLOPS = 157.3
 GATHER_PEAKS = [(4 << 20, "l2", 17800.0), (256 << 20, "infinity_cache", 8600.0), (1 << 62, "hbm", HBM_PEAK_GBS)]
 FLOPS_NODE_VISIT = 48
 FLOPS_TRI_TEST_FP64 = 74
-BYTES_NODE_VISIT = 128
+# bytes one node visit fetches: the 128-B BvhNode4 (k_mis_rays, k_extend_brdf) or the 64-B compressed
+# BvhNode4Q that k_rays_persistent reads ("Compressed nodes")
+BYTES_NODE_VISIT = {"k_mis_rays": 128, "k_extend_brdf": 128, "k_rays_persistent": 64}
 BYTES_TRI_TEST = 48
+# --config: BASELINE.json configs as bench workloads.  c3 (default) is the metric's configuration;
+# c4 is the 1600x1200 frame whose 4096-spp job is split over the ranks (strong scaling)
+CONFIGS = {"c3": dict(width=800, height=600, job_spp=None, scaling="weak"),
+           "c4": dict(width=1600, height=1200, job_spp=4096, scaling="strong")}
 SCENE = os.path.join(ROOT, "scenes", "veach-mis")
 SCENES = {  # --scene: (metric, data note)
     "veach": (METRIC, "synthetic: Veach-MIS stand-in scene (scenes/gen_veach_mis.py; the reference's scene files are missing)"),
@@ -154,8 +162,11 @@ def main():
     # Msamples/s; round 2e: 256 -> 467-468, 1024 -> 480-481); the default step is the whole
     # 1024-spp frame of BASELINE.json in one call, as the reference renders it
     ap.add_argument("--spp-per-step", type=int, default=1024)
-    ap.add_argument("--width", type=int, default=800)
-    ap.add_argument("--height", type=int, default=600)
+    ap.add_argument("--width", type=int, default=None, help="default: the --config's (800)")
+    ap.add_argument("--height", type=int, default=None, help="default: the --config's (600)")
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="c3: BASELINE.json's metric config (800x600, spp_per_step samples per rank, weak scaling); "
+                         "c4: 1600x1200, each step one 4096-spp frame split over the ranks (strong scaling)")
     ap.add_argument("--mode", default="mis", choices=["mis", "brdf", "shade", "shade_area"])
     ap.add_argument("--scene", default="veach", choices=sorted(SCENES),
                     help="veach: the north-star workload (C3); cornell1m: config C5")
@@ -196,7 +207,15 @@ def main():
         if world > 1:
             dist.barrier()
 
-    W, H, S = args.width, args.height, args.spp_per_step
+    cfg = CONFIGS[args.config]
+    W = args.width or cfg["width"]
+    H = args.height or cfg["height"]
+    if cfg["job_spp"]:  # strong scaling: the step's job is fixed, split over the ranks by the library
+        if cfg["job_spp"] % world:
+            raise SystemExit("--config %s: %d spp do not split over %d ranks" % (args.config, cfg["job_spp"], world))
+        S = cfg["job_spp"] // world
+    else:
+        S = args.spp_per_step
     frame_spp = args.steps * world * S
     obj, xml, xml_cam = scene_files(args.scene)
     scene = mcpt.Scene.load(obj, xml)
@@ -261,7 +280,9 @@ def main():
         return
     pmc = load_json(os.path.join(ROOT, "profiles", "pmc_latest.json")) or {"kernels": {}}
     pk = pmc["kernels"]
-    busy = lambda *names: {n: pk[n]["valu_busy"] for n in names if n in pk}  # noqa: E731
+    # bounded VALU figure from the SQ pass (tools/summarize_profiles.py): 4 x SQ_INSTS_VALU / (SIMDs x
+    # cycles) -- the issue slots the kernel's VALU instructions hold (>= 4 cycles each for wave64)
+    busy = lambda *names: {n: pk[n]["valu_issue_frac"] for n in names if n in pk and "valu_issue_frac" in pk[n]}  # noqa: E731
     dev_s = max(totals.get("seconds", 0.0), 1e-12)
     # ---- roofline of the light prep (rank 0's launches; HIP events on its stream) ----
     roof_prep = None
@@ -287,9 +308,9 @@ def main():
             "bound": "valu_fp64", "kernel": "k_prep_cull_lanes+k_prep_pk2", "achieved": round(achieved, 3),
             "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": tsrc,
-            "valu_busy": busy("k_prep_cull_lanes<false>",
+            "valu_issue_frac": busy("k_prep_cull_lanes<false>",
                               "k_prep_pk2<5, false, true, %s>" % ("true" if args.precision == "fp32" else "false")),
-            "valu_busy_source": pmc.get("source"),
+            "valu_issue_frac_source": pmc.get("source"),
             "hbm_frac_algorithmic": round(alg_gbs / HBM_PEAK_GBS, 5),
             "hbm_frac_measured": round(traffic / t_launch / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
             "avg_launch_ms": round(t_launch * 1e3, 3), "launches": launches, "flop_per_launch": flops / launches,
@@ -308,22 +329,27 @@ def main():
         kname = "k_extend_brdf" if args.mode == "brdf" else ("k_rays_persistent" if pers else "k_mis_rays")
         t_launch = tr_s / tr_n
         fl = (visits * FLOPS_NODE_VISIT + tests * FLOPS_TRI_TEST_FP64 * 2) / tr_n
-        by = (visits * BYTES_NODE_VISIT + tests * BYTES_TRI_TEST) / tr_n
+        by = (visits * BYTES_NODE_VISIT[kname] + tests * BYTES_TRI_TEST) / tr_n
         _, level, mem_peak = next(g for g in GATHER_PEAKS if accel <= g[0])
         v_frac, h_frac = fl / t_launch / 1e12 / FP32_VECTOR_PEAK_TFLOPS, by / t_launch / 1e9 / mem_peak
         valu_bound = v_frac >= h_frac
         pk_name = ("k_extend_brdf<false>" if args.mode == "brdf" else
                    "k_rays_persistent<false>" if pers else "k_mis_rays<false, false>")
         hbm_meas = pk.get(pk_name, {}).get("hbm_bytes_per_dispatch")
+        # the fetch model against the HBM peak is meaningful only when the structure lives in HBM; a
+        # cache-resident tree (Veach: 0.5 MB in L2; Cornell-1M: 150 MB in the Infinity Cache) is
+        # priced at its cache level above, and the HBM ratio of that model is not reported
+        hbm_model = round(by / t_launch / 1e9 / HBM_PEAK_GBS, 4) if level == "hbm" else None
         roof_trace = {
             "bound": "valu" if valu_bound else level, "kernel": kname,
             "achieved": round(fl / t_launch / 1e12, 3) if valu_bound else round(by / t_launch / 1e9, 1),
             "peak": FP32_VECTOR_PEAK_TFLOPS if valu_bound else mem_peak,
             "unit": "TFLOP/s (fp32-equivalent: fp64 op = 2)" if valu_bound else "GB/s (node + triangle fetch model)",
             "frac": round(max(v_frac, h_frac), 4), "valu_frac": round(v_frac, 4), "mem_model_frac": round(h_frac, 4),
-            "accel_bytes": accel, "hbm_model_frac": round(by / t_launch / 1e9 / HBM_PEAK_GBS, 4),
+            "accel_bytes": accel, "bytes_per_node_visit": BYTES_NODE_VISIT[kname], "structure_level": level,
+            "hbm_model_frac": hbm_model,
             "traffic": hbm_meas, "traffic_source": ("PMC profile, not this run: %s" % pmc.get("source")) if hbm_meas else None,
-            "valu_busy": busy(pk_name), "valu_busy_source": pmc.get("source"),
+            "valu_issue_frac": busy(pk_name), "valu_issue_frac_source": pmc.get("source"),
             "avg_launch_ms": round(t_launch * 1e3, 3), "launches": tr_n,
             "node_visits_per_ray": round(visits / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),
             "tri_tests_per_ray": round(tests / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),
@@ -346,14 +372,18 @@ def main():
     line = {
         "metric": SCENES[args.scene][0], "value": round(value, 4), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None,
+        "scaling": cfg["scaling"],
+        # the GPU over the compiled reference's own single thread on the same workload (the CPU
+        # baseline's reference-equivalent rate; BASELINE.md publishes only render times of another frame)
+        "vs_baseline": round(value / cpu["reference_equivalent_value"], 1) if cpu and cpu.get("reference_equivalent_value") else None,
         "dtype": "f64" if args.precision == "fp64" else "f64 (light-prep weights f32, MCPT_RENDER_PRECISION_FP32)",
         "data": SCENES[args.scene][1],
         "config": {"workload": "%s %s %dx%d" % ("veach-mis" if args.scene == "veach" else "cornell-1M", args.mode.upper(), W, H),
-                   "width": W, "height": H,
+                   "config": args.config, "width": W, "height": H,
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
                    "precision": args.precision, "root_cache": not args.no_root_cache,
-                   "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world},
+                   "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world,
+                   "job_spp_per_step": world * S},
         "roofline": roofline,
         "roofline_prep": roof_prep,
         "roofline_trace": roof_trace,

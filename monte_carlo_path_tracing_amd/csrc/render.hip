@@ -536,11 +536,13 @@ __device__ inline Hit grid_trace(const DScene& S, d3 ro, d3 rd, int exclude, boo
 // ============================================================================================
 // wavefront queue (SoA)
 // ============================================================================================
+// 3-vectors are component-major, x[cap] y[cap] z[cap] (node i's y at p[cap + i]): a wave's 64 nodes
+// read or write each component as one contiguous 512-B run (8 lines) instead of 24 lines per load
 struct Queue {
-    double* p;      // 3*cap  shading point
-    double* n;      // 3*cap  interpolated normal
-    double* wo;     // 3*cap
-    double* tp;     // 3*cap  path throughput
+    double* p;      // [3][cap]  shading point
+    double* n;      // [3][cap]  interpolated normal
+    double* wo;     // [3][cap]
+    double* tp;     // [3][cap]  path throughput
     int* f;         // cap
     int* pixel;     // cap
     int* sample;    // cap
@@ -697,10 +699,10 @@ __device__ inline void queue_push(const Params& P, bool push, const Entry& e, in
         return;
     }
     const size_t s = (size_t)slot;
-    q.p[3 * s] = e.p.x, q.p[3 * s + 1] = e.p.y, q.p[3 * s + 2] = e.p.z;
-    q.n[3 * s] = e.N.x, q.n[3 * s + 1] = e.N.y, q.n[3 * s + 2] = e.N.z;
-    q.wo[3 * s] = wo.x, q.wo[3 * s + 1] = wo.y, q.wo[3 * s + 2] = wo.z;
-    q.tp[3 * s] = tp.x, q.tp[3 * s + 1] = tp.y, q.tp[3 * s + 2] = tp.z;
+    q.p[s] = e.p.x, q.p[q.cap + s] = e.p.y, q.p[2 * (size_t)q.cap + s] = e.p.z;
+    q.n[s] = e.N.x, q.n[q.cap + s] = e.N.y, q.n[2 * (size_t)q.cap + s] = e.N.z;
+    q.wo[s] = wo.x, q.wo[q.cap + s] = wo.y, q.wo[2 * (size_t)q.cap + s] = wo.z;
+    q.tp[s] = tp.x, q.tp[q.cap + s] = tp.y, q.tp[2 * (size_t)q.cap + s] = tp.z;
     q.f[s] = f;
     q.pixel[s] = pixel;
     q.sample[s] = sample;
@@ -787,10 +789,10 @@ __global__ __launch_bounds__(256) void k_queue_move(Queue src, int sb, Queue dst
     const size_t s = (size_t)sb + k, d = (size_t)db + k;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-        dst.p[3 * d + c] = src.p[3 * s + c];
-        dst.n[3 * d + c] = src.n[3 * s + c];
-        dst.wo[3 * d + c] = src.wo[3 * s + c];
-        dst.tp[3 * d + c] = src.tp[3 * s + c];
+        dst.p[(size_t)c * dst.cap + d] = src.p[(size_t)c * src.cap + s];
+        dst.n[(size_t)c * dst.cap + d] = src.n[(size_t)c * src.cap + s];
+        dst.wo[(size_t)c * dst.cap + d] = src.wo[(size_t)c * src.cap + s];
+        dst.tp[(size_t)c * dst.cap + d] = src.tp[(size_t)c * src.cap + s];
     }
     dst.f[d] = src.f[s];
     dst.pixel[d] = src.pixel[s];
@@ -816,8 +818,8 @@ __global__ __launch_bounds__(256) void k_root_points(DScene S, CamFrame cam, con
     }
     const int slot = block_append(q.count, want);
     if (want && slot < q.cap) {
-        q.p[3 * slot] = p.x, q.p[3 * slot + 1] = p.y, q.p[3 * slot + 2] = p.z;
-        q.n[3 * slot] = N.x, q.n[3 * slot + 1] = N.y, q.n[3 * slot + 2] = N.z;
+        q.p[slot] = p.x, q.p[q.cap + slot] = p.y, q.p[2 * (size_t)q.cap + slot] = p.z;
+        q.n[slot] = N.x, q.n[q.cap + slot] = N.y, q.n[2 * (size_t)q.cap + slot] = N.z;
         q.pixel[slot] = px;
     }
 }
@@ -846,7 +848,7 @@ __device__ inline void wave_count2(unsigned long long* ca, unsigned a, unsigned 
     }
 }
 __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
-                                                   const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                                   const double* __restrict__ qn, int qs, const int* __restrict__ qpixel,
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                    const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                    int* __restrict__ pick_out, int* __restrict__ count_out,
@@ -855,8 +857,8 @@ __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int 
     const bool active = i < n;
     unsigned long long surv = 0, cand = 0, c1 = 0;
     if (active) {
-        const d3 x1 = mk3(qp[3 * i], qp[3 * i + 1], qp[3 * i + 2]);
-        const d3 nn = mk3(qn[3 * i], qn[3 * i + 1], qn[3 * i + 2]);
+        const d3 x1 = mk3(qp[i], qp[qs + i], qp[2 * (size_t)qs + i]);
+        const d3 nn = mk3(qn[i], qn[qs + i], qn[2 * (size_t)qs + i]);
         // the reference's literal chain (light_tri_stage: Mylight.cpp:335-413, six acos), so weights,
         // weights_sum (summed in index order below) and the pick are the reference's bit for bit
         auto eval = [&](int li, bool* ok) -> double {
@@ -1099,7 +1101,7 @@ constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
 constexpr int kPrepGrab = 4;     // nodes a wave takes per work-counter atomic
 
 __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
-                                              const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                              const double* __restrict__ qn, int qs, const int* __restrict__ qpixel,
                                               const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                               const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                               int* __restrict__ pick_out, int* __restrict__ count_out,
@@ -1125,8 +1127,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
         const int node = grab++;
         left--;
         if (node >= n) break;
-        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
-        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
+        const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
         const NodeF nf = node_f(x1, nn, S.light_bound);
         int qcnt = 0, nb = 0, survivors = 0, candidates = 0, culled1 = 0;
         double sacc = 0;  // flagged slivers' band terms (exact pick)
@@ -1622,13 +1624,13 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
 
 template <bool kCountC1>
 __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
-                                                         const double* __restrict__ qn, uint64_t* __restrict__ masks,
+                                                         const double* __restrict__ qn, int qs, uint64_t* __restrict__ masks,
                                                          int nchunks, unsigned long long* stats) {
     const int node = blockIdx.x * blockDim.x + threadIdx.x;
     const bool act = node < n;
     const int nd = act ? node : n - 1;
-    const d3 x1 = mk3(qp[3 * nd], qp[3 * nd + 1], qp[3 * nd + 2]);
-    const d3 nn = mk3(qn[3 * nd], qn[3 * nd + 1], qn[3 * nd + 2]);
+    const d3 x1 = mk3(qp[nd], qp[qs + nd], qp[2 * (size_t)qs + nd]);
+    const d3 nn = mk3(qn[nd], qn[qs + nd], qn[2 * (size_t)qs + nd]);
     const NodeF f = node_f(x1, nn, S.light_bound);
     const float cn = (float)(dot(nn, x1) + MCPT_EPS);
     CullLane cl;
@@ -1679,7 +1681,7 @@ __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S,
 constexpr int kMaskBatch = kMaskLine;  // candidate words per batch of scalar loads (k_prep_pk2): one line
 template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false, bool kF32 = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
-                                                  const double* __restrict__ qn, const int* __restrict__ qpixel,
+                                                  const double* __restrict__ qn, int qs, const int* __restrict__ qpixel,
                                                   const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                   const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                   int* __restrict__ pick_out, int* __restrict__ count_out,
@@ -1711,7 +1713,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         const int node = __builtin_amdgcn_readfirstlane(grab++);
         left--;
         if (node >= n) break;
-        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
+        const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
         auto u_of = [&]() {
             return u_override ? u_override[node]
                               : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
@@ -1746,7 +1748,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                 }
             }
         } else {
-        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
         const NodeF nf = node_f(x1, nn, S.light_bound);
         const float cn = (float)dot(nn, x1);
         const v2f nx2{nf.nx, nf.nx}, ny2{nf.ny, nf.ny}, nz2{nf.nz, nf.nz};
@@ -2046,7 +2048,7 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
 // almost every node; the node's candidate words are read only when it does not.  Nodes inside the band
 // are appended to the exact list (count in list[0], wave-aggregated).
 __global__ __launch_bounds__(256) void k_prep_band(DScene S, int n, const double* __restrict__ slack,
-                                                  const double* __restrict__ qp, const uint64_t* __restrict__ masks,
+                                                  const double* __restrict__ qp, int qs, const uint64_t* __restrict__ masks,
                                                   int nchunks, int* __restrict__ list) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool amb = false;
@@ -2056,7 +2058,7 @@ __global__ __launch_bounds__(256) void k_prep_band(DScene S, int n, const double
             if (!(sl > 0.0)) {
                 amb = true;
             } else {
-                const d3 x1 = mk3(qp[3 * i], qp[3 * i + 1], qp[3 * i + 2]);
+                const d3 x1 = mk3(qp[i], qp[qs + i], qp[2 * (size_t)qs + i]);
                 if (!(sl > band_base_upper(S, x1)))
                     amb = !(sl > band_base(S, x1, masks ? masks + (size_t)i * mask_stride(nchunks) : nullptr, nchunks));
             }
@@ -2079,7 +2081,7 @@ __global__ __launch_bounds__(256) void k_prep_band(DScene S, int n, const double
 constexpr int kExactBlock = 256;
 constexpr int kExactBlocks = 256;  // grid-stride; the list is short (~1e-3 of the prep nodes)
 __global__ __launch_bounds__(kExactBlock) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
-                                                         const double* __restrict__ qp, const double* __restrict__ qn,
+                                                         const double* __restrict__ qp, const double* __restrict__ qn, int qs,
                                                          const int* __restrict__ qpixel, const int* __restrict__ qsample,
                                                          const uint64_t* __restrict__ qnode,
                                                          const double* __restrict__ u_override, double* __restrict__ wsum_out,
@@ -2095,8 +2097,8 @@ __global__ __launch_bounds__(kExactBlock) void k_prep_exact(DScene S, uint64_t s
     if (gw == 0 && lane == 0 && stats && cnt) atomicAdd(stats + 10, (unsigned long long)cnt);
     for (int j = gw; j < cnt; j += waves) {
         const int node = list[kExactHead + j];
-        const d3 x1 = mk3(qp[3 * node], qp[3 * node + 1], qp[3 * node + 2]);
-        const d3 nn = mk3(qn[3 * node], qn[3 * node + 1], qn[3 * node + 2]);
+        const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
+        const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
         int ncand = 0;
         for (int c = 0; c < S.NL; c += 64) {  // cheap stages, candidates compacted in index order
             const int li = c + lane;
@@ -2322,10 +2324,10 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const d3 p = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
-    const d3 N = mk3(cur.n[3 * i], cur.n[3 * i + 1], cur.n[3 * i + 2]);
-    const d3 wo = mk3(cur.wo[3 * i], cur.wo[3 * i + 1], cur.wo[3 * i + 2]);
-    const d3 tp = mk3(cur.tp[3 * i], cur.tp[3 * i + 1], cur.tp[3 * i + 2]);
+    const d3 p = mk3(cur.p[i], cur.p[cur.cap + i], cur.p[2 * (size_t)cur.cap + i]);
+    const d3 N = mk3(cur.n[i], cur.n[cur.cap + i], cur.n[2 * (size_t)cur.cap + i]);
+    const d3 wo = mk3(cur.wo[i], cur.wo[cur.cap + i], cur.wo[2 * (size_t)cur.cap + i]);
+    const d3 tp = mk3(cur.tp[i], cur.tp[cur.cap + i], cur.tp[2 * (size_t)cur.cap + i]);
     const int f = cur.f[i];
     const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
     const float* m = S.mtl + 7 * S.tri_mat[f];
@@ -2368,10 +2370,10 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
         if (!(fabs(wsum) < MCPT_EPS)) flags |= 4;  // light pdf can only be nonzero with a light set
         w2 = kStale ? brdf_phong(N, wi, wo, kd, ks, sh) : hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh));
     }
-    A.d1[3 * i] = wl.x, A.d1[3 * i + 1] = wl.y, A.d1[3 * i + 2] = wl.z;
-    A.d2[3 * i] = wi.x, A.d2[3 * i + 1] = wi.y, A.d2[3 * i + 2] = wi.z;
-    A.w1[3 * i] = w1.x, A.w1[3 * i + 1] = w1.y, A.w1[3 * i + 2] = w1.z;
-    A.w2[3 * i] = w2.x, A.w2[3 * i + 1] = w2.y, A.w2[3 * i + 2] = w2.z;
+    A.d1[i] = wl.x, A.d1[A.cap + i] = wl.y, A.d1[2 * (size_t)A.cap + i] = wl.z;
+    A.d2[i] = wi.x, A.d2[A.cap + i] = wi.y, A.d2[2 * (size_t)A.cap + i] = wi.z;
+    A.w1[i] = w1.x, A.w1[A.cap + i] = w1.y, A.w1[2 * (size_t)A.cap + i] = w1.z;
+    A.w2[i] = w2.x, A.w2[A.cap + i] = w2.y, A.w2[2 * (size_t)A.cap + i] = w2.z;
     A.c2[2 * i] = pdf, A.c2[2 * i + 1] = dot(wi, N);
     if (kStale) A.s1[i] = s1;
     A.flags[i] = flags;
@@ -2402,8 +2404,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
     unsigned visits = 0, tests = 0;
     if (fl & (1 << set)) {
         const double* d = set == 0 ? A.d1 : A.d2;
-        const d3 ro = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
-        const d3 rd = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        const d3 ro = mk3(cur.p[i], cur.p[cur.cap + i], cur.p[2 * (size_t)cur.cap + i]);
+        const d3 rd = mk3(d[i], d[A.cap + i], d[2 * (size_t)A.cap + i]);
         const float4* leafv = set == 2 ? S.lleaf_v : S.leaf_v;  // uniform per block
         Hit h;
         if (kGrid)
@@ -2567,8 +2569,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                     best = Hit{-1, DBL_MAX, 0, 0};
                     if (A.flags[ii] & (1 << set)) {
                         const double* d = set == 0 ? A.d1 : A.d2;
-                        ro = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
-                        rd = mk3(d[3 * ii], d[3 * ii + 1], d[3 * ii + 2]);
+                        ro = mk3(cur.p[ii], cur.p[cur.cap + ii], cur.p[2 * (size_t)cur.cap + ii]);
+                        rd = mk3(d[ii], d[A.cap + ii], d[2 * (size_t)A.cap + ii]);
                         excl = cur.f[ii];
                         if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) {  // reference: UB (Myobj.cpp:463-468)
                             finish();
@@ -2695,14 +2697,14 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
     const size_t o1 = ii, o2 = (size_t)A.cap + ii, ol = 2 * (size_t)A.cap + ii;
     const bool c1 = active && (fl & 1) && A.hf[o1] >= 0;
     const bool c2 = active && (fl & 2) && A.hf[o2] >= 0;
-    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
-    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
+    const d3 p = mk3(cur.p[ii], cur.p[cur.cap + ii], cur.p[2 * (size_t)cur.cap + ii]);
+    const d3 N = mk3(cur.n[ii], cur.n[cur.cap + ii], cur.n[2 * (size_t)cur.cap + ii]);
     const int li = (c2 && (fl & 4) && A.hf[ol] >= 0) ? S.tri_light[A.hf[ol]] : -1;
     const double own[7] = {p.x, p.y, p.z, N.x, N.y, N.z, cur.wsum[ii]};
-    const d3 d1 = mk3(A.d1[3 * ii], A.d1[3 * ii + 1], A.d1[3 * ii + 2]);
-    const d3 d2 = mk3(A.d2[3 * ii], A.d2[3 * ii + 1], A.d2[3 * ii + 2]);
-    const d3 w1 = mk3(A.w1[3 * ii], A.w1[3 * ii + 1], A.w1[3 * ii + 2]);
-    const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
+    const d3 d1 = mk3(A.d1[ii], A.d1[A.cap + ii], A.d1[2 * (size_t)A.cap + ii]);
+    const d3 d2 = mk3(A.d2[ii], A.d2[A.cap + ii], A.d2[2 * (size_t)A.cap + ii]);
+    const d3 w1 = mk3(A.w1[ii], A.w1[A.cap + ii], A.w1[2 * (size_t)A.cap + ii]);
+    const d3 w2 = mk3(A.w2[ii], A.w2[A.cap + ii], A.w2[2 * (size_t)A.cap + ii]);
     const double pdf = A.c2[2 * ii], cosb = A.c2[2 * ii + 1];
     if (!kStale) {  // fresh light pdf (this node's own prep) and forward throughputs
         d3 tp2 = mk3(0, 0, 0);
@@ -2864,10 +2866,10 @@ __global__ __launch_bounds__(256, MCPT_LB_SHADE_GEN) void k_shade_gen(Params P, 
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const d3 p = mk3(cur.p[3 * i], cur.p[3 * i + 1], cur.p[3 * i + 2]);
-    const d3 N = mk3(cur.n[3 * i], cur.n[3 * i + 1], cur.n[3 * i + 2]);
-    const d3 wo = mk3(cur.wo[3 * i], cur.wo[3 * i + 1], cur.wo[3 * i + 2]);
-    const d3 tp = mk3(cur.tp[3 * i], cur.tp[3 * i + 1], cur.tp[3 * i + 2]);
+    const d3 p = mk3(cur.p[i], cur.p[cur.cap + i], cur.p[2 * (size_t)cur.cap + i]);
+    const d3 N = mk3(cur.n[i], cur.n[cur.cap + i], cur.n[2 * (size_t)cur.cap + i]);
+    const d3 wo = mk3(cur.wo[i], cur.wo[cur.cap + i], cur.wo[2 * (size_t)cur.cap + i]);
+    const d3 tp = mk3(cur.tp[i], cur.tp[cur.cap + i], cur.tp[2 * (size_t)cur.cap + i]);
     const int f = cur.f[i];
     const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
     const float* m = S.mtl + 7 * S.tri_mat[f];
@@ -2918,10 +2920,10 @@ __global__ __launch_bounds__(256, MCPT_LB_SHADE_GEN) void k_shade_gen(Params P, 
             w2 = mul(hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
         }
     }
-    A.d1[3 * i] = wl.x, A.d1[3 * i + 1] = wl.y, A.d1[3 * i + 2] = wl.z;
-    A.d2[3 * i] = wi.x, A.d2[3 * i + 1] = wi.y, A.d2[3 * i + 2] = wi.z;
-    A.w1[3 * i] = w1.x, A.w1[3 * i + 1] = w1.y, A.w1[3 * i + 2] = w1.z;
-    A.w2[3 * i] = w2.x, A.w2[3 * i + 1] = w2.y, A.w2[3 * i + 2] = w2.z;
+    A.d1[i] = wl.x, A.d1[A.cap + i] = wl.y, A.d1[2 * (size_t)A.cap + i] = wl.z;
+    A.d2[i] = wi.x, A.d2[A.cap + i] = wi.y, A.d2[2 * (size_t)A.cap + i] = wi.z;
+    A.w1[i] = w1.x, A.w1[A.cap + i] = w1.y, A.w1[2 * (size_t)A.cap + i] = w1.z;
+    A.w2[i] = w2.x, A.w2[A.cap + i] = w2.y, A.w2[2 * (size_t)A.cap + i] = w2.z;
     A.hf[2 * (size_t)A.cap + i] = pick >= 0 ? S.light_facet[pick] : -1;
     A.flags[i] = flags;
 }
@@ -2935,14 +2937,14 @@ __global__ __launch_bounds__(256) void k_shade_combine(Params P, Queue cur, int 
     const size_t o1 = ii, o2 = (size_t)A.cap + ii;
     if (active && (fl & 1) && A.hf[o1] >= 0 && A.hf[o1] == A.hf[2 * (size_t)A.cap + ii]) {
         double* px = P.fb + 3 * (size_t)cur.pixel[ii];
-        unsafeAtomicAdd(px + 0, A.w1[3 * ii]);
-        unsafeAtomicAdd(px + 1, A.w1[3 * ii + 1]);
-        unsafeAtomicAdd(px + 2, A.w1[3 * ii + 2]);
+        unsafeAtomicAdd(px + 0, A.w1[ii]);
+        unsafeAtomicAdd(px + 1, A.w1[A.cap + ii]);
+        unsafeAtomicAdd(px + 2, A.w1[2 * (size_t)A.cap + ii]);
     }
     const int h2 = A.hf[o2];
     const bool c = active && (fl & 2) && h2 >= 0 && S.tri_light[h2] < 0;
-    const d3 d2 = mk3(A.d2[3 * ii], A.d2[3 * ii + 1], A.d2[3 * ii + 2]);
-    const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
+    const d3 d2 = mk3(A.d2[ii], A.d2[A.cap + ii], A.d2[2 * (size_t)A.cap + ii]);
+    const d3 w2 = mk3(A.w2[ii], A.w2[A.cap + ii], A.w2[2 * (size_t)A.cap + ii]);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
     block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u);
@@ -2953,9 +2955,9 @@ __global__ __launch_bounds__(256) void k_brdf_gen(Params P, Queue cur, int n, Au
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const d3 N = mk3(cur.n[3 * i], cur.n[3 * i + 1], cur.n[3 * i + 2]);
-    const d3 wo = mk3(cur.wo[3 * i], cur.wo[3 * i + 1], cur.wo[3 * i + 2]);
-    const d3 tp = mk3(cur.tp[3 * i], cur.tp[3 * i + 1], cur.tp[3 * i + 2]);
+    const d3 N = mk3(cur.n[i], cur.n[cur.cap + i], cur.n[2 * (size_t)cur.cap + i]);
+    const d3 wo = mk3(cur.wo[i], cur.wo[cur.cap + i], cur.wo[2 * (size_t)cur.cap + i]);
+    const d3 tp = mk3(cur.tp[i], cur.tp[cur.cap + i], cur.tp[2 * (size_t)cur.cap + i]);
     const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
     const float* m = S.mtl + 7 * S.tri_mat[cur.f[i]];
     const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
@@ -2968,8 +2970,8 @@ __global__ __launch_bounds__(256) void k_brdf_gen(Params P, Queue cur, int n, Au
         flags = 2;
         w2 = mul(hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
     }
-    A.d2[3 * i] = wi.x, A.d2[3 * i + 1] = wi.y, A.d2[3 * i + 2] = wi.z;
-    A.w2[3 * i] = w2.x, A.w2[3 * i + 1] = w2.y, A.w2[3 * i + 2] = w2.z;
+    A.d2[i] = wi.x, A.d2[A.cap + i] = wi.y, A.d2[2 * (size_t)A.cap + i] = wi.z;
+    A.w2[i] = w2.x, A.w2[A.cap + i] = w2.y, A.w2[2 * (size_t)A.cap + i] = w2.z;
     A.flags[i] = flags;
 }
 
@@ -2981,8 +2983,8 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
     const size_t o2 = (size_t)A.cap + ii;
     const int h2 = A.hf[o2];
     const bool c = active && (fl & 2) && h2 >= 0;
-    const d3 d2 = mk3(A.d2[3 * ii], A.d2[3 * ii + 1], A.d2[3 * ii + 2]);
-    const d3 w2 = mk3(A.w2[3 * ii], A.w2[3 * ii + 1], A.w2[3 * ii + 2]);
+    const d3 d2 = mk3(A.d2[ii], A.d2[A.cap + ii], A.d2[2 * (size_t)A.cap + ii]);
+    const d3 w2 = mk3(A.w2[ii], A.w2[A.cap + ii], A.w2[2 * (size_t)A.cap + ii]);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
     block_count(P.stats + 2, (active && (fl & 2)) ? 1u : 0u);
@@ -3014,10 +3016,10 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
     const int ii = active ? i : 0;
-    const d3 p = mk3(cur.p[3 * ii], cur.p[3 * ii + 1], cur.p[3 * ii + 2]);
-    const d3 N = mk3(cur.n[3 * ii], cur.n[3 * ii + 1], cur.n[3 * ii + 2]);
-    const d3 wo = mk3(cur.wo[3 * ii], cur.wo[3 * ii + 1], cur.wo[3 * ii + 2]);
-    const d3 tp = mk3(cur.tp[3 * ii], cur.tp[3 * ii + 1], cur.tp[3 * ii + 2]);
+    const d3 p = mk3(cur.p[ii], cur.p[cur.cap + ii], cur.p[2 * (size_t)cur.cap + ii]);
+    const d3 N = mk3(cur.n[ii], cur.n[cur.cap + ii], cur.n[2 * (size_t)cur.cap + ii]);
+    const d3 wo = mk3(cur.wo[ii], cur.wo[cur.cap + ii], cur.wo[2 * (size_t)cur.cap + ii]);
+    const d3 tp = mk3(cur.tp[ii], cur.tp[cur.cap + ii], cur.tp[2 * (size_t)cur.cap + ii]);
     const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
     const uint64_t node = cur.node[ii];
     bool c = false;
@@ -3107,12 +3109,21 @@ struct mcpt_scene {
     Grid grid;             // Myobj::cal_scene_boundingbox(eye) + meshing(n0) (mcpt_scene_meshing)
     int grid_version = 0;  // bumped by every rebuild; devices re-upload on mismatch
     std::vector<std::unique_ptr<DeviceState>> devs;
+    std::mutex devs_mu;             // devs (render_multi creates device states on its worker threads)
     std::vector<int> comm_devices;  // distinct devices of the cached ncclCommInitAll communicators
     std::vector<void*> comms;
     std::mutex mu;
 };
 
 namespace {
+
+// n 3-vectors [n][3] -> component-major [3][n]
+std::vector<double> soa3(const double* v, int n) {
+    std::vector<double> o(3 * (size_t)n);
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++) o[(size_t)k * n + i] = v[3 * (size_t)i + k];
+    return o;
+}
 
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return MCPT_OK;
@@ -3197,14 +3208,20 @@ std::vector<float4> leaf_vertices(const HostScene& s, const Bvh& b) {
 
 int prep_chunks(int NL);
 
+// the device's scene state, created (scene, light tables and BVHs uploaded) on first use.  Thread-safe
+// for distinct devices: render_multi's workers create theirs concurrently (the lookup and the insertion
+// hold devs_mu, the uploads do not)
 int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if (device < 0) HIP_OK(hipGetDevice(&device));
-    for (auto& d : sc->devs)
-        if (d->device == device) {
-            HIP_OK(hipSetDevice(device));
-            *out = d.get();
-            return MCPT_OK;
-        }
+    {
+        std::lock_guard<std::mutex> lk(sc->devs_mu);
+        for (auto& d : sc->devs)
+            if (d->device == device) {
+                HIP_OK(hipSetDevice(device));
+                *out = d.get();
+                return MCPT_OK;
+            }
+    }
     HIP_OK(hipSetDevice(device));
     auto D = std::make_unique<DeviceState>();
     D->device = device;
@@ -3388,6 +3405,7 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     HIP_OK(hipEventCreate(&D->evr0));
     HIP_OK(hipEventCreate(&D->evr1));
     *out = D.get();
+    std::lock_guard<std::mutex> lk(sc->devs_mu);
     sc->devs.push_back(std::move(D));
     return MCPT_OK;
 }
@@ -3532,7 +3550,7 @@ constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 #define MCPT_PK2_F32_WAVES 5
 #endif
 constexpr int kPk2F32Waves = MCPT_PK2_F32_WAVES;
-hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn,
+hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn, int qs,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
                        const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr, bool count_c1 = true,
@@ -3543,7 +3561,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? 17 : 8) : 0;  // A/B: tools/prep_variants.py
     if (variant != 0 && variant != 8 && variant != 9 && variant != 17) return hipErrorInvalidValue;
     if (variant == 9) {
-        hipLaunchKernelGGL(k_prep_lane, dim3((n + 255) / 256), dim3(256), 0, st, d, seed, n, qp, qn, qpixel, qsample, qnode,
+        hipLaunchKernelGGL(k_prep_lane, dim3((n + 255) / 256), dim3(256), 0, st, d, seed, n, qp, qn, qs, qpixel, qsample, qnode,
                            u, wsum, pick, count, stats);
         return hipGetLastError();
     }
@@ -3555,26 +3573,26 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     if (variant == 0) {
-        hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qpixel,
+        hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qs, qpixel,
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, work, cache.slack, cache.exact_off,
                            cache.exact_counts);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
         if (count_c1 || !stats)
             hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
-                               n, qp, qn, masks, nchunks, stats);
+                               n, qp, qn, qs, masks, nchunks, stats);
         else
             hipLaunchKernelGGL(k_prep_cull_lanes<false>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
-                               n, qp, qn, masks, nchunks, stats);
+                               n, qp, qn, qs, masks, nchunks, stats);
         // fp32: MCPT_RENDER_PRECISION_FP32's packed-fp32 full stage (light_weight_f32x2)
         auto kern = cache.build ? (fp32 ? k_prep_pk2<kPk2F32Waves, true, true, true> : k_prep_pk2<5, true, true, false>)
                                 : (fp32 ? k_prep_pk2<kPk2F32Waves, false, true, true> : k_prep_pk2<5, false, true, false>);
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel, qsample, qnode, u, wsum,
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qs, qpixel, qsample, qnode, u, wsum,
                            pick, count, stats, nchunks, wb, work, cache, masks);
     } else if (cache.build) {
-        hipLaunchKernelGGL((k_prep_pk2<5, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+        hipLaunchKernelGGL((k_prep_pk2<5, true>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qs, qpixel,
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
     } else {
-        hipLaunchKernelGGL((k_prep_pk2<5, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qpixel,
+        hipLaunchKernelGGL((k_prep_pk2<5, false>), dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qs, qpixel,
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, wb, work, cache);
     }
     return hipGetLastError();
@@ -3619,6 +3637,26 @@ int use_grid(mcpt_scene* sc, DeviceState& D, const double eye[3], int n0) {
     return MCPT_OK;
 }
 
+// every option a render checks before it starts (spp, sample range, mode, acceleration, flags) --
+// called first by every path, and by every rank of a communicator before any collective, so that a
+// bad option fails on all ranks alike instead of leaving some of them in the reduce
+int validate_render(const mcpt_render_opts* o) {
+    const int s0 = (o->sample_begin == 0 && o->sample_end == 0) ? 0 : o->sample_begin;
+    const int s1 = (o->sample_begin == 0 && o->sample_end == 0) ? o->spp : o->sample_end;
+    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp ||
+        (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF && o->mode != MCPT_MODE_SHADE && o->mode != MCPT_MODE_SHADE_AREA) ||
+        (o->accel != MCPT_ACCEL_BVH && o->accel != MCPT_ACCEL_GRID)) {
+        set_error("invalid render options (spp %d, range [%d,%d), mode %d, accel %d)", o->spp, s0, s1, o->mode, o->accel);
+        return MCPT_E_INVALID;
+    }
+    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
+                     MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL)) {
+        set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
+        return MCPT_E_INVALID;
+    }
+    return MCPT_OK;
+}
+
 // the wavefront render into a device framebuffer already resident on D's device
 int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o,
                      double* dfb, mcpt_stats* stats) {
@@ -3626,10 +3664,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int W = cam->width, H = cam->height, npx = W * H;
     const int s0 = (o->sample_begin == 0 && o->sample_end == 0) ? 0 : o->sample_begin;
     const int s1 = (o->sample_begin == 0 && o->sample_end == 0) ? o->spp : o->sample_end;
-    if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp || (o->mode != MCPT_MODE_MIS && o->mode != MCPT_MODE_BRDF && o->mode != MCPT_MODE_SHADE && o->mode != MCPT_MODE_SHADE_AREA) ||
-        (o->accel != MCPT_ACCEL_BVH && o->accel != MCPT_ACCEL_GRID)) {
-        set_error("invalid render options (spp %d, range [%d,%d), mode %d, accel %d)", o->spp, s0, s1, o->mode, o->accel);
-        return MCPT_E_INVALID;
+    {
+        const int rv = validate_render(o);
+        if (rv) return rv;
     }
     // MCPT_ACCEL_GRID: the reference's uniform grid over the scene and this camera's eye, n0 =
     // 100000 (main.cpp:501-504), built here unless the scene already holds that grid
@@ -3711,11 +3748,6 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         set_error("too many light triangles for the LDS chunk table (%d)", D.d.NL);
         return MCPT_E_SCENE;
     }
-    if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
-                     MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL)) {
-        set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
-        return MCPT_E_INVALID;
-    }
     const bool count_c1 = !(o->flags & MCPT_RENDER_NO_BACKFACE_STATS);
     const bool fp32 = (o->flags & MCPT_RENDER_PRECISION_FP32) != 0;
     double prep_ms = 0, trace_ms = 0, cache_ms = 0;
@@ -3780,7 +3812,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (nr > 0) {
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
-            HIP_OK(launch_prep(masks ? 17 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.pixel, nullptr, nullptr, nullptr, nullptr,
+            HIP_OK(launch_prep(masks ? 17 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.cap, qb.pixel, nullptr, nullptr, nullptr, nullptr,
                                nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks, count_c1, fp32));
             HIP_OK(hipEventRecord(D.evp1, st));
             HIP_OK(hipEventSynchronize(D.evp1));
@@ -3906,7 +3938,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 const int nc = (int)n_children, nr = ni - nc;
                 if (nc > 0) {
                     HIP_OK(hipEventRecord(D.evp0, st));
-                    HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
+                    HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                        cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
                                        count_c1, fp32));
                     HIP_OK(hipEventRecord(D.evp1, st));
@@ -3924,7 +3956,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 }
             } else {
                 HIP_OK(hipEventRecord(D.evp0, st));
-                HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr,
+                HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                    cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
                                    count_c1, fp32));
                 HIP_OK(hipEventRecord(D.evp1, st));
@@ -3932,10 +3964,10 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             }
             prep_launches += timed;
             if (exact_pick) {  // the band's nodes: the reference's literal prep and pick
-                hipLaunchKernelGGL(k_prep_band, dim3((ni + 255) / 256), dim3(256), 0, st, D.d, ni, slack, cur->p, masks,
+                hipLaunchKernelGGL(k_prep_band, dim3((ni + 255) / 256), dim3(256), 0, st, D.d, ni, slack, cur->p, cur->cap, masks,
                                    nchunks, exact_list);
                 hipLaunchKernelGGL(k_prep_exact, dim3(kExactBlocks), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
-                                   cur->p, cur->n, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
+                                   cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
                                    nullptr, P.stats, exact_scr);
                 HIP_OK(hipGetLastError());
             }
@@ -4190,30 +4222,16 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
     }
     const int nu = (int)uniq.size();
     const size_t nfb = 3ull * cam->width * cam->height;
-    std::vector<DeviceState*> Ds(nu);
-    std::vector<double*> fbs(nu);
     int rc;
-    for (int u = 0; u < nu; u++) {  // device states are created on this thread (sc->devs is not thread-safe)
-        if ((rc = get_device_state(sc, uniq[u], &Ds[u]))) return rc;
-        HIP_OK(hipDeviceSynchronize());  // the caller's buffers may still be written by other streams
-        if (u == 0 && !host_out) {
-            fbs[0] = root_out;
-            continue;
-        }
-        if ((rc = ensure(Ds[u]->fb, nfb * sizeof(double)))) return rc;
-        fbs[u] = (double*)Ds[u]->fb.p;
-        if (u == 0)
-            HIP_OK(hipMemcpyAsync(fbs[0], host_out, nfb * sizeof(double), hipMemcpyHostToDevice, Ds[0]->stream));
-        else
-            HIP_OK(hipMemsetAsync(fbs[u], 0, nfb * sizeof(double), Ds[u]->stream));
-        HIP_OK(hipStreamSynchronize(Ds[u]->stream));
+    if ((rc = validate_render(o))) return rc;
+    // the reference grid (MCPT_ACCEL_GRID) is built here, before the workers, which then only read it
+    if (o->accel == MCPT_ACCEL_GRID) {
+        const CamFrame cf = cam_setup(*cam);
+        const double eye[3] = {cf.eye.x, cf.eye.y, cf.eye.z};
+        if ((rc = ensure_host_grid(sc, eye, 100000))) return rc;
     }
-    if (sc->comm_devices != uniq) {  // RCCL communicators over exactly these devices (cached)
-        comm_all_destroy(sc->comms);
-        sc->comm_devices.clear();
-        if ((rc = comm_all_init(uniq, sc->comms))) return rc;
-        sc->comm_devices = uniq;
-    }
+    std::vector<DeviceState*> Ds(nu, nullptr);
+    std::vector<double*> fbs(nu, nullptr);
     int s0, s1;
     job_range(o, &s0, &s1);
     MultiProgress mp;
@@ -4225,11 +4243,32 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
     std::vector<int> urc(nu, MCPT_OK);
     std::vector<std::string> uerr(nu);
     const auto t0 = std::chrono::steady_clock::now();
+    // one worker thread per distinct device: its scene state (the uploads of a 1M-triangle scene run
+    // on all devices at once, not one after another), its framebuffer, then its shards in order
     auto worker = [&](int u) {
-        if (hipSetDevice(uniq[u]) != hipSuccess) {
-            urc[u] = MCPT_E_DEVICE;
-            uerr[u] = "hipSetDevice failed";
-            return;
+        auto fail = [&](int r) {
+            urc[u] = r;
+            uerr[u] = mcpt_last_error();
+            mp.cancel.store(true);
+        };
+        int r;
+        if ((r = get_device_state(sc, uniq[u], &Ds[u]))) return fail(r);
+        DeviceState& D = *Ds[u];
+        if (hipDeviceSynchronize() != hipSuccess) {  // the caller's buffers may still be written by other streams
+            set_error("hipDeviceSynchronize failed");
+            return fail(MCPT_E_DEVICE);
+        }
+        if (u == 0 && !host_out) {
+            fbs[0] = root_out;
+        } else {
+            if ((r = ensure(D.fb, nfb * sizeof(double)))) return fail(r);
+            fbs[u] = (double*)D.fb.p;
+            const hipError_t e = u == 0 ? hipMemcpyAsync(fbs[0], host_out, nfb * sizeof(double), hipMemcpyHostToDevice, D.stream)
+                                        : hipMemsetAsync(fbs[u], 0, nfb * sizeof(double), D.stream);
+            if (e != hipSuccess || hipStreamSynchronize(D.stream) != hipSuccess) {
+                set_error("framebuffer setup on device %d failed", uniq[u]);
+                return fail(MCPT_E_DEVICE);
+            }
         }
         for (int k = 0; k < nshards; k++) {
             if (shard_dev[k] != u) continue;
@@ -4245,24 +4284,35 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
             sp[k] = ShardProgress{&mp, k};
             ok.progress = multi_progress_cb;
             ok.progress_user = &sp[k];
-            const int r = render_on_device(sc, *Ds[u], cam, &ok, fbs[u], &sst[k]);
-            if (r) {
-                urc[u] = r;
-                uerr[u] = mcpt_last_error();
-                mp.cancel.store(true);
-                return;
-            }
+            if ((r = render_on_device(sc, D, cam, &ok, fbs[u], &sst[k]))) return fail(r);
         }
     };
     std::vector<std::thread> th;
-    for (int u = 1; u < nu; u++) th.emplace_back(worker, u);
-    worker(0);
+    for (int u = 0; u < nu; u++) th.emplace_back(worker, u);
+    int crc = MCPT_OK;  // meanwhile: the RCCL communicators over exactly these devices (cached)
+    std::string cerr;
+    if (sc->comm_devices != uniq) {
+        comm_all_destroy(sc->comms);
+        sc->comm_devices.clear();
+        if ((crc = comm_all_init(uniq, sc->comms)))
+            cerr = mcpt_last_error();
+        else
+            sc->comm_devices = uniq;
+    }
     for (auto& t : th) t.join();
+    // report the first real failure: a shard stopped by another's failure reports MCPT_E_CANCELLED,
+    // which is the answer only when the user's progress callback asked for it
+    int fu = -1;
     for (int u = 0; u < nu; u++)
-        if (urc[u]) {
-            set_error("device %d: %s", uniq[u], uerr[u].c_str());
-            return urc[u];
-        }
+        if (urc[u] && (fu < 0 || (urc[fu] == MCPT_E_CANCELLED && urc[u] != MCPT_E_CANCELLED))) fu = u;
+    if (fu >= 0) {
+        set_error("device %d: %s", uniq[fu], uerr[fu].c_str());
+        return urc[fu];
+    }
+    if (crc) {
+        set_error("%s", cerr.c_str());
+        return crc;
+    }
     const auto t1 = std::chrono::steady_clock::now();
     std::vector<hipStream_t> streams(nu);
     for (int u = 0; u < nu; u++) streams[u] = Ds[u]->stream;
@@ -4288,43 +4338,70 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
     return MCPT_OK;
 }
 
-// One process per device (mcpt_render_opts.comm): this rank's shard of the job's sample range, then
-// ncclReduce(sum) to rank 0.  Rank 0 accumulates straight into its buffer `out` (the reduce is in
-// place there); other ranks render into a zeroed library buffer, so that only this call's samples
-// are summed and their `out` is left unchanged.
+// adds src into dst (n doubles): rank 0's share of the reduced job onto the caller's buffer
+__global__ void k_add_fb(double* __restrict__ dst, const double* __restrict__ src, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) dst[i] += src[i];
+}
+
+// One process per device (mcpt_render_opts.comm): this rank's shard of the job's sample range, then ONE
+// ncclReduce(sum) to rank 0.  Every rank renders into a zeroed library buffer of W*H*3 + 1 doubles whose
+// last slot carries the rank's status (0 ok, 1 failed), so the one reduce also tells rank 0 whether any
+// rank failed; rank 0 then adds the reduced frame to its `out` (or leaves it unchanged and fails).
+// Failures never skip the collective: options are validated identically on every rank before it
+// (validate_render), and a rank whose render fails later (out of memory, spill cap, a cancel from its
+// own progress callback -- cancelling is per rank) zeroes its buffer, sets its status and still joins
+// the reduce, then returns its error.  Other ranks' buffers (`out`) are left unchanged.
 int render_rank(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o, double* out,
                 mcpt_stats* stats) {
     int nranks, rank, device;
     int rc;
     if ((rc = comm_rank_info(o->comm, &nranks, &rank, &device))) return rc;
-    double* fb = out;
-    if (rank != 0) {
-        const size_t bytes = 3ull * cam->width * cam->height * sizeof(double);
-        if ((rc = ensure(D.rank_fb, bytes))) return rc;
-        fb = (double*)D.rank_fb.p;
-        HIP_OK(hipMemsetAsync(fb, 0, bytes, D.stream));
-    }
+    if ((rc = validate_render(o))) return rc;  // same outcome on every rank: nobody enters the reduce
+    const size_t nfb = 3ull * cam->width * cam->height;
+    if ((rc = ensure(D.rank_fb, (nfb + 1) * sizeof(double)))) return rc;
+    double* fb = (double*)D.rank_fb.p;
+    HIP_OK(hipMemsetAsync(fb, 0, (nfb + 1) * sizeof(double), D.stream));
     int s0, s1, a, b;
     job_range(o, &s0, &s1);
     shard_range(s0, s1, rank, nranks, &a, &b);
     mcpt_stats st{};
+    int local = MCPT_OK;
+    std::string lerr;
     if (a < b) {
         mcpt_render_opts ok = *o;
         ok.sample_begin = a;
         ok.sample_end = b;
         ok.comm = nullptr;
         ok.device = device;
-        if ((rc = render_on_device(sc, D, cam, &ok, fb, &st))) return rc;
-    } else {  // an empty shard still validates its options and joins the reduce
-        if (o->spp <= 0 || s0 < 0 || s1 < s0 || s1 > o->spp) {
-            set_error("invalid render options (spp %d, range [%d,%d))", o->spp, s0, s1);
-            return MCPT_E_INVALID;
+        local = render_on_device(sc, D, cam, &ok, fb, &st);
+        if (local) {  // join the reduce anyway, with a zero frame and the failure flag
+            lerr = mcpt_last_error();
+            (void)hipGetLastError();
+            static const double one = 1.0;
+            HIP_OK(hipMemsetAsync(fb, 0, nfb * sizeof(double), D.stream));
+            HIP_OK(hipMemcpyAsync(fb + nfb, &one, sizeof(double), hipMemcpyHostToDevice, D.stream));
         }
     }
     HIP_OK(hipEventRecord(D.ev0, D.stream));
-    if ((rc = comm_rank_reduce_sum(o->comm, fb, 3ull * cam->width * cam->height, D.stream))) return rc;
+    if ((rc = comm_rank_reduce_sum(o->comm, fb, nfb + 1, D.stream))) return rc;
     HIP_OK(hipEventRecord(D.ev1, D.stream));
+    double failed = 0;
+    if (rank == 0) HIP_OK(hipMemcpyAsync(&failed, fb + nfb, sizeof(double), hipMemcpyDeviceToHost, D.stream));
     HIP_OK(hipEventSynchronize(D.ev1));
+    HIP_OK(hipStreamSynchronize(D.stream));
+    if (local) {
+        set_error("rank %d: %s", rank, lerr.c_str());
+        return local;
+    }
+    if (failed > 0) {
+        set_error("%d of %d ranks failed their shard; the frame is not added", (int)failed, nranks);
+        return MCPT_E_DEVICE;
+    }
+    if (rank == 0) {
+        hipLaunchKernelGGL(k_add_fb, dim3(1024), dim3(256), 0, D.stream, out, (const double*)fb, nfb);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipStreamSynchronize(D.stream));
+    }
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, D.ev0, D.ev1));
     if (stats) {
@@ -4369,8 +4446,11 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
         HIP_OK(hipMalloc(&dsl, 8ull * n));
         HIP_OK(hipMemset(dl, 0, 4));
     }
-    HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
+    {  // the kernels read node coordinates component-major (x[n], y[n], z[n], like the wavefront queue)
+        const std::vector<double> px = soa3(x1, n), pn = soa3(nrm, n);
+        HIP_OK(hipMemcpy(dp, px.data(), 24ull * n, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(dn, pn.data(), 24ull * n, hipMemcpyHostToDevice));
+    }
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
     if ((rc = ensure(D->work, 256))) return rc;
     if (all_exact) {
@@ -4382,16 +4462,16 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
         PrepCache cx{};
         cx.slack = (double*)dsl;
         cx.exact_counts = 1;
-        HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+        HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream,
                            cx, (uint64_t*)dm));
         if (exact)
             hipLaunchKernelGGL(k_prep_band, dim3((n + 255) / 256), dim3(256), 0, D->stream, D->d, n, (const double*)dsl,
-                               (const double*)dp, (const uint64_t*)dm, prep_chunks(D->d.NL), (int*)dl);
+                               (const double*)dp, n, (const uint64_t*)dm, prep_chunks(D->d.NL), (int*)dl);
     }
     if (exact)
         hipLaunchKernelGGL(k_prep_exact, dim3(kExactBlocks), dim3(kExactBlock), 0, D->stream, D->d, (uint64_t)0,
-                           (const int*)dl, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+                           (const int*)dl, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (double*)ds);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
@@ -4773,16 +4853,19 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     HIP_OK(hipMalloc(&du, 8ull * n));
     HIP_OK(hipMalloc(&dw, 8ull * n));
     HIP_OK(hipMalloc(&dk, 4ull * n));
-    HIP_OK(hipMemcpy(dp, x1, 24ull * n, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(dn, nrm, 24ull * n, hipMemcpyHostToDevice));
+    {  // the kernels read node coordinates component-major (x[n], y[n], z[n], like the wavefront queue)
+        const std::vector<double> px = soa3(x1, n), pn = soa3(nrm, n);
+        HIP_OK(hipMemcpy(dp, px.data(), 24ull * n, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(dn, pn.data(), 24ull * n, hipMemcpyHostToDevice));
+    }
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
     if ((rc = ensure(D->work, 256))) return rc;
-    HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+    HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                        (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream,
                        PrepCache{}, (uint64_t*)dm));
     HIP_OK(hipEventRecord(D->ev0, D->stream));
     for (int it = 0; it < iters; it++)
-        HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, nullptr, nullptr, nullptr,
+        HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream,
                        PrepCache{}, (uint64_t*)dm));
     HIP_OK(hipEventRecord(D->ev1, D->stream));

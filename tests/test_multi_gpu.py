@@ -166,3 +166,49 @@ def test_c4_frame_1600x1200_vs_oracle_subset(scene):
     l2, mx = rel_l2(g, c), max_px_rel(g, c)
     print("C4 1600x1200x%d MIS subset: rel L2 %.3e, max per-pixel %.3e" % (spp, l2, mx))
     assert l2 <= 1e-3 and mx <= 1e-3
+
+
+def test_comm_failures_join_the_reduce_and_leave_the_comm_usable(scene, single):
+    """A rank's failure never skips the collective (render_rank): options are validated on every rank
+    before the reduce (an unknown flag fails alike everywhere), and a shard that fails later (here: its own
+    progress callback cancels) still joins the reduce with a zero frame and the failure flag, so rank 0
+    reports the failure instead of the peers hanging.  Multi-rank RCCL on distinct GPUs is the driver's
+    8-GPU run; RCCL refuses two ranks on one device, so these run on a 1-rank communicator."""
+    uid = mcpt.Comm.unique_id()
+    comm = mcpt.Comm(1, 0, uid, device=0)
+    try:
+        cam = mcpt.Camera.reference(80, 60)
+        with pytest.raises(mcpt.MCPTError, match="flags"):
+            mcpt.render(scene, cam, 8, mode="mis", seed=SEED, comm=comm, flags=1 << 12)
+        out = np.zeros((60, 80, 3))
+        with pytest.raises(mcpt.MCPTError, match="cancelled"):
+            mcpt.render(scene, cam, 8, mode="mis", seed=SEED, comm=comm, out=out, samples_per_launch=1,
+                        progress=lambda d, t: True)
+        assert not out.any()  # a failed job adds nothing to rank 0's buffer
+        img, _ = mcpt.render(scene, cam, 8, mode="mis", seed=SEED, comm=comm)
+        assert rel_l2(img, single[0]) <= 1e-12  # the communicator still works
+    finally:
+        comm.close()
+
+
+def test_device_list_with_reference_grid(scene):
+    """accel="grid" over a device list: the grid is built once on the calling thread before the device
+    workers start (they only read it), and the frame equals the single-device grid render"""
+    cam = mcpt.Camera.reference(40, 30)
+    a, _ = mcpt.render(scene, cam, 4, mode="mis", seed=SEED, accel="grid", device=0)
+    b, st = mcpt.render(scene, cam, 4, mode="mis", seed=SEED, accel="grid", devices=[0, 0])
+    assert rel_l2(b, a) <= 1e-12 and st.camera_samples == 40 * 30 * 4
+
+
+def test_c4_split_512spp_per_shard_reports_cache_build(scene):
+    """BASELINE C4's split on the device-list path: a 1600x1200 job split into 512-spp shards (two on
+    this one-GPU box; 8 x 512 = 4096 spp on the driver's node).  Each shard builds its own root-point
+    cache over the 1.92 M pixels; the time it takes is reported (mcpt_stats.cache_build_seconds)."""
+    W, H = 1600, 1200
+    cam = mcpt.Camera.reference(W, H)
+    img, st = mcpt.render(scene, cam, 1024, mode="mis", seed=SEED, devices=[0, 0])
+    assert st.camera_samples == W * H * 1024 and np.isfinite(img).all() and img.mean() > 0
+    assert st.prep_cache_points >= 2 * 0.9 * W * H  # both shards built the cache
+    print("C4 split 2 x 512 spp at 1600x1200: %.2f Msamples/s (wall, incl. reduce); root-point cache build "
+          "%.1f ms per shard of %.0f ms device time per shard" % (
+              st.camera_samples / st.seconds / 1e6, 1e3 * st.cache_build_seconds / 2, 1e3 * st.seconds / 2))

@@ -52,17 +52,20 @@ def main():
     # replay of the timed steps (the cull statistic pass, MIS/shade) -- same work per step
     nodes = tot["prep_full_nodes"] * (2 * a.steps + a.warmup) / a.steps
     kernels = [k for k in fetch if k.startswith("k_prep_cull_lanes") or k.startswith("k_prep_pk2")]
-    fb = sum(2 * fetch[k] for k in kernels)
+    # FETCH_SIZE x2 only for 16-B-per-lane loads (MI355X_MICROARCH.md): k_prep_pk2's light records are
+    # buffer_load_dwordx4; k_prep_cull_lanes reads its table with scalar loads (width uncalibrated, x1)
+    mult = {k: (2 if k.startswith("k_prep_pk2") else 1) for k in kernels}
+    fb = sum(mult[k] * fetch[k] for k in kernels)
     wb = sum(write.get(k, 0.0) for k in kernels)
     out = {
         "kernel": "k_prep_cull_lanes + k_prep_pk2<mask-in> (one full light prep per node)",
         "hbm_bytes_per_node": round((fb + wb) / nodes, 1),
         "fetch_bytes_per_node": round(fb / nodes, 1),
         "write_bytes_per_node": round(wb / nodes, 1),
-        "per_kernel_bytes_per_node": {k: round((2 * fetch[k] + write.get(k, 0.0)) / nodes, 1) for k in kernels},
+        "per_kernel_bytes_per_node": {k: round((mult[k] * fetch[k] + write.get(k, 0.0)) / nodes, 1) for k in kernels},
         "dispatches": {k: nf[k] for k in kernels},
         "full_prep_nodes": int(nodes),
-        "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 64-B tally of 128-B requests) and --pmc WRITE_SIZE in "
+        "method": "rocprofv3 --pmc FETCH_SIZE (x2 for k_prep_pk2's 16-B-per-lane record loads, gfx950's 64-B tally of 128-B requests; x1 for the cull's scalar loads) and --pmc WRITE_SIZE in "
                   "separate passes over `bench.py --steps %d --warmup %d --no-cpu`; bytes of both kernels over all "
                   "dispatches / full-prep nodes (timed-step count scaled to the profiled steps: warmup + timed + replay); "
                   "tools/prep_hbm_bytes.py"

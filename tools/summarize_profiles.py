@@ -9,11 +9,21 @@ Either rocprofv3's CSV output (--output-format csv) or its default rocpd databas
         --fetch gpurun_out/pmc_r1_fetch --write gpurun_out/pmc_r1_write --sq gpurun_out/pmc_r1_sq \
         --bench gpurun_out/bench_default.log
 
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) is doubled (gfx950 tallies the 128-B
-requests of 16-B-per-lane loads at 64 B), WRITE_SIZE is taken as is; both come from separate
---pmc passes.  They are L2 fabric-side requests, so Infinity-Cache hits are included (an upper
-bound on HBM bytes).
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) is doubled only for the kernels whose
+loads are 16 B per lane (WIDE_LOAD_KERNELS: gfx950 tallies those 128-B requests at 64 B); other
+widths are uncalibrated and taken as is (labelled so).  WRITE_SIZE is taken as is; both come from
+separate --pmc passes.  They are L2 fabric-side requests, so Infinity-Cache hits are included (an
+upper bound on HBM bytes).
+
+VALU: valu_issue_frac = 4 x SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) -- the share of
+the SIMDs' issue cycles held by VALU instructions (a wave64 VALU instruction holds its SIMD for at
+least 4 cycles, the transcendentals longer: a lower bound, <= 1 up to the GRBM clock estimate).
 """
+WIDE_LOAD_KERNELS = ("k_prep_pk2", "k_mis_rays", "k_rays_persistent", "k_extend_brdf", "k_primary")
+
+
+def wide(kernel):
+    return kernel.startswith(WIDE_LOAD_KERNELS)
 import argparse
 import collections
 import csv
@@ -44,10 +54,9 @@ def counters(d):
 
 def pmc_latest(tag, summary):
     """Per-kernel PMC figures bench.py attaches to its roofline objects (profiles/pmc_latest.json):
-    VALU busy = 4 * SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs),
-    the effective clock GRBM_GUI_ACTIVE / 8 / duration, and HBM-side bytes per dispatch (FETCH_SIZE
-    x2 + WRITE_SIZE, MI355X_MICROARCH.md); the SQ and GRBM counters come from separate passes over
-    the same workload, so both are taken per dispatch."""
+    valu_issue_frac (module docstring), the effective clock GRBM_GUI_ACTIVE / 8 / duration, and
+    HBM-side bytes per dispatch (FETCH_SIZE, x2 for 16-B-per-lane loads, + WRITE_SIZE); the SQ and
+    GRBM counters come from separate passes over the same workload, so both are taken per dispatch."""
     ks, sq, hbm = summary.get("kernel_stats", {}), summary.get("sq", {}), summary.get("hbm", {})
     out = {"source": "profiles/%s_summary.json (rocprofv3 --pmc passes; tools/summarize_profiles.py)" % tag,
            "kernels": {}}
@@ -55,9 +64,10 @@ def pmc_latest(tag, summary):
         if not k.startswith("k_") or k not in sq or not h.get("grbm_gui_active"):
             continue
         g = h["grbm_gui_active"] / h["dispatches"]  # summed over the 8 XCDs, per dispatch
-        a = sq[k]["SQ_ACTIVE_INST_VALU"] / sq[k]["dispatches"]
-        e = {"valu_busy": round(4 * a / (1024 * g / 8), 4),
+        iv = sq[k]["SQ_INSTS_VALU"] / sq[k]["dispatches"]
+        e = {"valu_issue_frac": round(4 * iv / (1024 * g / 8), 4),
              "hbm_bytes_per_dispatch": h["fetch_bytes_per_dispatch"] + h["write_bytes_per_dispatch"],
+             "fetch_width": "16B/lane (FETCH_SIZE x2)" if wide(k) else "uncalibrated (FETCH_SIZE x1)",
              "dispatches": h["dispatches"]}
         if k in ks:
             e["avg_us"] = ks[k]["avg_us"]
@@ -100,7 +110,7 @@ def main():
         for k in fc:
             if k not in wc:
                 continue
-            fetch_b = 2 * fc[k]["FETCH_SIZE"] * 1024
+            fetch_b = (2 if wide(k) else 1) * fc[k]["FETCH_SIZE"] * 1024
             write_b = wc[k]["WRITE_SIZE"] * 1024
             n = fc[k]["dispatches"]
             hbm[k] = {"dispatches": n, "fetch_bytes_per_dispatch": fetch_b / n,
