@@ -2130,14 +2130,20 @@ __global__ __launch_bounds__(kExactBlock) void k_prep_exact(DScene S, uint64_t s
         for (int k0 = 0; k0 < ncand; k0 += 64) {
             const bool in = k0 + lane < ncand;
             const double wv = in ? wsc[k0 + lane] : -1.0;
-            const int nk = min(64, ncand - k0);
+            const uint64_t sm = __ballot(in && wv >= 0.0);
+            surv += __popcll(sm);
             double mine = -1.0;
-            for (int q = 0; q < nk; q++) {
-                const double wq = __shfl(wv, q);
-                run += fmax(wq, 0.0);  // a culled candidate (-1) adds +0, leaving the sum unchanged
-                mine = lane == q ? (wq >= 0.0 ? run : -1.0) : mine;
+            // the chunk's survivors in order: each weight read into SGPRs (v_readlane) and added by every
+            // lane to the same running sum, so the chain is one dependent v_add_f64 per survivor
+            for (uint64_t m = sm; m; m &= m - 1) {
+                const int q = __ffsll((unsigned long long)m) - 1;
+                const unsigned long long b = __double_as_longlong(wv);
+                const double wq = __longlong_as_double(
+                    ((long long)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), q) << 32) |
+                    (unsigned)__builtin_amdgcn_readlane((int)b, q));
+                run += wq;
+                mine = lane == q ? run : mine;
             }
-            surv += __popcll(__ballot(in && wv >= 0.0));
             if (in) wsc[k0 + lane] = mine;  // running sum after this survivor, -1 if culled
         }
         wave_lds_sync();
