@@ -134,10 +134,15 @@ def lib():
         L.mcpt_closest_hit.argtypes = [P, I, dp, dp, ip, I, ip, dp]
         L.mcpt_light_prep.argtypes = [P, I, dp, dp, dp, dp, ip, ip]
         L.mcpt_primary_hits.argtypes = [P, C.POINTER(Camera), ip, dp]
-        L.mcpt_debug_prep_bench.argtypes = [P, I, dp, dp, dp, I, I, C.POINTER(C.c_double), dp, ip]
-        L.mcpt_debug_tri_filter.argtypes = [I, fp, dp, dp, fp, ip, fp]
-        L.mcpt_debug_light_prep_exact.argtypes = [P, I, dp, dp, dp, dp, ip, ip]
-        L.mcpt_debug_light_literal.argtypes = [P, dp, dp, dp]
+        # debug entry points (include/mcpt_debug.h): bound when present, so an older build can still
+        # be timed against this one through MCPT_LIB_PATH (tools/ab_run.sh)
+        dbg = {"mcpt_debug_prep_bench": [P, I, dp, dp, dp, I, I, C.POINTER(C.c_double), dp, ip],
+               "mcpt_debug_tri_filter": [I, fp, dp, dp, fp, ip, fp],
+               "mcpt_debug_light_prep_exact": [P, I, dp, dp, dp, dp, ip, ip],
+               "mcpt_debug_light_literal": [P, dp, dp, dp]}
+        for name, argt in dbg.items():
+            if hasattr(L, name):
+                getattr(L, name).argtypes = argt
         L.mcpt_tone_map.argtypes = [dp, I, I, D, D, u8]
         L.mcpt_write_bmp.argtypes = [C.c_char_p, u8, I, I]
         L.mcpt_comm_unique_id.argtypes = [C.c_char_p]

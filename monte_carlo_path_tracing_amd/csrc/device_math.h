@@ -6,6 +6,8 @@
 
 #include <cstdint>
 
+#include "acos_cr.h"
+
 namespace mcpt {
 
 #define MCPT_EPS 1e-8
@@ -109,11 +111,11 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
     double theta, st, ct, sp, cp;
     double phi = 2 * MCPT_PI * k2;
     if (ind == 0) {
-        theta = 0.5 * acos(fmax(-1.0, fmin(1.0, 1 - 2 * k1)));
+        theta = 0.5 * acos_cr(fmax(-1.0, fmin(1.0, 1 - 2 * k1)));
         sincos(theta, &st, &ct);
         pdf *= ct / MCPT_PI;
     } else {
-        theta = acos(fmax(-1.0, fmin(1.0, pow(k1, 1 / (sh + 1)))));
+        theta = acos_cr(fmax(-1.0, fmin(1.0, pow(k1, 1 / (sh + 1)))));
         sincos(theta, &st, &ct);
         pdf *= (sh + 1) / (2 * MCPT_PI) * pow(k1, sh / (sh + 1));
         axis = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
@@ -167,13 +169,13 @@ __device__ inline int light_tri_stage(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d
         B = C;
         C = t;
     }
-    double a = acos(fmax(-1.0, fmin(1.0, dot(B, C))));
-    double b = acos(fmax(-1.0, fmin(1.0, dot(A, C))));
-    double c = acos(fmax(-1.0, fmin(1.0, dot(A, B))));
+    double a = acos_cr(fmax(-1.0, fmin(1.0, dot(B, C))));
+    double b = acos_cr(fmax(-1.0, fmin(1.0, dot(A, C))));
+    double c = acos_cr(fmax(-1.0, fmin(1.0, dot(A, B))));
     if (a < MCPT_EPS || b < MCPT_EPS || c < MCPT_EPS) return 3;
-    double alpha = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(B, A)), normalized(cross(A, C))))));
-    double beta = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(C, B)), normalized(cross(B, A))))));
-    double gamma = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(A, C)), normalized(cross(C, B))))));
+    double alpha = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(B, A)), normalized(cross(A, C))))));
+    double beta = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(C, B)), normalized(cross(B, A))))));
+    double gamma = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(A, C)), normalized(cross(C, B))))));
     if (alpha < MCPT_EPS || beta < MCPT_EPS || gamma < MCPT_EPS) return 3;
     double sA = alpha + beta + gamma - MCPT_PI;
     if (sA < 0) return 3;

@@ -212,8 +212,11 @@ __device__ inline void load_node(const BvhNode4* nd, float (&lo)[3][4], float (&
 // -- the same plane (org + byte * scale, quantize_bvh4 rounds it outward) with a few more fp32
 // roundings, each ~1 ulp of |plane - origin| * |inv|, far inside the boxes' 1e-5-of-the-scene
 // margins; 2 VALU per plane (v_cvt_f32_ubyteN + v_fma_f32) plus 2 per axis
-__device__ inline void node_tplanes(const BvhNode4Q* nd, const float (&inv)[3], const float (&oi)[3], float (&tl)[3][4],
-                                    float (&th)[3][4], int (&ch)[4]) {
+// The planes come out as near (tn) and far (tf) per axis: the byte arrays are swapped by the sign of
+// the inverse direction (neg[a]), as m = scale * inv carries that sign and fma(q, m, b) is monotone
+// in q -- tn / tf are exactly the fminf / fmaxf of the two slab distances.
+__device__ inline void node_tplanes(const BvhNode4Q* nd, const float (&inv)[3], const float (&oi)[3], const bool (&neg)[3],
+                                    float (&tn)[3][4], float (&tf)[3][4], int (&ch)[4]) {
     const float4 v0 = *reinterpret_cast<const float4*>(nd->org);
     const uint4 v1 = *reinterpret_cast<const uint4*>(nd->q);
     const uint2 v2 = *reinterpret_cast<const uint2*>(nd->q + 4);
@@ -225,10 +228,11 @@ __device__ inline void node_tplanes(const BvhNode4Q* nd, const float (&inv)[3], 
     for (int a = 0; a < 3; a++) {
         const float m = __uint_as_float(((ex >> (8 * a)) & 0xffu) << 23) * inv[a];
         const float b = fmaf(org[a], inv[a], -oi[a]);
+        const unsigned qn = neg[a] ? qh[a] : ql[a], qf = neg[a] ? ql[a] : qh[a];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            tl[a][k] = fmaf((float)((ql[a] >> (8 * k)) & 0xffu), m, b);
-            th[a][k] = fmaf((float)((qh[a] >> (8 * k)) & 0xffu), m, b);
+            tn[a][k] = fmaf((float)((qn >> (8 * k)) & 0xffu), m, b);
+            tf[a][k] = fmaf((float)((qf >> (8 * k)) & 0xffu), m, b);
         }
     }
     ch[0] = c.x, ch[1] = c.y, ch[2] = c.z, ch[3] = c.w;
@@ -346,6 +350,14 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     };
     const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
     const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
+    // near / far plane of each axis picked once per ray by the sign of the inverse direction, as
+    // byte offsets into the node (lo[a] at 16a, hi[a] at 48 + 16a): fma is monotone in the plane
+    // for a fixed inverse, so fma(near) is exactly the fminf of the two slab distances the min/max
+    // form computes, and the per-node min/max pairs go away.  Empty child slots (lo = FLT_MAX,
+    // hi = -FLT_MAX, collapse_bvh4) then give t0 >= FLT_MAX > t1 for any |inverse| >= 1 (a unit
+    // direction's), so they miss without a child-code test.
+    const unsigned nx = ix < 0 ? 48u : 0u, ny = iy < 0 ? 64u : 16u, nz = iz < 0 ? 80u : 32u;
+    const unsigned fx = 48u - nx, fy = 80u - ny, fz = 112u - nz;
     // tlimit0: at least the t of a triangle tri_hit accepts (or FLT_MAX) -- boxes beyond it hold no
     // closest hit
     float tlimit = tlimit0;
@@ -389,26 +401,35 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     while (node != kDone || leaf < 0) {
         while (node >= 0 && node != kDone) {
             if (kCount) ++*visits;
-            float lo[3][4], hi[3][4];
-            int chs[4];
-            // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch,
-            // so each side reads one address space: ds_read from the LDS copy, global loads else)
-            if (kTop > 0 && __all(node < kTop)) load_node(top + node, lo, hi, chs);
-            else load_node(nodes + node, lo, hi, chs);
-            const float* lxs = lo[0], *lys = lo[1], *lzs = lo[2], *hxs = hi[0], *hys = hi[1], *hzs = hi[2];
             float t[4];
             int code[4];
+            // 32-bit byte offsets from the (wave-uniform) tree base: one v_or per load
+            const unsigned noff = (unsigned)node * (unsigned)sizeof(BvhNode4);
+            // loads + four slab tests, instantiated once per address space so that the two paths
+            // join on (t, code) rather than on the 28 loaded dwords (a join on those made the
+            // compiler wait for the first loads before issuing the rest)
+            auto visit = [&](const BvhNode4* base) {
+                const char* b = reinterpret_cast<const char*>(base);
+                auto at = [&](unsigned o) { return *reinterpret_cast<const float4*>(b + (noff + o)); };
+                const float4 pnx = at(nx), pfx = at(fx), pny = at(ny), pfy = at(fy), pnz = at(nz), pfz = at(fz);
+                const int4 c4 = *reinterpret_cast<const int4*>(b + (noff + (unsigned)offsetof(BvhNode4, child)));
+                const float nxs[4] = {pnx.x, pnx.y, pnx.z, pnx.w}, fxs[4] = {pfx.x, pfx.y, pfx.z, pfx.w};
+                const float nys[4] = {pny.x, pny.y, pny.z, pny.w}, fys[4] = {pfy.x, pfy.y, pfy.z, pfy.w};
+                const float nzs[4] = {pnz.x, pnz.y, pnz.z, pnz.w}, fzs[4] = {pfz.x, pfz.y, pfz.z, pfz.w};
+                const int chs[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const float tx0 = fmaf(lxs[k], ix, -oix), tx1 = fmaf(hxs[k], ix, -oix);
-                const float ty0 = fmaf(lys[k], iy, -oiy), ty1 = fmaf(hys[k], iy, -oiy);
-                const float tz0 = fmaf(lzs[k], iz, -oiz), tz1 = fmaf(hzs[k], iz, -oiz);
-                const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
-                const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
-                t[k] = h ? t0 : FLT_MAX;
-                code[k] = h ? chs[k] : kDone;  // leaves come pre-packed (pack_leaf_codes)
-            }
+                for (int k = 0; k < 4; k++) {
+                    const float t0 = fmaxf(fmaxf(fmaf(nxs[k], ix, -oix), fmaf(nys[k], iy, -oiy)), fmaxf(fmaf(nzs[k], iz, -oiz), 0.0f));
+                    const float t1 = fminf(fminf(fmaf(fxs[k], ix, -oix), fmaf(fys[k], iy, -oiy)), fminf(fmaf(fzs[k], iz, -oiz), tlimit));
+                    const bool h = t0 <= fmaf(t1, 1.00001f, 1e-6f);
+                    t[k] = h ? t0 : FLT_MAX;
+                    code[k] = h ? chs[k] : kDone;  // leaves come pre-packed (pack_leaf_codes)
+                }
+            };
+            // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch,
+            // so each side reads one address space: ds_read from the LDS copy, global loads else)
+            if (kTop > 0 && __all(node < kTop)) visit(top);
+            else visit(nodes);
             // sort (t, code) ascending; misses (FLT_MAX, kDone) sink to the end
             auto cs = [&](int a, int b) {
                 const bool sw = t[b] < t[a];
@@ -456,6 +477,19 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     if (kFilter && pend0 >= 0) exact(pend0);
     if (kFilter && pend1 >= 0) exact(pend1);
     return best;
+}
+
+// The picked triangle's spherical triangle for Arvo's sampler (Mylight.cpp:453-461): the reference's
+// literal chain (light_tri_stage -- sqrt / division unit vectors, six correctly rounded acos,
+// alpha + beta + gamma - pi), so the sampled direction follows the oracle's arithmetic; light_full's
+// rsqrt / atan2 form differs by up to ~1e-10 relative in sA for small triangles.  One triangle per
+// node, so the literal chain costs little here.  light_full stays as the fallback for a pick the
+// literal chain would cull (a pick from the fp32 prep's weights).
+__device__ inline void pick_sph(const DScene& S, int pick, d3 p, d3 N, SphTri* sph) {
+    const double4 ln = S.lt_n[pick];
+    const d3 p0 = f3(S.lt_v[3 * pick]), p1 = f3(S.lt_v[3 * pick + 1]), p2 = f3(S.lt_v[3 * pick + 2]);
+    if (light_tri_stage(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, sph) != 0)
+        light_full(p0, p1, p2, 2.0 * ln.w, p, N, sph);
 }
 
 // x86 cvttsd2si semantics for (int)floor(x) of the reference (out of range -> INT_MIN)
@@ -565,6 +599,9 @@ struct Queue {
 // k_rays_persistent reads the 64-B compressed nodes (BvhNode4Q): Cornell-1M traversal -6%; the
 // L2-resident kernels keep the 128-B fp32 nodes (their decode VALU costs more than the lines save:
 // Veach MIS -1.5%, BRDF -5%; profiles/round2b_ab_bvh_quant.txt)
+#ifndef MCPT_EXACT_PICK
+#define MCPT_EXACT_PICK 1
+#endif
 #ifndef MCPT_PERSIST_QUANT
 #define MCPT_PERSIST_QUANT 1
 #endif
@@ -2074,8 +2111,8 @@ __global__ __launch_bounds__(256) void k_prep_band(DScene S, int n, const double
 // (light_tri_stage: sqrt / division unit vectors, six acos, alpha + beta + gamma - pi,
 // Mylight.cpp:360-413), weights_sum summed candidate by candidate in index order (Mylight.cpp:415-418)
 // and the pick "first survivor whose running sum >= u weights_sum, else the last survivor" -- so
-// weights_sum, the survivor count and the pick are the oracle's bit for bit (up to libm's acos: ocml
-// vs glibc).  One wave per node: the candidate list and weights go to this wave's scratch slab;
+// weights_sum, the survivor count and the pick are the oracle's bit for bit (acos_cr: correctly
+// rounded, so up to glibc's acos on the ~5e-4 of arguments it rounds the other way).  One wave per node: the candidate list and weights go to this wave's scratch slab;
 // the running sum is sequential (each lane adds the same broadcast weight in order, lane q keeps the
 // sum after candidate q), the pick a ballot search over the stored running sums.
 constexpr int kExactBlock = 256;
@@ -2191,12 +2228,12 @@ __global__ void k_light_literal(DScene S, d3 x1, d3 nn, double* out) {
         C = tt;
     }
     o[1] = A.x, o[2] = A.y, o[3] = A.z, o[4] = B.x, o[5] = B.y, o[6] = B.z, o[7] = C.x, o[8] = C.y, o[9] = C.z;
-    o[10] = acos(fmax(-1.0, fmin(1.0, dot(B, C))));
-    o[11] = acos(fmax(-1.0, fmin(1.0, dot(A, C))));
-    o[12] = acos(fmax(-1.0, fmin(1.0, dot(A, B))));
-    o[13] = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(B, A)), normalized(cross(A, C))))));
-    o[14] = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(C, B)), normalized(cross(B, A))))));
-    o[15] = acos(fmax(-1.0, fmin(1.0, -dot(normalized(cross(A, C)), normalized(cross(C, B))))));
+    o[10] = acos_cr(fmax(-1.0, fmin(1.0, dot(B, C))));
+    o[11] = acos_cr(fmax(-1.0, fmin(1.0, dot(A, C))));
+    o[12] = acos_cr(fmax(-1.0, fmin(1.0, dot(A, B))));
+    o[13] = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(B, A)), normalized(cross(A, C))))));
+    o[14] = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(C, B)), normalized(cross(B, A))))));
+    o[15] = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(A, C)), normalized(cross(C, B))))));
     o[16] = o[13] + o[14] + o[15] - MCPT_PI;
     o[17] = o[0] == 0 ? t.w : -1.0;
     o[18] = -dot(normalized(cross(B, A)), normalized(cross(A, C)));  // alpha's acos argument
@@ -2348,7 +2385,7 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
     if (pick >= 0) {
         const double4 ln = S.lt_n[pick];
         SphTri sph;
-        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), 2.0 * ln.w, p, N, &sph);
+        pick_sph(S, pick, p, N, &sph);
         const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
         TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
         coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:475-481)
@@ -2614,29 +2651,33 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
 #endif
             const float4* __restrict__ leafv = set == 2 ? S.lleaf_v : S.leaf_v;
             const float inv3[3] = {ix, iy, iz}, oi3[3] = {oix, oiy, oiz};
+            const bool neg3[3] = {ix < 0, iy < 0, iz < 0};
             while (node >= 0 && node != kDone) {
                 if (kCount) ++visits;
-                float tl[3][4], th[3][4];
+                float tn[3][4], tf[3][4];  // near / far slab distances per axis and child
                 int chs[4];
 #if MCPT_PERSIST_QUANT
-                node_tplanes(nodes + node, inv3, oi3, tl, th, chs);
+                node_tplanes(nodes + node, inv3, oi3, neg3, tn, tf, chs);
 #else
-                load_node(nodes + node, tl, th, chs);
+                float lo[3][4], hi[3][4];
+                load_node(nodes + node, lo, hi, chs);
 #pragma unroll
                 for (int a = 0; a < 3; a++)
 #pragma unroll
-                    for (int k = 0; k < 4; k++) tl[a][k] = fmaf(tl[a][k], inv3[a], -oi3[a]), th[a][k] = fmaf(th[a][k], inv3[a], -oi3[a]);
+                    for (int k = 0; k < 4; k++) {
+                        const float t0 = fmaf(lo[a][k], inv3[a], -oi3[a]), t1 = fmaf(hi[a][k], inv3[a], -oi3[a]);
+                        tn[a][k] = neg3[a] ? t1 : t0, tf[a][k] = neg3[a] ? t0 : t1;
+                    }
 #endif
                 float t[4];
                 int code[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const float tx0 = tl[0][k], tx1 = th[0][k];
-                    const float ty0 = tl[1][k], ty1 = th[1][k];
-                    const float tz0 = tl[2][k], tz1 = th[2][k];
-                    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
-                    const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
+                    const float t0 = fmaxf(fmaxf(tn[0][k], tn[1][k]), fmaxf(tn[2][k], 0.0f));
+                    const float t1 = fminf(fminf(tf[0][k], tf[1][k]), fminf(tf[2][k], tlimit));
+                    // empty slots keep their test here: a quantized empty slot's planes (255, 0) can
+                    // fall inside the margin when the node's scale is tiny
+                    const bool h = chs[k] != kBvh4Empty && t0 <= fmaf(t1, 1.00001f, 1e-6f);
                     t[k] = h ? t0 : FLT_MAX;
                     code[k] = h ? chs[k] : kDone;
                 }
@@ -2897,7 +2938,7 @@ __global__ __launch_bounds__(256, MCPT_LB_SHADE_GEN) void k_shade_gen(Params P, 
     } else if ((pick = cur.pick[i]) >= 0) {
         const double4 ln = S.lt_n[pick];
         SphTri sph;
-        light_full(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), 2.0 * ln.w, p, N, &sph);
+        pick_sph(S, pick, p, N, &sph);
         const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
         TriHit th = tri_hit(f3(S.lt_v[3 * pick]), f3(S.lt_v[3 * pick + 1]), f3(S.lt_v[3 * pick + 2]), p, Pd);
         coord = add(p, mul(Pd, th.hit ? th.t : 0.0));  // miss: t = 0 (Mylight.cpp:311-317)
@@ -3766,7 +3807,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     }
     // exact pick: nodes inside the ambiguity band go to k_prep_exact; the opt-in fp32
     // precision makes no exactness claim, and the small-table prep (k_prep_lane) is exact by construction
-    const bool exact_pick = needs_prep && !fp32 && D.d.NL > kSmallNL;
+    // MCPT_EXACT_PICK=0 builds the pre-round-3 prep (VOS weights' own pick) for the cost A/B only
+    const bool exact_pick = MCPT_EXACT_PICK && needs_prep && !fp32 && D.d.NL > kSmallNL;
     int* exact_list = nullptr;
     double *exact_scr = nullptr, *slack = nullptr;
     if (exact_pick) {

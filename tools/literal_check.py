@@ -1,10 +1,12 @@
 """GPU diagnostics (run on the box): the reference's literal light-prep chain on the GPU
 (mcpt_debug_light_literal: fp64 sqrt, division, ocml acos) against the same formulas on the host
-(numpy float64 in the reference's operation order, glibc acos) and the oracle's weights, at the golden
+(numpy float64 in the reference's operation order, glibc acos through math.acos -- numpy's own
+arccos is a vector implementation that is not glibc's) and the oracle's weights, at the golden
 prep points -- locates the first intermediate that differs.  Test infrastructure (loads the oracle).
 
     python tools/literal_check.py [npoints]
 """
+import math
 import sys
 
 import numpy as np
@@ -30,6 +32,9 @@ def cross(a, b):
                      a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]], -1)
 
 
+_acos = np.vectorize(math.acos, otypes=[np.float64])
+
+
 def main():
     npts = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     sc = mcpt.Scene.load(OBJ, XML)
@@ -51,14 +56,14 @@ def main():
         B, C = B2, C2
         h = {}
         h["A"], h["B"], h["C"] = A, B, C
-        h["a"] = np.arccos(np.clip(dot(B, C), -1, 1))
-        h["b"] = np.arccos(np.clip(dot(A, C), -1, 1))
-        h["c"] = np.arccos(np.clip(dot(A, B), -1, 1))
+        h["a"] = _acos(np.clip(dot(B, C), -1, 1))
+        h["b"] = _acos(np.clip(dot(A, C), -1, 1))
+        h["c"] = _acos(np.clip(dot(A, B), -1, 1))
         h["alpha_arg"] = -dot(norm(cross(B, A)), norm(cross(A, C)))
         h["BC"] = dot(B, C)
-        h["alpha"] = np.arccos(np.clip(h["alpha_arg"], -1, 1))
-        h["beta"] = np.arccos(np.clip(-dot(norm(cross(C, B)), norm(cross(B, A))), -1, 1))
-        h["gamma"] = np.arccos(np.clip(-dot(norm(cross(A, C)), norm(cross(C, B))), -1, 1))
+        h["alpha"] = _acos(np.clip(h["alpha_arg"], -1, 1))
+        h["beta"] = _acos(np.clip(-dot(norm(cross(C, B)), norm(cross(B, A))), -1, 1))
+        h["gamma"] = _acos(np.clip(-dot(norm(cross(A, C)), norm(cross(C, B))), -1, 1))
         h["sA"] = h["alpha"] + h["beta"] + h["gamma"] - 3.141592653589793
         gv = {"A": g[:, 1:4], "B": g[:, 4:7], "C": g[:, 7:10], "a": g[:, 10], "b": g[:, 11], "c": g[:, 12],
               "alpha": g[:, 13], "beta": g[:, 14], "gamma": g[:, 15], "sA": g[:, 16], "w": g[:, 17],
