@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 20100 /* 2.1.0: mcpt_stats gains prep_exact_nodes and cache_build_seconds (appended);
+#define MCPT_VERSION 20100 /* 2.1.0: mcpt_stats gains prep_exact_nodes, cache_build_seconds and prep_band_nodes
+                               * (appended);
                                * 2.0.0: mcpt_render_opts carries struct_size (checked first), a device list
                                * and a multi-process communicator; debug entry points moved to mcpt_debug.h */
 
@@ -180,6 +181,8 @@ typedef struct {
                                 * boundary and were redone with the reference's literal formulas and
                                 * summation order (Mylight.cpp:335-438), so the pick is the reference's */
     double cache_build_seconds; /* device time building the per-pixel root-point cache (in prep_seconds) */
+    uint64_t prep_band_nodes;   /* light preps whose slack the whole-table band bound could not clear and
+                                 * that took the per-chunk band test (prep_exact_nodes of them failed it) */
 } mcpt_stats;
 /* With several devices, `seconds` is the wall time of the whole call (shards + reduce), counts are
  * summed over devices and prep_seconds is summed device time. */

@@ -77,7 +77,8 @@ class Stats(C.Structure):
                 ("prep_full_nodes", C.c_uint64), ("prep_cached_nodes", C.c_uint64), ("prep_cache_points", C.c_uint64),
                 ("spilled_nodes", C.c_uint64), ("reduce_seconds", C.c_double), ("devices_used", C.c_int32),
                 ("trace_seconds", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
-                ("tri_tests", C.c_uint64), ("prep_exact_nodes", C.c_uint64), ("cache_build_seconds", C.c_double)]
+                ("tri_tests", C.c_uint64), ("prep_exact_nodes", C.c_uint64), ("cache_build_seconds", C.c_double),
+                ("prep_band_nodes", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -11,7 +11,8 @@
 // evaluated in double-double: x - cos(y0) = (x - 1) + (1 - cos y0), where x - 1 is exact (two_sum)
 // and 1 - cos y0 = z (1/2 - z/24 + z^2/720 - ...) with z = y0^2 as a double-double (the first four
 // coefficients as double-doubles, the rest in double: their terms are < 1e-5 of the sum), so the
-// residual carries ~1e-32 absolute error; y = y0 - residual / sin(y0), sin(y0) = sqrt((1 - x)(1 + x)).
+// residual carries ~1e-32 absolute error; y = y0 - residual / sin(y0), sin(y0) = sqrt((1 - x)(1 + x))
+// (on the GPU through v_rsq_f64: the step is ~1 ulp, so its own few-ulp error is irrelevant).
 // Negative x: acos(x) = pi - acos(-x) with pi as a double-double.  The last step adds a correction of
 // ~1 ulp to y0 in one rounding, so the result is correctly rounded unless the true value lies within
 // ~1e-30 relative of a rounding boundary.
@@ -75,8 +76,14 @@ __host__ __device__ inline double acos_newton_corr(double x, double y0) {
     const DD omc = dd_mul(z, p);                 // 1 - cos(y0)
     const DD xm1 = dd_two_sum(x, -1.0);          // x - 1, exactly
     const double r = (xm1.h + omc.h) + (xm1.l + omc.l);  // x - cos(y0); the first sum is exact (Sterbenz)
-    const double s = sqrt((1.0 - x) * (1.0 + x));        // sin(y0) to ~1 ulp: enough for a ~1-ulp step
-    return -r / s;
+    // 1 / sin(y0): the step is ~1 ulp of y0, so ~1e-6 relative accuracy of it is plenty -- the
+    // hardware reciprocal square root on the GPU instead of sqrt and a division
+    const double s2 = (1.0 - x) * (1.0 + x);
+#ifdef __HIP_DEVICE_COMPILE__
+    return -r * __builtin_amdgcn_rsq(s2);
+#else
+    return -r / sqrt(s2);
+#endif
 }
 
 __host__ __device__ inline double acos_cr(double x) {

@@ -34,9 +34,29 @@ __device__ inline d3 cross(d3 a, d3 b) {
     return d3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 __device__ inline double norm2(d3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
-__device__ inline d3 normalized(d3 a) {  // vec.cpp:99-103
-    double l = norm2(a);
-    return d3{a.x / l, a.y / l, a.z / l};
+// vec.cpp:99-103: a.x / l, a.y / l, a.z / l with l = sqrt(x^2 + y^2 + z^2), each quotient correctly
+// rounded.  The backend's fp64 division is v_div_scale (x2), v_rcp_f64, two Newton steps on the
+// reciprocal, q = n y, r = fma(-l, q, n), v_div_fmas (= fma(r, y, q) unscaled) and v_div_fixup; the
+// reciprocal part depends on l alone, so for the three quotients by one l it is done once here.  In the
+// range where v_div_scale leaves its operands alone and v_div_fixup returns its input (l and the
+// quotients' exponents far from the limits: l in [2^-500, 2^500], each nonzero |n| >= l 2^-500) this is
+// the same arithmetic, so the quotients are the same correctly rounded values (a zero numerator keeps
+// its sign through r == 0); outside it, plain division.
+__device__ inline d3 normalized(d3 a) {
+    const double l = norm2(a);
+    const double lo = l * 0x1.0p-500;
+    const bool fast = l >= 0x1.0p-500 && l <= 0x1.0p500 && (a.x == 0.0 || fabs(a.x) >= lo) &&
+                      (a.y == 0.0 || fabs(a.y) >= lo) && (a.z == 0.0 || fabs(a.z) >= lo);
+    if (!fast) return d3{a.x / l, a.y / l, a.z / l};
+    const double y0 = __builtin_amdgcn_rcp(l);
+    const double y1 = fma(y0, fma(-l, y0, 1.0), y0);
+    const double y = fma(y1, fma(-l, y1, 1.0), y1);
+    auto q = [&](double n) {
+        const double q0 = n * y;
+        const double r = fma(-l, q0, n);
+        return r == 0.0 ? q0 : fma(r, y, q0);
+    };
+    return d3{q(a.x), q(a.y), q(a.z)};
 }
 __device__ inline double det3(d3 a, d3 b, d3 c) { return dot(cross(a, b), c); }
 __device__ inline d3 cols_mul(d3 c0, d3 c1, d3 c2, d3 x) {  // matrix3d(c0,c1,c2) * x
@@ -156,7 +176,12 @@ struct SphTri {
     double alpha, c, sA, w;
 };
 // cull stage reached: 0 = survives the reference's cull chain, 1 = culled by the light-side test
-// (Mylight.cpp:340-345), 2 = by the tangent-plane test (:347-357), 3 = by a later degeneracy test
+// (Mylight.cpp:340-345), 2 = by the tangent-plane test (:347-357), 3 = by a later degeneracy test.
+// The edge-length culls a, b, c < 1e-8 (:372-374) need no acos: acos(x) < 1e-8 iff the clamped x is
+// 1 (acos of the largest double below 1 is 1.49e-8, for glibc as for the correctly rounded acos_cr;
+// NaN clamps to 1 as well), so the chain takes three acos (alpha, beta, gamma) plus c = acos(A.B)
+// when Arvo's sampler needs it (kArvo: o->alpha, o->c).  w = sA lsum.
+template <bool kArvo = false>
 __device__ inline int light_tri_stage(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d3 x1, d3 n, SphTri* o) {
     double tmp = dot(nl, sub(x1, p0));
     if (tmp < 0 || fabs(tmp) < MCPT_EPS) return 1;
@@ -169,13 +194,14 @@ __device__ inline int light_tri_stage(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d
         B = C;
         C = t;
     }
-    double a = acos_cr(fmax(-1.0, fmin(1.0, dot(B, C))));
-    double b = acos_cr(fmax(-1.0, fmin(1.0, dot(A, C))));
-    double c = acos_cr(fmax(-1.0, fmin(1.0, dot(A, B))));
-    if (a < MCPT_EPS || b < MCPT_EPS || c < MCPT_EPS) return 3;
-    double alpha = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(B, A)), normalized(cross(A, C))))));
-    double beta = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(C, B)), normalized(cross(B, A))))));
-    double gamma = acos_cr(fmax(-1.0, fmin(1.0, -dot(normalized(cross(A, C)), normalized(cross(C, B))))));
+    const double ca = fmax(-1.0, fmin(1.0, dot(B, C)));
+    const double cb = fmax(-1.0, fmin(1.0, dot(A, C)));
+    const double cc = fmax(-1.0, fmin(1.0, dot(A, B)));
+    if (ca == 1.0 || cb == 1.0 || cc == 1.0) return 3;  // a, b or c < 1e-8
+    const d3 uBA = normalized(cross(B, A)), uAC = normalized(cross(A, C)), uCB = normalized(cross(C, B));
+    double alpha = acos_cr(fmax(-1.0, fmin(1.0, -dot(uBA, uAC))));
+    double beta = acos_cr(fmax(-1.0, fmin(1.0, -dot(uCB, uBA))));
+    double gamma = acos_cr(fmax(-1.0, fmin(1.0, -dot(uAC, uCB))));
     if (alpha < MCPT_EPS || beta < MCPT_EPS || gamma < MCPT_EPS) return 3;
     double sA = alpha + beta + gamma - MCPT_PI;
     if (sA < 0) return 3;
@@ -187,7 +213,7 @@ __device__ inline int light_tri_stage(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d
         o->B = B;
         o->C = C;
         o->alpha = alpha;
-        o->c = c;
+        o->c = kArvo ? acos_cr(cc) : 0.0;
         o->sA = sA;
         o->w = w;
     }

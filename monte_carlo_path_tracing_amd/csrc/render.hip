@@ -479,16 +479,20 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     return best;
 }
 
+// MCPT_PICK_LITERAL=0: light_full's form for the picked triangle (A/B of the literal chain's cost)
+#ifndef MCPT_PICK_LITERAL
+#define MCPT_PICK_LITERAL 1
+#endif
 // The picked triangle's spherical triangle for Arvo's sampler (Mylight.cpp:453-461): the reference's
-// literal chain (light_tri_stage -- sqrt / division unit vectors, six correctly rounded acos,
-// alpha + beta + gamma - pi), so the sampled direction follows the oracle's arithmetic; light_full's
+// literal chain (light_tri_stage -- sqrt / division unit vectors, correctly rounded acos for
+// alpha, beta, gamma and c, alpha + beta + gamma - pi), so the sampled direction follows the oracle's arithmetic; light_full's
 // rsqrt / atan2 form differs by up to ~1e-10 relative in sA for small triangles.  One triangle per
 // node, so the literal chain costs little here.  light_full stays as the fallback for a pick the
 // literal chain would cull (a pick from the fp32 prep's weights).
 __device__ inline void pick_sph(const DScene& S, int pick, d3 p, d3 N, SphTri* sph) {
     const double4 ln = S.lt_n[pick];
     const d3 p0 = f3(S.lt_v[3 * pick]), p1 = f3(S.lt_v[3 * pick + 1]), p2 = f3(S.lt_v[3 * pick + 2]);
-    if (light_tri_stage(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, sph) != 0)
+    if (!MCPT_PICK_LITERAL || light_tri_stage<true>(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, sph) != 0)
         light_full(p0, p1, p2, 2.0 * ln.w, p, N, sph);
 }
 
@@ -1053,11 +1057,12 @@ constexpr int kExactHead = 16;  // exact list: [0] count, entries from [kExactHe
 __device__ inline double band_round(int ncand, double wsum) { return (2.0 * ncand + 4096.0) * kU53 * fabs(wsum); }
 // the slivers' terms: sum over flagged candidates of lsum2 sqrt(2x)/num (sliver_term), to band units
 __device__ inline double band_sliver(double acc) { return MCPT_BAND_SLIVER * 0.5 * kU53 * acc; }
-// upper bound of band_base over the whole table (scene sphere and maxima, at most N_L candidates)
-__device__ inline double band_base_upper(const DScene& S, d3 x1) {
+// upper bound of band_base for a node with ncand candidates (sum of n_c = ncand; every chunk's m_c within
+// the scene sphere's and the table's maxima)
+__device__ inline double band_base_upper(const DScene& S, d3 x1, int ncand) {
     const double dx = x1.x - S.band_ctr[0], dy = x1.y - S.band_ctr[1], dz = x1.z - S.band_ctr[2];
     const double m = S.band_S + S.band_K * (sqrt(dx * dx + dy * dy + dz * dz) + S.band_R);
-    return MCPT_BAND_KAPPA * kU53 * sqrt((double)S.NL) * m * 1.0001;
+    return MCPT_BAND_KAPPA * kU53 * sqrt((double)ncand) * m * 1.0001;
 }
 // the per-chunk term of the band for one node (this lane): n_c = set bits of the node's candidate word c
 // (mrow), or 64 without words
@@ -1088,6 +1093,15 @@ __device__ inline double pick_margin(double base, double sc, int pl, double targ
 __device__ inline double pick_slack(double margin, double wsum) {
     const double s = fmin(margin, fabs(fabs(wsum) - MCPT_EPS));
     return s == s ? s : -INFINITY;
+}
+// one lane per node: a slack the whole-table bound of the per-chunk term cannot clear is stored and the
+// node listed (maybe: count in [0], entries from kExactHead) for k_prep_band's per-chunk test
+__device__ inline void band_candidate(const DScene& S, double* slack, int* maybe, int idx, double sl, d3 x1, int ncand) {
+    if (!(sl > band_base_upper(S, x1, ncand))) {
+        slack[idx] = sl;
+        const int q = atomicAdd(maybe, 1);
+        maybe[kExactHead + q] = idx;
+    }
 }
 
 struct PrepLight {
@@ -1143,7 +1157,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
                                               const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                               int* __restrict__ pick_out, int* __restrict__ count_out,
                                               unsigned long long* stats, int nchunks, unsigned* __restrict__ work,
-                                              double* __restrict__ slack, int exact_off, int exact_counts) {
+                                              double* __restrict__ slack, int exact_off, int exact_counts,
+                                              int* __restrict__ maybe) {
     extern __shared__ double prep_lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
@@ -1288,7 +1303,7 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
             double sl = pick_slack(margin, wsum) - (band_sliver(__shfl(wave_incl_scan(sacc, lane), 63)) +
                                                     band_round(candidates, wsum));
             if (exact_counts && __ballot(degen)) sl = -INFINITY;
-            if (lane == 0) slack[exact_off + node] = sl;
+            if (lane == 0) band_candidate(S, slack, maybe, exact_off + node, sl, x1, candidates);
         }
         surv_acc += survivors;
         cand_acc += candidates;
@@ -1439,13 +1454,17 @@ struct PrepCache {
     int build;            // this launch builds entries of pixel qpixel[node] (qpixel == nullptr: node)
     int use;              // host side: root nodes go to k_prep_pick
     // exact pick: the pick's slack -- its margin less the band's terms known here
-    // (flagged slivers, summation rounding; k_prep_pick: the whole band, so +-inf) -- goes to
-    // slack[exact_off + node] for k_prep_band; null: no band (the opt-in fp32 precision, benches of
+    // (flagged slivers, summation rounding) -- is compared with the whole-table upper bound of the
+    // band's per-chunk term right away (band_candidate); only a node it does not clear has its slack
+    // stored (slack[exact_off + node]) and is listed for k_prep_band.  k_prep_pick holds the whole band
+    // (cached) and lists an ambiguous root on the exact list directly.  null: no band (the opt-in fp32 precision, benches of
     // the prep alone).  exact_counts: -inf also for nodes whose survivor count may differ (a candidate
     // the full stage culls, a near-degenerate sliver) -- the mcpt_light_prep entry reports counts.
     double* slack;
     int exact_off;
     int exact_counts;
+    int* maybe;  // nodes whose slack the whole-table bound cannot clear (band_candidate), for k_prep_band
+    int* exact;  // k_prep_pick: roots inside the cached band go straight to the exact list
 };
 
 // inverse-CDF pick from the batch totals bt[0, nb) and candidate list lst (LDS or global): returns
@@ -1906,12 +1925,12 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             pick_out[node] = pick;
             if (count_out) count_out[node] = survivors;
         }
-        if (!kF32 && C.slack) {  // exact pick: k_prep_band compares the slack with the per-chunk term
+        if (!kF32 && C.slack) {  // exact pick: the slack against the band (band_candidate, k_prep_band)
             double sl = pick_slack(margin, wsum) - (band_sl + band_round(ncand, wsum));
             // survivor counts: a candidate the full stage culls (the reference may keep it) or a
             // near-degenerate sliver (the reference may cull it) -- survivors < ncand without padding
             if (C.exact_counts && (survivors < ncand || __ballot(ndeg != 0))) sl = -INFINITY;
-            if (lane == 0) C.slack[C.exact_off + node] = sl;
+            if (lane == 0) band_candidate(S, C.slack, C.maybe, C.exact_off + node, sl, x1, ncand);
         }
         wave_lds_sync();
     }
@@ -2055,11 +2074,14 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
                 if (pls[k] >= 0) margin[k] = pick_margin(base[k], sc, pls[k], target[k]);
             }
         }
-        if (C.slack) {  // exact pick: the band stored by the cache build (same weights) + this sum's rounding
+        if (C.exact) {  // exact pick: the band stored by the cache build (same weights) + this sum's rounding
 #pragma unroll
             for (int k = 0; k < kPickNodes; k++) {
                 const double band = (double)__int_as_float(inf[k].w) + band_round(inf[k].y, wsum[k]);
-                if (lane == 0 && n0 + k < n) C.slack[C.exact_off + n0 + k] = pick_slack(margin[k], wsum[k]) > band ? INFINITY : -INFINITY;
+                if (lane == 0 && n0 + k < n && !(pick_slack(margin[k], wsum[k]) > band)) {
+                    const int q = atomicAdd(C.exact, 1);
+                    C.exact[kExactHead + q] = C.exact_off + n0 + k;
+                }
             }
         }
         int pk[kPickNodes];
@@ -2079,134 +2101,170 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
     if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
 }
 
-// Exact pick, the band test's second half (lane per node): the per-chunk term of the
-// band against the slack the prep kernels left (k_prep_pk2 / k_prep: margin less the slivers' and the
-// rounding terms; k_prep_pick: +-inf, its cached band is complete).  The whole-table upper bound decides
-// almost every node; the node's candidate words are read only when it does not.  Nodes inside the band
-// are appended to the exact list (count in list[0], wave-aggregated).
-__global__ __launch_bounds__(256) void k_prep_band(DScene S, int n, const double* __restrict__ slack,
+// Exact pick, the band test's second half (lane per listed node): the per-chunk term
+// of the band against the slack of each node band_candidate listed (k_prep_pk2 / k_prep: margin less
+// the slivers' and the rounding terms, not above the whole-table bound), from the node's candidate
+// words.  Nodes inside the band are appended to the exact list (count in list[0], wave-aggregated).
+constexpr int kBandBlocks = 128;
+__global__ __launch_bounds__(256) void k_prep_band(DScene S, const int* __restrict__ maybe, const double* __restrict__ slack,
                                                   const double* __restrict__ qp, int qs, const uint64_t* __restrict__ masks,
-                                                  int nchunks, int* __restrict__ list) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool amb = false;
-    if (i < n) {
-        const double sl = slack[i];
-        if (sl != INFINITY) {
+                                                  int nchunks, int* __restrict__ list, unsigned long long* stats) {
+    const int cnt = maybe[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && stats && cnt) atomicAdd(stats + 11, (unsigned long long)cnt);
+    for (int j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {  // block-uniform trip count
+        const int j = j0 + threadIdx.x;
+        bool amb = false;
+        int i = 0;
+        if (j < cnt) {
+            i = maybe[kExactHead + j];
+            const double sl = slack[i];
             if (!(sl > 0.0)) {
                 amb = true;
             } else {
                 const d3 x1 = mk3(qp[i], qp[qs + i], qp[2 * (size_t)qs + i]);
-                if (!(sl > band_base_upper(S, x1)))
-                    amb = !(sl > band_base(S, x1, masks ? masks + (size_t)i * mask_stride(nchunks) : nullptr, nchunks));
+                amb = !(sl > band_base(S, x1, masks ? masks + (size_t)i * mask_stride(nchunks) : nullptr, nchunks));
             }
         }
+        const int q = wave_append(reinterpret_cast<unsigned*>(list), amb);
+        if (amb) list[kExactHead + q] = i;
     }
-    const int q = wave_append(reinterpret_cast<unsigned*>(list), amb);
-    if (amb) list[kExactHead + q] = i;
 }
 
 // Exact fallback of the light prep's pick.  For the nodes the prep kernels put on
 // the exact list (list[kExactHead + j] = node index, count in list[0]): the reference's own arithmetic
-// end to end -- the cheap culls (light_cheap_stage, Mylight.cpp:340-357), the literal full stage
-// (light_tri_stage: sqrt / division unit vectors, six acos, alpha + beta + gamma - pi,
+// end to end -- the cheap culls (light_cheap_stage, Mylight.cpp:340-357; for a node whose candidate
+// words k_prep_cull_lanes wrote, those words: the same decisions), the literal full stage
+// (light_tri_stage: sqrt / division unit vectors, acos_cr vertex angles, alpha + beta + gamma - pi,
 // Mylight.cpp:360-413), weights_sum summed candidate by candidate in index order (Mylight.cpp:415-418)
 // and the pick "first survivor whose running sum >= u weights_sum, else the last survivor" -- so
 // weights_sum, the survivor count and the pick are the oracle's bit for bit (acos_cr: correctly
-// rounded, so up to glibc's acos on the ~5e-4 of arguments it rounds the other way).  One wave per node: the candidate list and weights go to this wave's scratch slab;
-// the running sum is sequential (each lane adds the same broadcast weight in order, lane q keeps the
-// sum after candidate q), the pick a ballot search over the stored running sums.
+// rounded, so up to glibc's acos on the ~5e-4 of arguments it rounds the other way).
+// One workgroup (4 waves) per node: the candidate list and the literal stage run over the workgroup's
+// 256 lanes, the candidate list and weights go to the workgroup's scratch slab; the running sum, the
+// one sequential part, runs on a single lane over kExactChunk weights at a time staged in LDS (eight
+// loads in flight ahead of the chain of dependent adds), and the pick is a ballot search over the
+// stored running sums.
 constexpr int kExactBlock = 256;
-constexpr int kExactBlocks = 256;  // grid-stride; the list is short (~1e-3 of the prep nodes)
+constexpr int kExactChunk = 1024;
+inline int exact_blocks(int NL) {  // grid-stride; scratch (2 x 8 B per light per workgroup) kept <= 1 GiB
+    const long long per = 16ll * ((NL + 255) & ~255);
+    return (int)std::max(64ll, std::min(2048ll, (1ll << 30) / per));
+}
 __global__ __launch_bounds__(kExactBlock) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
                                                          const double* __restrict__ qp, const double* __restrict__ qn, int qs,
                                                          const int* __restrict__ qpixel, const int* __restrict__ qsample,
                                                          const uint64_t* __restrict__ qnode,
                                                          const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                          int* __restrict__ pick_out, int* __restrict__ count_out,
-                                                         unsigned long long* stats, double* __restrict__ scratch) {
-    const int lane = threadIdx.x & 63;
-    const int waves = gridDim.x * (kExactBlock / 64);
-    const int gw = blockIdx.x * (kExactBlock / 64) + (threadIdx.x >> 6);
-    const int nlp = (S.NL + 63) & ~63;
-    double* wsc = scratch + (size_t)gw * nlp;                  // candidates' weights, then running sums
-    int* lst = reinterpret_cast<int*>(scratch + (size_t)waves * nlp) + (size_t)gw * nlp;  // candidate list
+                                                         unsigned long long* stats, double* __restrict__ scratch,
+                                                         const uint64_t* __restrict__ masks, int nmask, int nchunks) {
+    __shared__ int wcnt[kExactBlock / 64];
+    __shared__ int nsurv;
+    __shared__ double cw[kExactChunk];
+    __shared__ double wtot;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nlp = (S.NL + 255) & ~255;
+    double* wsc = scratch + (size_t)blockIdx.x * nlp;  // candidates' weights, then running sums
+    int* lst = reinterpret_cast<int*>(scratch + (size_t)gridDim.x * nlp) + (size_t)blockIdx.x * nlp;  // candidate list
     const int cnt = list[0];
-    if (gw == 0 && lane == 0 && stats && cnt) atomicAdd(stats + 10, (unsigned long long)cnt);
-    for (int j = gw; j < cnt; j += waves) {
+    if (blockIdx.x == 0 && tid == 0 && stats && cnt) atomicAdd(stats + 10, (unsigned long long)cnt);
+    for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
         const int node = list[kExactHead + j];
         const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
         const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
+        const uint64_t* mrow = masks && node < nmask ? masks + (size_t)node * mask_stride(nchunks) : nullptr;
         int ncand = 0;
-        for (int c = 0; c < S.NL; c += 64) {  // cheap stages, candidates compacted in index order
-            const int li = c + lane;
+        for (int c = 0; c < S.NL; c += kExactBlock) {  // cheap stages, candidates compacted in index order
+            const int li = c + tid;
             bool cand = false;
             if (li < S.NL) {
-                const double4 ln = S.lt_n[li];
-                cand = light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                         mk3(ln.x, ln.y, ln.z), x1, nn) == 0;
+                if (mrow) {
+                    cand = (mrow[li >> 6] >> (li & 63)) & 1;
+                } else {
+                    const double4 ln = S.lt_n[li];
+                    cand = light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                             mk3(ln.x, ln.y, ln.z), x1, nn) == 0;
+                }
             }
             const uint64_t m = __ballot(cand);
-            if (cand) lst[ncand + lane_rank(m)] = li;
-            ncand += __popcll(m);
+            if (lane == 0) wcnt[wv] = __popcll(m);
+            __syncthreads();
+            int off = ncand, tot = ncand;
+#pragma unroll
+            for (int w = 0; w < kExactBlock / 64; w++) {
+                off += w < wv ? wcnt[w] : 0;
+                tot += wcnt[w];
+            }
+            if (cand) lst[off + lane_rank(m)] = li;
+            ncand = tot;
+            __syncthreads();
         }
-        wave_lds_sync();
-        for (int k0 = 0; k0 < ncand; k0 += 64) {  // the literal full stage, 64 candidates at a time
-            const int k = k0 + lane;
-            if (k < ncand) {
-                const int li = lst[k];
-                const double4 ln = S.lt_n[li];
-                SphTri o;
-                const int st = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                               mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
-                wsc[k] = st == 0 ? o.w : -1.0;
+        if (tid == 0) nsurv = 0;
+        int mysurv = 0;
+        for (int k = tid; k < ncand; k += kExactBlock) {  // the literal full stage
+            const int li = lst[k];
+            const double4 ln = S.lt_n[li];
+            SphTri o;
+            const int st = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                           mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
+            wsc[k] = st == 0 ? o.w : -1.0;
+            mysurv += st == 0;
+        }
+        __syncthreads();
+        if (mysurv) atomicAdd(&nsurv, mysurv);
+        // the running sum, in the reference's order, one chunk at a time through LDS
+        double run = 0;  // thread 0
+        for (int k0 = 0; k0 < ncand; k0 += kExactChunk) {
+            const int m = min(kExactChunk, ncand - k0);
+            for (int k = tid; k < m; k += kExactBlock) cw[k] = wsc[k0 + k];
+            __syncthreads();
+            if (tid == 0) {
+                for (int k = 0; k < m; k += 8) {
+                    double w8[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) w8[q] = k + q < m ? cw[k + q] : -1.0;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        if (w8[q] >= 0.0) run += w8[q];
+                        w8[q] = w8[q] >= 0.0 ? run : -1.0;  // running sum after this survivor, -1 if culled
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (k + q < m) cw[k + q] = w8[q];
+                }
+            }
+            __syncthreads();
+            for (int k = tid; k < m; k += kExactBlock) wsc[k0 + k] = cw[k];
+            __syncthreads();
+        }
+        if (tid == 0) wtot = run;
+        __syncthreads();
+        if (wv == 0) {
+            const double W = wtot;
+            int pick = -1;
+            if (!(fabs(W) < MCPT_EPS)) {
+                const double u = u_override ? u_override[node]
+                                            : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+                const double target = u * W;
+                int found = -1, last = -1;
+                for (int k0 = 0; k0 < ncand && found < 0; k0 += 64) {
+                    const bool in = k0 + lane < ncand;
+                    const double rv = in ? wsc[k0 + lane] : -1.0;
+                    const uint64_t hm = __ballot(rv >= 0.0 && rv >= target);
+                    const uint64_t sm = __ballot(rv >= 0.0);
+                    if (hm) found = k0 + __ffsll((unsigned long long)hm) - 1;
+                    if (sm) last = k0 + 63 - __clzll((long long)sm);
+                }
+                const int at = found >= 0 ? found : last;
+                if (at >= 0) pick = lst[at];
+            }
+            if (lane == 0) {
+                wsum_out[node] = W;
+                pick_out[node] = pick;
+                if (count_out) count_out[node] = nsurv;
             }
         }
-        wave_lds_sync();
-        double run = 0;  // the reference's weights_sum, in its order
-        int surv = 0;
-        for (int k0 = 0; k0 < ncand; k0 += 64) {
-            const bool in = k0 + lane < ncand;
-            const double wv = in ? wsc[k0 + lane] : -1.0;
-            const uint64_t sm = __ballot(in && wv >= 0.0);
-            surv += __popcll(sm);
-            double mine = -1.0;
-            // the chunk's survivors in order: each weight read into SGPRs (v_readlane) and added by every
-            // lane to the same running sum, so the chain is one dependent v_add_f64 per survivor
-            for (uint64_t m = sm; m; m &= m - 1) {
-                const int q = __ffsll((unsigned long long)m) - 1;
-                const unsigned long long b = __double_as_longlong(wv);
-                const double wq = __longlong_as_double(
-                    ((long long)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), q) << 32) |
-                    (unsigned)__builtin_amdgcn_readlane((int)b, q));
-                run += wq;
-                mine = lane == q ? run : mine;
-            }
-            if (in) wsc[k0 + lane] = mine;  // running sum after this survivor, -1 if culled
-        }
-        wave_lds_sync();
-        int pick = -1;
-        if (!(fabs(run) < MCPT_EPS)) {
-            const double u = u_override ? u_override[node]
-                                        : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-            const double target = u * run;
-            int found = -1, last = -1;
-            for (int k0 = 0; k0 < ncand && found < 0; k0 += 64) {
-                const bool in = k0 + lane < ncand;
-                const double rv = in ? wsc[k0 + lane] : -1.0;
-                const uint64_t hm = __ballot(rv >= 0.0 && rv >= target);
-                const uint64_t sm = __ballot(rv >= 0.0);
-                if (hm) found = k0 + __ffsll((unsigned long long)hm) - 1;
-                if (sm) last = k0 + 63 - __clzll((long long)sm);
-            }
-            const int at = found >= 0 ? found : last;
-            if (at >= 0) pick = lst[at];
-        }
-        if (lane == 0) {
-            wsum_out[node] = run;
-            pick_out[node] = pick;
-            if (count_out) count_out[node] = surv;
-        }
-        wave_lds_sync();
+        __syncthreads();  // the slab and LDS are reused by the next node
     }
 }
 // diagnostics (mcpt_debug_light_literal): the literal chain's intermediates for every light at one point,
@@ -2240,7 +2298,7 @@ __global__ void k_light_literal(DScene S, d3 x1, d3 nn, double* out) {
     o[19] = dot(B, C);
 }
 // scratch doubles k_prep_exact needs (per wave: weights + list)
-inline size_t exact_scratch_doubles(int NL) { return (size_t)kExactBlocks * (kExactBlock / 64) * 2 * (size_t)((NL + 63) & ~63); }
+inline size_t exact_scratch_doubles(int NL) { return (size_t)exact_blocks(NL) * 2 * (size_t)((NL + 255) & ~255); }
 
 // ---- MIS node split into three kernels (ray generation / traversal / combination) -------------
 // (one MIS node per lane with three inlined traversals measured 152 VGPRs, 3 waves/SIMD.)  Split,
@@ -3597,6 +3655,11 @@ constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 #define MCPT_PK2_F32_WAVES 5
 #endif
 constexpr int kPk2F32Waves = MCPT_PK2_F32_WAVES;
+// whether launch_prep(-1, ...) with these masks takes the split form (variant 17), which writes every
+// node's candidate words (k_prep_exact reads them instead of redoing the cheap stages)
+inline bool prep_writes_masks(const DScene& d, const uint64_t* masks) {
+    return masks && d.NL > kSmallNL && d.NL <= 65535 && 4 * prep_list_wave_bytes(prep_chunks(d.NL)) <= kPrepListMaxLds;
+}
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn, int qs,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
@@ -3622,7 +3685,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     if (variant == 0) {
         hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qs, qpixel,
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, work, cache.slack, cache.exact_off,
-                           cache.exact_counts);
+                           cache.exact_counts, cache.maybe);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
         if (count_c1 || !stats)
             hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
@@ -3809,13 +3872,14 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // precision makes no exactness claim, and the small-table prep (k_prep_lane) is exact by construction
     // MCPT_EXACT_PICK=0 builds the pre-round-3 prep (VOS weights' own pick) for the cost A/B only
     const bool exact_pick = MCPT_EXACT_PICK && needs_prep && !fp32 && D.d.NL > kSmallNL;
-    int* exact_list = nullptr;
+    int *exact_list = nullptr, *maybe_list = nullptr;  // [0] count, entries from kExactHead
     double *exact_scr = nullptr, *slack = nullptr;
     if (exact_pick) {
-        if ((rc = ensure(D.exact, 4ull * ((size_t)cap + kExactHead))) ||
+        if ((rc = ensure(D.exact, 8ull * ((size_t)cap + kExactHead))) ||
             (rc = ensure(D.exact_scr, 8 * exact_scratch_doubles(D.d.NL))) || (rc = ensure(D.slack, 8ull * cap)))
             return rc;
         exact_list = (int*)D.exact.p;
+        maybe_list = exact_list + cap + kExactHead;
         exact_scr = (double*)D.exact_scr.p;
         slack = (double*)D.slack.p;
     }
@@ -3980,11 +4044,17 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         bool timed = false;
         if (needs_prep) {
             PrepCache cx{};  // the children's full prep: no cache, the picks' slack
+            int nmask = 0;   // nodes [0, nmask) have candidate words (k_prep_exact)
             cx.slack = slack;
-            if (exact_pick) HIP_OK(hipMemsetAsync(exact_list, 0, 4, st));
+            cx.maybe = maybe_list;
+            if (exact_pick) {
+                HIP_OK(hipMemsetAsync(exact_list, 0, 4, st));
+                HIP_OK(hipMemsetAsync(maybe_list, 0, 4, st));
+            }
             if (pc.use) {  // children: full prep; roots: pick from the root-point cache
                 const int nc = (int)n_children, nr = ni - nc;
                 if (nc > 0) {
+                    nmask = prep_writes_masks(D.d, masks) ? nc : 0;
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                        cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
@@ -3994,7 +4064,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 }
                 if (nr > 0) {
                     PrepCache pr = pc;
-                    pr.slack = slack;
+                    pr.exact = exact_list;
                     pr.exact_off = nc;
                     const int blocks = std::max(1, std::min((nr + 4 * kPickNodes - 1) / (4 * kPickNodes), 8192));
                     hipLaunchKernelGGL(k_prep_pick, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
@@ -4003,6 +4073,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     HIP_OK(hipGetLastError());
                 }
             } else {
+                nmask = prep_writes_masks(D.d, masks) ? ni : 0;
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                    cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
@@ -4012,11 +4083,11 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             }
             prep_launches += timed;
             if (exact_pick) {  // the band's nodes: the reference's literal prep and pick
-                hipLaunchKernelGGL(k_prep_band, dim3((ni + 255) / 256), dim3(256), 0, st, D.d, ni, slack, cur->p, cur->cap, masks,
-                                   nchunks, exact_list);
-                hipLaunchKernelGGL(k_prep_exact, dim3(kExactBlocks), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
+                hipLaunchKernelGGL(k_prep_band, dim3(kBandBlocks), dim3(256), 0, st, D.d, maybe_list, slack, cur->p, cur->cap,
+                                   masks, nchunks, exact_list, P.stats);
+                hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D.d.NL)), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
                                    cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
-                                   nullptr, P.stats, exact_scr);
+                                   nullptr, P.stats, exact_scr, masks, nmask, nchunks);
                 HIP_OK(hipGetLastError());
             }
         }
@@ -4138,6 +4209,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->prep_seconds = prep_ms * 1e-3;
         stats->prep_launches = prep_launches;
         stats->prep_exact_nodes = hs[10];
+        stats->prep_band_nodes = hs[11];
         stats->cache_build_seconds = cache_ms * 1e-3;
     }
     return MCPT_OK;
@@ -4222,6 +4294,7 @@ void add_stats(mcpt_stats& t, const mcpt_stats& x) {
     t.node_visits += x.node_visits;
     t.tri_tests += x.tri_tests;
     t.prep_exact_nodes += x.prep_exact_nodes;
+    t.prep_band_nodes += x.prep_band_nodes;
     t.cache_build_seconds += x.cache_build_seconds;
 }
 
@@ -4489,10 +4562,11 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
     HIP_OK(hipMalloc(&dc, 4ull * n));
     HIP_OK(hipMalloc(&dk, 4ull * n));
     if (exact) {
-        HIP_OK(hipMalloc(&dl, 4ull * (n + kExactHead)));
+        HIP_OK(hipMalloc(&dl, 8ull * (n + kExactHead)));  // exact list, then the band's candidate list
         HIP_OK(hipMalloc(&ds, 8 * exact_scratch_doubles(D->d.NL)));
         HIP_OK(hipMalloc(&dsl, 8ull * n));
         HIP_OK(hipMemset(dl, 0, 4));
+        HIP_OK(hipMemset((int*)dl + n + kExactHead, 0, 4));
     }
     {  // the kernels read node coordinates component-major (x[n], y[n], z[n], like the wavefront queue)
         const std::vector<double> px = soa3(x1, n), pn = soa3(nrm, n);
@@ -4510,17 +4584,21 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
         PrepCache cx{};
         cx.slack = (double*)dsl;
         cx.exact_counts = 1;
+        cx.maybe = exact ? (int*)dl + n + kExactHead : nullptr;
         HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream,
                            cx, (uint64_t*)dm));
         if (exact)
-            hipLaunchKernelGGL(k_prep_band, dim3((n + 255) / 256), dim3(256), 0, D->stream, D->d, n, (const double*)dsl,
-                               (const double*)dp, n, (const uint64_t*)dm, prep_chunks(D->d.NL), (int*)dl);
+            hipLaunchKernelGGL(k_prep_band, dim3(kBandBlocks), dim3(256), 0, D->stream, D->d, (const int*)cx.maybe,
+                               (const double*)dsl, (const double*)dp, n, (const uint64_t*)dm, prep_chunks(D->d.NL), (int*)dl,
+                               nullptr);
     }
     if (exact)
-        hipLaunchKernelGGL(k_prep_exact, dim3(kExactBlocks), dim3(kExactBlock), 0, D->stream, D->d, (uint64_t)0,
+        hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D->d.NL)), dim3(kExactBlock), 0, D->stream, D->d, (uint64_t)0,
                            (const int*)dl, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
-                           (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (double*)ds);
+                           (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (double*)ds,
+                           all_exact ? nullptr : (const uint64_t*)dm, prep_writes_masks(D->d, (const uint64_t*)dm) ? n : 0,
+                           prep_chunks(D->d.NL));
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));

@@ -165,7 +165,9 @@ def test_light_prep_exact_fallback_is_the_reference(scene, oscene):
     cumulative boundary.  weights_sum is bit-identical wherever glibc's acos (the oracle's) is correctly
     rounded on all of the point's survivors: glibc rounds ~5e-4 of arguments the other way
     (tools/acos_cr_check.py), so ~0.1% of the light weights differ in their last bits and ~20% of the
-    points' sums (~900 survivors each) in their last bits (asserted <= 1e-12 relative)."""
+    points' sums (~900 survivors each) slightly: sA = alpha + beta + gamma - pi cancels, so one angle's
+    ulp (4.4e-16) moves a small triangle's weight by 4.4e-16 / sA relative (measured <= 4e-12 on the sums;
+    asserted <= 1e-10)."""
     pin, pout = np.load(GOLDEN / "prep_in.npy"), np.load(GOLDEN / "prep_out.npy")
     u = np.array([rng.counter_uniform(SEED, k, 0, 1, 1) for k in range(len(pin))])
     ws, cnt, pick = mcpt.debug_light_prep_exact(scene, pin[:, :3], pin[:, 3:6], u)
@@ -173,7 +175,7 @@ def test_light_prep_exact_fallback_is_the_reference(scene, oscene):
     rel = np.abs(ws - pout[:, 0]) / np.maximum(np.abs(pout[:, 0]), 1e-300)
     print("exact fallback: weights_sum bit-identical on %d/%d points, max rel diff of the rest %.2e" % (
         same.sum(), len(pin), rel.max()))
-    assert same.mean() >= 0.7 and rel.max() <= 1e-12, (np.nonzero(~same)[0][:10], rel[~same][:5])
+    assert same.mean() >= 0.7 and rel.max() <= 1e-10, (np.nonzero(~same)[0][:10], rel[~same][:5])
     assert np.array_equal(cnt, pout[:, 1].astype(np.int32))
     opick = np.array([int(oscene.light_sample_u(pin[k, :3], pin[k, 3:6], u[k], 0.5, 0.5)[0]) for k in range(len(pin))])
     assert np.array_equal(pick, opick)

@@ -111,6 +111,7 @@ def test_device_buffer_must_be_device_memory(scene):
 _WORKER = r"""
 import os, sys
 sys.path.insert(0, os.environ["MCPT_ROOT"])
+sys.path.insert(0, os.path.join(os.environ["MCPT_ROOT"], "tests"))
 import numpy as np
 import torch
 import torch.distributed as dist
