@@ -603,6 +603,9 @@ struct Queue {
 // k_rays_persistent reads the 64-B compressed nodes (BvhNode4Q): Cornell-1M traversal -6%; the
 // L2-resident kernels keep the 128-B fp32 nodes (their decode VALU costs more than the lines save:
 // Veach MIS -1.5%, BRDF -5%; profiles/round2b_ab_bvh_quant.txt)
+#ifndef MCPT_BAND_DIAG
+#define MCPT_BAND_DIAG 0
+#endif
 #ifndef MCPT_EXACT_PICK
 #define MCPT_EXACT_PICK 1
 #endif
@@ -1082,9 +1085,17 @@ __device__ inline double band_base(const DScene& S, d3 x1, const uint64_t* mrow,
 // distance of target = u W from the boundaries around the picked candidate (lane pl of the batch whose
 // exclusive prefix is base; sc = this lane's inclusive in-batch scan): below, the cumulative weight
 // before it (none if that is 0: no earlier weight); above, the cumulative weight including it
+// (pl is wave-uniform -- it comes from a ballot -- so the two values are read with v_readlane into
+// SGPRs rather than an LDS permute)
+__device__ inline double readlane_f64(double v, int l) {
+    const unsigned long long b = __double_as_longlong(v);
+    return __longlong_as_double(((long long)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l) << 32) |
+                                (unsigned)__builtin_amdgcn_readlane((int)b, l));
+}
 __device__ inline double pick_margin(double base, double sc, int pl, double target) {
-    const double c_hi = base + __shfl(sc, pl);
-    const double c_lo = pl > 0 ? base + __shfl(sc, pl > 0 ? pl - 1 : 0) : base;
+    const int l = __builtin_amdgcn_readfirstlane(pl);
+    const double c_hi = base + readlane_f64(sc, l);
+    const double c_lo = l > 0 ? base + readlane_f64(sc, l - 1) : base;
     const double m_lo = c_lo == 0.0 ? INFINITY : target - c_lo;
     return fmin(m_lo, c_hi - target);
 }
@@ -2133,138 +2144,147 @@ __global__ __launch_bounds__(256) void k_prep_band(DScene S, const int* __restri
 // Exact fallback of the light prep's pick.  For the nodes the prep kernels put on
 // the exact list (list[kExactHead + j] = node index, count in list[0]): the reference's own arithmetic
 // end to end -- the cheap culls (light_cheap_stage, Mylight.cpp:340-357; for a node whose candidate
-// words k_prep_cull_lanes wrote, those words: the same decisions), the literal full stage
-// (light_tri_stage: sqrt / division unit vectors, acos_cr vertex angles, alpha + beta + gamma - pi,
-// Mylight.cpp:360-413), weights_sum summed candidate by candidate in index order (Mylight.cpp:415-418)
-// and the pick "first survivor whose running sum >= u weights_sum, else the last survivor" -- so
-// weights_sum, the survivor count and the pick are the oracle's bit for bit (acos_cr: correctly
-// rounded, so up to glibc's acos on the ~5e-4 of arguments it rounds the other way).
-// One workgroup (4 waves) per node: the candidate list and the literal stage run over the workgroup's
-// 256 lanes, the candidate list and weights go to the workgroup's scratch slab; the running sum, the
-// one sequential part, runs on a single lane over kExactChunk weights at a time staged in LDS (eight
-// loads in flight ahead of the chain of dependent adds), and the pick is a ballot search over the
-// stored running sums.
+// words k_prep_cull_lanes wrote, those words, and for a root its pixel's cached candidate list: the same
+// decisions), the literal full stage (light_tri_stage: sqrt / division unit vectors, acos_cr vertex
+// angles, alpha + beta + gamma - pi, Mylight.cpp:360-413), weights_sum summed candidate by candidate in
+// index order (Mylight.cpp:415-418) and the pick "first survivor whose running sum >= u weights_sum,
+// else the last survivor" -- so weights_sum, the survivor count and the pick are the oracle's bit for
+// bit (acos_cr: correctly rounded, so up to glibc's acos on the ~5e-4 of arguments it rounds the other
+// way).
+// One wave per node, with enough waves for 4 per SIMD (a launch holds ~10^3-10^4 listed nodes; with one
+// wave per SIMD the serial running sum ran at the latency of every instruction -- ~100 us per node).
+// The running sum is the one sequential part: each 64-candidate chunk's weights sit one per lane and
+// are added in order through v_readlane (culled candidates contribute +0, which leaves an fp64 sum
+// unchanged), fully unrolled, lane q keeping the sum after candidate q; the pick is a ballot search
+// over the stored running sums.
 constexpr int kExactBlock = 256;
-constexpr int kExactChunk = 1024;
-inline int exact_blocks(int NL) {  // grid-stride; scratch (2 x 8 B per light per workgroup) kept <= 1 GiB
-    const long long per = 16ll * ((NL + 255) & ~255);
-    return (int)std::max(64ll, std::min(2048ll, (1ll << 30) / per));
+inline int exact_waves(int NL) {  // grid-stride; scratch (2 x 8 B per light per wave) kept <= 1 GiB
+    const long long per = 16ll * ((NL + 63) & ~63);
+    return (int)std::max(256ll, std::min(8192ll, (1ll << 30) / per)) & ~3;
 }
-__global__ __launch_bounds__(kExactBlock) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
+inline int exact_blocks(int NL) { return exact_waves(NL) / (kExactBlock / 64); }
+__global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
                                                          const double* __restrict__ qp, const double* __restrict__ qn, int qs,
                                                          const int* __restrict__ qpixel, const int* __restrict__ qsample,
                                                          const uint64_t* __restrict__ qnode,
                                                          const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                          int* __restrict__ pick_out, int* __restrict__ count_out,
                                                          unsigned long long* stats, double* __restrict__ scratch,
-                                                         const uint64_t* __restrict__ masks, int nmask, int nchunks) {
-    __shared__ int wcnt[kExactBlock / 64];
-    __shared__ int nsurv;
-    __shared__ double cw[kExactChunk];
-    __shared__ double wtot;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int nlp = (S.NL + 255) & ~255;
-    double* wsc = scratch + (size_t)blockIdx.x * nlp;  // candidates' weights, then running sums
-    int* lst = reinterpret_cast<int*>(scratch + (size_t)gridDim.x * nlp) + (size_t)blockIdx.x * nlp;  // candidate list
+                                                         const uint64_t* __restrict__ masks, int nmask, int nchunks,
+                                                         const unsigned short* __restrict__ clst, const int4* __restrict__ cinfo,
+                                                         int lstride, int root_off) {
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * (kExactBlock / 64);
+    const int gw = blockIdx.x * (kExactBlock / 64) + (threadIdx.x >> 6);
+    const int nlp = (S.NL + 63) & ~63;
+    double* wsc = scratch + (size_t)gw * nlp;                  // candidates' weights, then running sums
+    int* lst = reinterpret_cast<int*>(scratch + (size_t)waves * nlp) + (size_t)gw * nlp;  // candidate list
     const int cnt = list[0];
-    if (blockIdx.x == 0 && tid == 0 && stats && cnt) atomicAdd(stats + 10, (unsigned long long)cnt);
-    for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+    if (gw == 0 && lane == 0 && stats && cnt) atomicAdd(stats + 10, (unsigned long long)cnt);
+    for (int j = gw; j < cnt; j += waves) {
         const int node = list[kExactHead + j];
         const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
         const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
-        const uint64_t* mrow = masks && node < nmask ? masks + (size_t)node * mask_stride(nchunks) : nullptr;
+#if MCPT_BAND_DIAG
+        const unsigned long long t0 = wall_clock64();
+#endif
         int ncand = 0;
-        for (int c = 0; c < S.NL; c += kExactBlock) {  // cheap stages, candidates compacted in index order
-            const int li = c + tid;
-            bool cand = false;
-            if (li < S.NL) {
-                if (mrow) {
-                    cand = (mrow[li >> 6] >> (li & 63)) & 1;
-                } else {
+        if (clst && node >= root_off) {  // a root: its pixel's cached candidate list
+            const int px = qpixel[node];
+            ncand = cinfo[px].y;
+            for (int k = lane; k < ncand; k += 64) lst[k] = clst[(size_t)px * lstride + k];
+        } else if (masks && node < nmask) {  // the node's candidate words
+            const uint64_t* mrow = masks + (size_t)node * mask_stride(nchunks);
+            for (int c = 0; c < nchunks; c++) {
+                const uint64_t m = mrow[c];
+                if ((m >> lane) & 1) lst[ncand + __popcll(m & ((1ull << lane) - 1))] = 64 * c + lane;
+                ncand += __popcll(m);
+            }
+        } else {
+            for (int c = 0; c < S.NL; c += 64) {  // cheap stages, candidates compacted in index order
+                const int li = c + lane;
+                bool cand = false;
+                if (li < S.NL) {
                     const double4 ln = S.lt_n[li];
                     cand = light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
                                              mk3(ln.x, ln.y, ln.z), x1, nn) == 0;
                 }
-            }
-            const uint64_t m = __ballot(cand);
-            if (lane == 0) wcnt[wv] = __popcll(m);
-            __syncthreads();
-            int off = ncand, tot = ncand;
-#pragma unroll
-            for (int w = 0; w < kExactBlock / 64; w++) {
-                off += w < wv ? wcnt[w] : 0;
-                tot += wcnt[w];
-            }
-            if (cand) lst[off + lane_rank(m)] = li;
-            ncand = tot;
-            __syncthreads();
-        }
-        if (tid == 0) nsurv = 0;
-        int mysurv = 0;
-        for (int k = tid; k < ncand; k += kExactBlock) {  // the literal full stage
-            const int li = lst[k];
-            const double4 ln = S.lt_n[li];
-            SphTri o;
-            const int st = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                           mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
-            wsc[k] = st == 0 ? o.w : -1.0;
-            mysurv += st == 0;
-        }
-        __syncthreads();
-        if (mysurv) atomicAdd(&nsurv, mysurv);
-        // the running sum, in the reference's order, one chunk at a time through LDS
-        double run = 0;  // thread 0
-        for (int k0 = 0; k0 < ncand; k0 += kExactChunk) {
-            const int m = min(kExactChunk, ncand - k0);
-            for (int k = tid; k < m; k += kExactBlock) cw[k] = wsc[k0 + k];
-            __syncthreads();
-            if (tid == 0) {
-                for (int k = 0; k < m; k += 8) {
-                    double w8[8];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) w8[q] = k + q < m ? cw[k + q] : -1.0;
-#pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        if (w8[q] >= 0.0) run += w8[q];
-                        w8[q] = w8[q] >= 0.0 ? run : -1.0;  // running sum after this survivor, -1 if culled
-                    }
-#pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        if (k + q < m) cw[k + q] = w8[q];
-                }
-            }
-            __syncthreads();
-            for (int k = tid; k < m; k += kExactBlock) wsc[k0 + k] = cw[k];
-            __syncthreads();
-        }
-        if (tid == 0) wtot = run;
-        __syncthreads();
-        if (wv == 0) {
-            const double W = wtot;
-            int pick = -1;
-            if (!(fabs(W) < MCPT_EPS)) {
-                const double u = u_override ? u_override[node]
-                                            : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-                const double target = u * W;
-                int found = -1, last = -1;
-                for (int k0 = 0; k0 < ncand && found < 0; k0 += 64) {
-                    const bool in = k0 + lane < ncand;
-                    const double rv = in ? wsc[k0 + lane] : -1.0;
-                    const uint64_t hm = __ballot(rv >= 0.0 && rv >= target);
-                    const uint64_t sm = __ballot(rv >= 0.0);
-                    if (hm) found = k0 + __ffsll((unsigned long long)hm) - 1;
-                    if (sm) last = k0 + 63 - __clzll((long long)sm);
-                }
-                const int at = found >= 0 ? found : last;
-                if (at >= 0) pick = lst[at];
-            }
-            if (lane == 0) {
-                wsum_out[node] = W;
-                pick_out[node] = pick;
-                if (count_out) count_out[node] = nsurv;
+                const uint64_t m = __ballot(cand);
+                if (cand) lst[ncand + lane_rank(m)] = li;
+                ncand += __popcll(m);
             }
         }
-        __syncthreads();  // the slab and LDS are reused by the next node
+        wave_lds_sync();
+#if MCPT_BAND_DIAG
+        const unsigned long long t1 = wall_clock64();
+#endif
+        for (int k0 = 0; k0 < ncand; k0 += 64) {  // the literal full stage, 64 candidates at a time
+            const int k = k0 + lane;
+            if (k < ncand) {
+                const int li = lst[k];
+                const double4 ln = S.lt_n[li];
+                SphTri o;
+                const int st = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                               mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
+                wsc[k] = st == 0 ? o.w : -1.0;
+            }
+        }
+        wave_lds_sync();
+#if MCPT_BAND_DIAG
+        const unsigned long long t2 = wall_clock64();
+#endif
+        double run = 0;  // the reference's weights_sum, in its order (wave-uniform)
+        int surv = 0;
+        for (int k0 = 0; k0 < ncand; k0 += 64) {
+            const bool in = k0 + lane < ncand;
+            const double w = in ? wsc[k0 + lane] : -1.0;
+            const bool ok = w >= 0.0;
+            surv += __popcll(__ballot(ok));
+            const double wz = ok ? w : 0.0;
+            double mine = 0.0;
+#pragma unroll 8
+            for (int q = 0; q < 64; q++) {
+                run += readlane_f64(wz, q);
+                mine = lane == q ? run : mine;
+            }
+            if (in) wsc[k0 + lane] = ok ? mine : -1.0;  // running sum after this survivor, -1 if culled
+        }
+        wave_lds_sync();
+#if MCPT_BAND_DIAG
+        const unsigned long long t3 = wall_clock64();
+#endif
+        int pick = -1;
+        if (!(fabs(run) < MCPT_EPS)) {
+            const double u = u_override ? u_override[node]
+                                        : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
+            const double target = u * run;
+            int found = -1, last = -1;
+            for (int k0 = 0; k0 < ncand && found < 0; k0 += 64) {
+                const bool in = k0 + lane < ncand;
+                const double rv = in ? wsc[k0 + lane] : -1.0;
+                const uint64_t hm = __ballot(rv >= 0.0 && rv >= target);
+                const uint64_t sm = __ballot(rv >= 0.0);
+                if (hm) found = k0 + __ffsll((unsigned long long)hm) - 1;
+                if (sm) last = k0 + 63 - __clzll((long long)sm);
+            }
+            const int at = found >= 0 ? found : last;
+            if (at >= 0) pick = lst[at];
+        }
+        if (lane == 0) {
+            wsum_out[node] = run;
+            pick_out[node] = pick;
+            if (count_out) count_out[node] = surv;
+#if MCPT_BAND_DIAG  // wall-clock ticks (100 MHz) per phase, summed over nodes: lists, literal, sum, pick
+            if (stats) {
+                const unsigned long long t4 = wall_clock64();
+                atomicAdd(stats + 12, t1 - t0);
+                atomicAdd(stats + 13, t2 - t1);
+                atomicAdd(stats + 14, t3 - t2);
+                atomicAdd(stats + 15, t4 - t3);
+            }
+#endif
+        }
+        wave_lds_sync();
     }
 }
 // diagnostics (mcpt_debug_light_literal): the literal chain's intermediates for every light at one point,
@@ -2298,7 +2318,7 @@ __global__ void k_light_literal(DScene S, d3 x1, d3 nn, double* out) {
     o[19] = dot(B, C);
 }
 // scratch doubles k_prep_exact needs (per wave: weights + list)
-inline size_t exact_scratch_doubles(int NL) { return (size_t)exact_blocks(NL) * 2 * (size_t)((NL + 255) & ~255); }
+inline size_t exact_scratch_doubles(int NL) { return (size_t)exact_waves(NL) * 2 * (size_t)((NL + 63) & ~63); }
 
 // ---- MIS node split into three kernels (ray generation / traversal / combination) -------------
 // (one MIS node per lane with three inlined traversals measured 152 VGPRs, 3 waves/SIMD.)  Split,
@@ -4045,6 +4065,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (needs_prep) {
             PrepCache cx{};  // the children's full prep: no cache, the picks' slack
             int nmask = 0;   // nodes [0, nmask) have candidate words (k_prep_exact)
+            int root_off = INT_MAX;  // nodes [root_off, ni) are roots with a cached candidate list
             cx.slack = slack;
             cx.maybe = maybe_list;
             if (exact_pick) {
@@ -4063,6 +4084,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     timed = true;
                 }
                 if (nr > 0) {
+                    root_off = nc;
                     PrepCache pr = pc;
                     pr.exact = exact_list;
                     pr.exact_off = nc;
@@ -4087,7 +4109,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                                    masks, nchunks, exact_list, P.stats);
                 hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D.d.NL)), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
                                    cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
-                                   nullptr, P.stats, exact_scr, masks, nmask, nchunks);
+                                   nullptr, P.stats, exact_scr, masks, nmask, nchunks, pc.use ? pc.lst : nullptr,
+                                   pc.use ? pc.info : nullptr, pc.lstride, root_off);
                 HIP_OK(hipGetLastError());
             }
         }
@@ -4210,6 +4233,10 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->prep_launches = prep_launches;
         stats->prep_exact_nodes = hs[10];
         stats->prep_band_nodes = hs[11];
+#if MCPT_BAND_DIAG
+        fprintf(stderr, "exact diag (10 ns ticks summed over nodes): lists %llu literal %llu sum %llu pick %llu\n", hs[12],
+                hs[13], hs[14], hs[15]);
+#endif
         stats->cache_build_seconds = cache_ms * 1e-3;
     }
     return MCPT_OK;
@@ -4598,7 +4625,7 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
                            (const int*)dl, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (double*)ds,
                            all_exact ? nullptr : (const uint64_t*)dm, prep_writes_masks(D->d, (const uint64_t*)dm) ? n : 0,
-                           prep_chunks(D->d.NL));
+                           prep_chunks(D->d.NL), nullptr, nullptr, 0, INT_MAX);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
