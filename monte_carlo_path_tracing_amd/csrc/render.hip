@@ -164,7 +164,7 @@ constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB p
 #define MCPT_LB_CULL 1
 #endif
 #ifndef MCPT_LB_PICK
-#define MCPT_LB_PICK 1
+#define MCPT_LB_PICK 7  // 72 VGPRs: k_prep_pick 427 -> 396 ms per profile run (round 3, same box)
 #endif
 #ifndef MCPT_LB_GEN
 #define MCPT_LB_GEN 1
@@ -307,6 +307,10 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 // they aim at, so the deferred fp64 slots run in nearly every wave), but with the light-ray seed
 // (tlimit known from the start, so the fp32 test also rejects triangles behind the light)
 // 4.04 -> 3.95 ms, shade-area +1.3%
+// MCPT_SLAB_NEARFAR=0: the round-2 slab test (A/B only)
+#ifndef MCPT_SLAB_NEARFAR
+#define MCPT_SLAB_NEARFAR 0
+#endif
 #ifndef MCPT_FILTER_MIS
 #define MCPT_FILTER_MIS 1
 #endif
@@ -356,7 +360,8 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     // form computes, and the per-node min/max pairs go away.  Empty child slots (lo = FLT_MAX,
     // hi = -FLT_MAX, collapse_bvh4) then give t0 >= FLT_MAX > t1 for any |inverse| >= 1 (a unit
     // direction's), so they miss without a child-code test.
-    const unsigned nx = ix < 0 ? 48u : 0u, ny = iy < 0 ? 64u : 16u, nz = iz < 0 ? 80u : 32u;
+    const unsigned nx = MCPT_SLAB_NEARFAR && ix < 0 ? 48u : 0u, ny = MCPT_SLAB_NEARFAR && iy < 0 ? 64u : 16u,
+                   nz = MCPT_SLAB_NEARFAR && iz < 0 ? 80u : 32u;
     const unsigned fx = 48u - nx, fy = 80u - ny, fz = 112u - nz;
     // tlimit0: at least the t of a triangle tri_hit accepts (or FLT_MAX) -- boxes beyond it hold no
     // closest hit
@@ -419,9 +424,18 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                 const int chs[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
+#if MCPT_SLAB_NEARFAR
                     const float t0 = fmaxf(fmaxf(fmaf(nxs[k], ix, -oix), fmaf(nys[k], iy, -oiy)), fmaxf(fmaf(nzs[k], iz, -oiz), 0.0f));
                     const float t1 = fminf(fminf(fmaf(fxs[k], ix, -oix), fmaf(fys[k], iy, -oiy)), fminf(fmaf(fzs[k], iz, -oiz), tlimit));
                     const bool h = t0 <= fmaf(t1, 1.00001f, 1e-6f);
+#else  // A/B: the round-2 form (lo / hi planes, min / max per pair, empty-slot test); nx.. = lo offsets
+                    const float tx0 = fmaf(nxs[k], ix, -oix), tx1 = fmaf(fxs[k], ix, -oix);
+                    const float ty0 = fmaf(nys[k], iy, -oiy), ty1 = fmaf(fys[k], iy, -oiy);
+                    const float tz0 = fmaf(nzs[k], iz, -oiz), tz1 = fmaf(fzs[k], iz, -oiz);
+                    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+                    const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
+#endif
                     t[k] = h ? t0 : FLT_MAX;
                     code[k] = h ? chs[k] : kDone;  // leaves come pre-packed (pack_leaf_codes)
                 }
@@ -3675,6 +3689,12 @@ constexpr int kPrepListMaxLds = 64 * 1024;  // per 4-wave block
 #define MCPT_PK2_F32_WAVES 5
 #endif
 constexpr int kPk2F32Waves = MCPT_PK2_F32_WAVES;
+// the fp64 split form's launch bound (waves/SIMD): 6 keeps it at 72 VGPRs (7 waves by registers)
+// since the exact-pick bookkeeping; 5 let it grow to 75 (same-box A/B with the pick at 7: +1.2%)
+#ifndef MCPT_PK2_WAVES
+#define MCPT_PK2_WAVES 6
+#endif
+constexpr int kPk2Waves = MCPT_PK2_WAVES;
 // whether launch_prep(-1, ...) with these masks takes the split form (variant 17), which writes every
 // node's candidate words (k_prep_exact reads them instead of redoing the cheap stages)
 inline bool prep_writes_masks(const DScene& d, const uint64_t* masks) {
@@ -3714,8 +3734,8 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
             hipLaunchKernelGGL(k_prep_cull_lanes<false>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
                                n, qp, qn, qs, masks, nchunks, stats);
         // fp32: MCPT_RENDER_PRECISION_FP32's packed-fp32 full stage (light_weight_f32x2)
-        auto kern = cache.build ? (fp32 ? k_prep_pk2<kPk2F32Waves, true, true, true> : k_prep_pk2<5, true, true, false>)
-                                : (fp32 ? k_prep_pk2<kPk2F32Waves, false, true, true> : k_prep_pk2<5, false, true, false>);
+        auto kern = cache.build ? (fp32 ? k_prep_pk2<kPk2F32Waves, true, true, true> : k_prep_pk2<kPk2Waves, true, true, false>)
+                                : (fp32 ? k_prep_pk2<kPk2F32Waves, false, true, true> : k_prep_pk2<kPk2Waves, false, true, false>);
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 4 * wb, st, d, seed, n, qp, qn, qs, qpixel, qsample, qnode, u, wsum,
                            pick, count, stats, nchunks, wb, work, cache, masks);
     } else if (cache.build) {
