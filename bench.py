@@ -282,7 +282,14 @@ def main():
     pk = pmc["kernels"]
     # bounded VALU figure from the SQ pass (tools/summarize_profiles.py): 4 x SQ_INSTS_VALU / (SIMDs x
     # cycles) -- the issue slots the kernel's VALU instructions hold (>= 4 cycles each for wave64)
-    busy = lambda *names: {n: pk[n]["valu_issue_frac"] for n in names if n in pk and "valu_issue_frac" in pk[n]}  # noqa: E731
+    def busy(*names):  # a name ending in "*>" matches any launch bound: "k_prep_pk2<*, false, true, false>"
+        out = {}
+        for n in names:
+            head, _, tail = n.partition("*")
+            for k, v in pk.items():
+                if (k == n or (tail and k.startswith(head) and k.endswith(tail))) and "valu_issue_frac" in v:
+                    out[k] = v["valu_issue_frac"]
+        return out
     dev_s = max(totals.get("seconds", 0.0), 1e-12)
     # ---- roofline of the light prep (rank 0's launches; HIP events on its stream) ----
     roof_prep = None
@@ -309,7 +316,7 @@ def main():
             "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": tsrc,
             "valu_issue_frac": busy("k_prep_cull_lanes<false>",
-                              "k_prep_pk2<5, false, true, %s>" % ("true" if args.precision == "fp32" else "false")),
+                              "k_prep_pk2<*, false, true, %s>" % ("true" if args.precision == "fp32" else "false")),
             "valu_issue_frac_source": pmc.get("source"),
             "hbm_frac_algorithmic": round(alg_gbs / HBM_PEAK_GBS, 5),
             "hbm_frac_measured": round(traffic / t_launch / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,

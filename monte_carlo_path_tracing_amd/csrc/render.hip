@@ -2205,6 +2205,9 @@ __global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_
         int ncand = 0;
         if (clst && node >= root_off) {  // a root: its pixel's cached candidate list
             const int px = qpixel[node];
+#if MCPT_BAND_DIAG  // exact roots per pixel, in the scratch's unused last quarter
+            if (lane == 0) atomicAdd(reinterpret_cast<int*>(scratch + (size_t)waves * nlp * 3 / 2) + px, 1);
+#endif
             ncand = cinfo[px].y;
             for (int k = lane; k < ncand; k += 64) lst[k] = clst[(size_t)px * lstride + k];
         } else if (masks && node < nmask) {  // the node's candidate words
@@ -3920,6 +3923,10 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             return rc;
         exact_list = (int*)D.exact.p;
         maybe_list = exact_list + cap + kExactHead;
+#if MCPT_BAND_DIAG
+        HIP_OK(hipMemset((double*)D.exact_scr.p + (size_t)exact_waves(D.d.NL) * ((D.d.NL + 63) & ~63) * 3 / 2, 0,
+                         4ull * cam->width * cam->height));
+#endif
         exact_scr = (double*)D.exact_scr.p;
         slack = (double*)D.slack.p;
     }
@@ -4256,6 +4263,15 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
 #if MCPT_BAND_DIAG
         fprintf(stderr, "exact diag (10 ns ticks summed over nodes): lists %llu literal %llu sum %llu pick %llu\n", hs[12],
                 hs[13], hs[14], hs[15]);
+        if (exact_scr) {
+            const int nlp = (D.d.NL + 63) & ~63;
+            std::vector<int> pc(npx);
+            HIP_OK(hipMemcpy(pc.data(), reinterpret_cast<int*>(exact_scr + (size_t)exact_waves(D.d.NL) * nlp * 3 / 2),
+                             4ull * npx, hipMemcpyDeviceToHost));
+            long long tot = 0, distinct = 0, mx = 0;
+            for (int v : pc) tot += v, distinct += v > 0, mx = std::max<long long>(mx, v);
+            fprintf(stderr, "exact diag: roots %lld over %lld pixels (max %lld per pixel)\n", tot, distinct, mx);
+        }
 #endif
         stats->cache_build_seconds = cache_ms * 1e-3;
     }
