@@ -2177,6 +2177,17 @@ inline int exact_waves(int NL) {  // grid-stride; scratch (2 x 8 B per light per
     return (int)std::max(256ll, std::min(8192ll, (1ll << 30) / per)) & ~3;
 }
 inline int exact_blocks(int NL) { return exact_waves(NL) / (kExactBlock / 64); }
+// Roots' literal sums, per pixel and per render call: a root's (x1, n) is its pixel's, so the literal
+// running sums of its candidates are the same for every sample; the first exact root of a pixel stores
+// them (pool entry: the running sum after each cached candidate, -1 if culled, then weights_sum) and
+// later ones only search.  slot[16 + px]: -1 none, -2 being computed, -3 no room, else
+// (launch << 20) | entry; an entry is read only by later launches (kernel boundaries order it).
+// slot[0]: the pool's allocation counter.
+struct RootLit {
+    int* slot;
+    double* pool;
+    int cap, stride, launch;
+};
 __global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
                                                          const double* __restrict__ qp, const double* __restrict__ qn, int qs,
                                                          const int* __restrict__ qpixel, const int* __restrict__ qsample,
@@ -2186,7 +2197,7 @@ __global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_
                                                          unsigned long long* stats, double* __restrict__ scratch,
                                                          const uint64_t* __restrict__ masks, int nmask, int nchunks,
                                                          const unsigned short* __restrict__ clst, const int4* __restrict__ cinfo,
-                                                         int lstride, int root_off) {
+                                                         int lstride, int root_off, RootLit RL) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (kExactBlock / 64);
     const int gw = blockIdx.x * (kExactBlock / 64) + (threadIdx.x >> 6);
@@ -2202,71 +2213,105 @@ __global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_
 #if MCPT_BAND_DIAG
         const unsigned long long t0 = wall_clock64();
 #endif
-        int ncand = 0;
-        if (clst && node >= root_off) {  // a root: its pixel's cached candidate list
-            const int px = qpixel[node];
-#if MCPT_BAND_DIAG  // exact roots per pixel, in the scratch's unused last quarter
-            if (lane == 0) atomicAdd(reinterpret_cast<int*>(scratch + (size_t)waves * nlp * 3 / 2) + px, 1);
-#endif
+        const bool root = clst && node >= root_off;
+        const int px = root ? qpixel[node] : -1;
+        const double* cum = wsc;  // the running sums searched by the pick
+        double run = 0;           // the reference's weights_sum, in its order (wave-uniform)
+        int ncand = 0, surv = -1;
+        bool claimed = false;
+        if (root) {
             ncand = cinfo[px].y;
-            for (int k = lane; k < ncand; k += 64) lst[k] = clst[(size_t)px * lstride + k];
-        } else if (masks && node < nmask) {  // the node's candidate words
-            const uint64_t* mrow = masks + (size_t)node * mask_stride(nchunks);
-            for (int c = 0; c < nchunks; c++) {
-                const uint64_t m = mrow[c];
-                if ((m >> lane) & 1) lst[ncand + __popcll(m & ((1ull << lane) - 1))] = 64 * c + lane;
-                ncand += __popcll(m);
-            }
-        } else {
-            for (int c = 0; c < S.NL; c += 64) {  // cheap stages, candidates compacted in index order
-                const int li = c + lane;
-                bool cand = false;
-                if (li < S.NL) {
-                    const double4 ln = S.lt_n[li];
-                    cand = light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                             mk3(ln.x, ln.y, ln.z), x1, nn) == 0;
+            if (RL.slot) {
+                const int sv = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(RL.slot + 16 + px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (sv >= 0 && (sv >> 20) < RL.launch) {  // stored by an earlier launch of this call
+                    cum = RL.pool + (size_t)(sv & 0xfffff) * RL.stride;
+                    run = cum[lstride];
+                } else if (sv == -1) {
+                    int old = 0;
+                    if (lane == 0) old = atomicCAS(RL.slot + 16 + px, -1, -2);
+                    claimed = __shfl(old, 0) == -1;
                 }
-                const uint64_t m = __ballot(cand);
-                if (cand) lst[ncand + lane_rank(m)] = li;
-                ncand += __popcll(m);
             }
         }
-        wave_lds_sync();
-#if MCPT_BAND_DIAG
-        const unsigned long long t1 = wall_clock64();
+        if (cum == wsc) {
+            if (root) {  // a root: its pixel's cached candidate list
+#if MCPT_BAND_DIAG  // exact roots per pixel, in the scratch's unused last quarter
+                if (lane == 0) atomicAdd(reinterpret_cast<int*>(scratch + (size_t)waves * nlp * 3 / 2) + px, 1);
 #endif
-        for (int k0 = 0; k0 < ncand; k0 += 64) {  // the literal full stage, 64 candidates at a time
-            const int k = k0 + lane;
-            if (k < ncand) {
-                const int li = lst[k];
-                const double4 ln = S.lt_n[li];
-                SphTri o;
-                const int st = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
-                                               mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
-                wsc[k] = st == 0 ? o.w : -1.0;
+                for (int k = lane; k < ncand; k += 64) lst[k] = clst[(size_t)px * lstride + k];
+            } else if (masks && node < nmask) {  // the node's candidate words
+                const uint64_t* mrow = masks + (size_t)node * mask_stride(nchunks);
+                for (int c = 0; c < nchunks; c++) {
+                    const uint64_t m = mrow[c];
+                    if ((m >> lane) & 1) lst[ncand + __popcll(m & ((1ull << lane) - 1))] = 64 * c + lane;
+                    ncand += __popcll(m);
+                }
+            } else {
+                for (int c = 0; c < S.NL; c += 64) {  // cheap stages, candidates compacted in index order
+                    const int li = c + lane;
+                    bool cand = false;
+                    if (li < S.NL) {
+                        const double4 ln = S.lt_n[li];
+                        cand = light_cheap_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                                 mk3(ln.x, ln.y, ln.z), x1, nn) == 0;
+                    }
+                    const uint64_t m = __ballot(cand);
+                    if (cand) lst[ncand + lane_rank(m)] = li;
+                    ncand += __popcll(m);
+                }
             }
-        }
-        wave_lds_sync();
+            wave_lds_sync();
 #if MCPT_BAND_DIAG
-        const unsigned long long t2 = wall_clock64();
+            const unsigned long long t1 = wall_clock64();
 #endif
-        double run = 0;  // the reference's weights_sum, in its order (wave-uniform)
-        int surv = 0;
-        for (int k0 = 0; k0 < ncand; k0 += 64) {
-            const bool in = k0 + lane < ncand;
-            const double w = in ? wsc[k0 + lane] : -1.0;
-            const bool ok = w >= 0.0;
-            surv += __popcll(__ballot(ok));
-            const double wz = ok ? w : 0.0;
-            double mine = 0.0;
+            for (int k0 = 0; k0 < ncand; k0 += 64) {  // the literal full stage, 64 candidates at a time
+                const int k = k0 + lane;
+                if (k < ncand) {
+                    const int li = lst[k];
+                    const double4 ln = S.lt_n[li];
+                    SphTri o;
+                    const int st = light_tri_stage(f3(S.lt_v[3 * li]), f3(S.lt_v[3 * li + 1]), f3(S.lt_v[3 * li + 2]),
+                                                   mk3(ln.x, ln.y, ln.z), S.light_sum[li], x1, nn, &o);
+                    wsc[k] = st == 0 ? o.w : -1.0;
+                }
+            }
+            wave_lds_sync();
+#if MCPT_BAND_DIAG
+            const unsigned long long t2 = wall_clock64();
+            if (lane == 0 && stats) {
+                atomicAdd(stats + 12, t1 - t0);
+                atomicAdd(stats + 13, t2 - t1);
+            }
+#endif
+            surv = 0;
+            for (int k0 = 0; k0 < ncand; k0 += 64) {
+                const bool in = k0 + lane < ncand;
+                const double w = in ? wsc[k0 + lane] : -1.0;
+                const bool ok = w >= 0.0;
+                surv += __popcll(__ballot(ok));
+                const double wz = ok ? w : 0.0;
+                double mine = 0.0;
 #pragma unroll 8
-            for (int q = 0; q < 64; q++) {
-                run += readlane_f64(wz, q);
-                mine = lane == q ? run : mine;
+                for (int q = 0; q < 64; q++) {
+                    run += readlane_f64(wz, q);
+                    mine = lane == q ? run : mine;
+                }
+                if (in) wsc[k0 + lane] = ok ? mine : -1.0;  // running sum after this survivor, -1 if culled
             }
-            if (in) wsc[k0 + lane] = ok ? mine : -1.0;  // running sum after this survivor, -1 if culled
+            wave_lds_sync();
+            if (claimed) {  // publish this pixel's sums for the later launches of the call
+                int e = 0;
+                if (lane == 0) e = atomicAdd(RL.slot, 1);
+                e = __shfl(e, 0);
+                if (e < RL.cap) {
+                    double* dst = RL.pool + (size_t)e * RL.stride;
+                    for (int k = lane; k < ncand; k += 64) dst[k] = wsc[k];
+                    if (lane == 0) dst[lstride] = run;
+                }
+                if (lane == 0) atomicExch(RL.slot + 16 + px, e < RL.cap ? (RL.launch << 20) | e : -3);
+            }
         }
-        wave_lds_sync();
 #if MCPT_BAND_DIAG
         const unsigned long long t3 = wall_clock64();
 #endif
@@ -2278,25 +2323,23 @@ __global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_
             int found = -1, last = -1;
             for (int k0 = 0; k0 < ncand && found < 0; k0 += 64) {
                 const bool in = k0 + lane < ncand;
-                const double rv = in ? wsc[k0 + lane] : -1.0;
+                const double rv = in ? cum[k0 + lane] : -1.0;
                 const uint64_t hm = __ballot(rv >= 0.0 && rv >= target);
                 const uint64_t sm = __ballot(rv >= 0.0);
                 if (hm) found = k0 + __ffsll((unsigned long long)hm) - 1;
                 if (sm) last = k0 + 63 - __clzll((long long)sm);
             }
             const int at = found >= 0 ? found : last;
-            if (at >= 0) pick = lst[at];
+            if (at >= 0) pick = root ? (int)clst[(size_t)px * lstride + at] : lst[at];
         }
         if (lane == 0) {
             wsum_out[node] = run;
             pick_out[node] = pick;
-            if (count_out) count_out[node] = surv;
-#if MCPT_BAND_DIAG  // wall-clock ticks (100 MHz) per phase, summed over nodes: lists, literal, sum, pick
+            if (count_out) count_out[node] = surv >= 0 ? surv : cinfo[px].z;
+#if MCPT_BAND_DIAG  // wall-clock ticks (100 MHz) summed over nodes: lists, literal (above), sum + pick
             if (stats) {
                 const unsigned long long t4 = wall_clock64();
-                atomicAdd(stats + 12, t1 - t0);
-                atomicAdd(stats + 13, t2 - t1);
-                atomicAdd(stats + 14, t3 - t2);
+                atomicAdd(stats + 14, t3 - t0);
                 atomicAdd(stats + 15, t4 - t3);
             }
 #endif
@@ -3236,6 +3279,7 @@ struct DeviceState {
     // reusable work buffers
     DevBuf hit_f, hit_tbg, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[9], sl[13], cache_bt, cache_lst, cache_info, cache_w, masks;
     DevBuf exact, exact_scr, slack;  // exact pick: list, k_prep_exact's scratch, per-node slack
+    DevBuf lit_slot, lit_pool;        // exact pick: roots' literal sums per pixel (RootLit)
     int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
@@ -3953,6 +3997,14 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         pc.lstride = lstride;
         pc.use = 1;  // built below, inside the timed region
     }
+    RootLit rl{};  // roots' literal sums per pixel (k_prep_exact), up to 2 GiB of entries
+    if (exact_pick && pc.use) {
+        rl.stride = (lstride + 8 + 7) & ~7;
+        rl.cap = (int)std::min<long long>({(long long)npx, (2ll << 30) / (8ll * rl.stride), 1ll << 20});
+        if ((rc = ensure(D.lit_slot, 4ull * (npx + 16))) || (rc = ensure(D.lit_pool, 8ull * rl.stride * rl.cap))) return rc;
+        rl.slot = (int*)D.lit_slot.p;
+        rl.pool = (double*)D.lit_pool.p;
+    }
     // every buffer is allocated above (first-call hipMalloc of the cache is not device work); the
     // timed region (seconds, HIP events) starts at the primary-hit kernel
     HIP_OK(hipMemsetAsync(D.stats.p, 0, 128, st));
@@ -3984,6 +4036,10 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         }
         pc.build = 0;
         pc.use = 1;
+        if (rl.slot) {  // a fresh set of per-pixel literal sums for this call's cache
+            HIP_OK(hipMemsetAsync(rl.slot, 0, 64, st));
+            HIP_OK(hipMemsetAsync(rl.slot + 16, 0xff, 4ull * npx, st));
+        }
     }
     Queue* cur = &qa;
     Queue* nxt = &qb;
@@ -4137,7 +4193,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D.d.NL)), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
                                    cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
                                    nullptr, P.stats, exact_scr, masks, nmask, nchunks, pc.use ? pc.lst : nullptr,
-                                   pc.use ? pc.info : nullptr, pc.lstride, root_off);
+                                   pc.use ? pc.info : nullptr, pc.lstride, root_off,
+                                   RootLit{rl.slot, rl.pool, rl.cap, rl.stride, (int)std::min<uint64_t>(gens, 2047)});
                 HIP_OK(hipGetLastError());
             }
         }
@@ -4261,8 +4318,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->prep_exact_nodes = hs[10];
         stats->prep_band_nodes = hs[11];
 #if MCPT_BAND_DIAG
-        fprintf(stderr, "exact diag (10 ns ticks summed over nodes): lists %llu literal %llu sum %llu pick %llu\n", hs[12],
-                hs[13], hs[14], hs[15]);
+        fprintf(stderr, "exact diag (10 ns ticks summed over nodes): lists %llu literal %llu lists+literal+sum %llu pick %llu\n",
+                hs[12], hs[13], hs[14], hs[15]);
         if (exact_scr) {
             const int nlp = (D.d.NL + 63) & ~63;
             std::vector<int> pc(npx);
@@ -4661,7 +4718,7 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
                            (const int*)dl, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (double*)ds,
                            all_exact ? nullptr : (const uint64_t*)dm, prep_writes_masks(D->d, (const uint64_t*)dm) ? n : 0,
-                           prep_chunks(D->d.NL), nullptr, nullptr, 0, INT_MAX);
+                           prep_chunks(D->d.NL), nullptr, nullptr, 0, INT_MAX, RootLit{});
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
