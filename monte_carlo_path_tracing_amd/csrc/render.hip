@@ -307,7 +307,17 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 // they aim at, so the deferred fp64 slots run in nearly every wave), but with the light-ray seed
 // (tlimit known from the start, so the fp32 test also rejects triangles behind the light)
 // 4.04 -> 3.95 ms, shade-area +1.3%
-// MCPT_SLAB_NEARFAR=0: the round-2 slab test (A/B only)
+// Round-3 traversal A/B switches (same-box, profiles/round3_ab_traversal.txt), both off:
+//   MCPT_NODE_OFFSETS=1: node loads as 32-bit byte offsets from the tree base (saddr global loads, one
+//     v_or per load) instead of a 64-bit node pointer: neutral (MIS 447.3 vs 446.0 with it off / on,
+//     BRDF-only 5 499 vs 5 477);
+//   MCPT_SLAB_NEARFAR=1 (needs the offsets): each axis's near / far plane picked once per ray by the
+//     inverse direction's sign, so the slab test has no min/max pairs and no empty-slot test (97 -> 63
+//     VALU per node visit) -- and k_mis_rays 3.81 -> 4.02 ms per launch: the per-lane offsets make
+//     each load instruction touch more distinct lines of the node.
+#ifndef MCPT_NODE_OFFSETS
+#define MCPT_NODE_OFFSETS 0
+#endif
 #ifndef MCPT_SLAB_NEARFAR
 #define MCPT_SLAB_NEARFAR 0
 #endif
@@ -442,8 +452,28 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
             };
             // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch,
             // so each side reads one address space: ds_read from the LDS copy, global loads else)
+#if MCPT_NODE_OFFSETS
             if (kTop > 0 && __all(node < kTop)) visit(top);
             else visit(nodes);
+#else  // A/B: the round-2 loads (a 64-bit node pointer, fixed lo / hi offsets)
+            {
+                float lo[3][4], hi[3][4];
+                int chs[4];
+                if (kTop > 0 && __all(node < kTop)) load_node(top + node, lo, hi, chs);
+                else load_node(nodes + node, lo, hi, chs);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float tx0 = fmaf(lo[0][k], ix, -oix), tx1 = fmaf(hi[0][k], ix, -oix);
+                    const float ty0 = fmaf(lo[1][k], iy, -oiy), ty1 = fmaf(hi[1][k], iy, -oiy);
+                    const float tz0 = fmaf(lo[2][k], iz, -oiz), tz1 = fmaf(hi[2][k], iz, -oiz);
+                    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+                    const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
+                    t[k] = h ? t0 : FLT_MAX;
+                    code[k] = h ? chs[k] : kDone;
+                }
+            }
+#endif
             // sort (t, code) ascending; misses (FLT_MAX, kDone) sink to the end
             auto cs = [&](int a, int b) {
                 const bool sw = t[b] < t[a];
@@ -588,13 +618,32 @@ __device__ inline Hit grid_trace(const DScene& S, d3 ro, d3 rd, int exclude, boo
 // ============================================================================================
 // wavefront queue (SoA)
 // ============================================================================================
-// 3-vectors are component-major, x[cap] y[cap] z[cap] (node i's y at p[cap + i]): a wave's 64 nodes
-// read or write each component as one contiguous 512-B run (8 lines) instead of 24 lines per load
+// 3-vectors (the queue's p, n, wo, tp, Aux's directions and throughputs, the prep kernels' node inputs)
+// are interleaved, [cap][3] (node i's y at p[3 i + 1]): a wave's loads of one vector cover 1 536
+// contiguous bytes, fully coalesced, and a vector is one dwordx4 + dwordx2 pair.  MCPT_QUEUE_SOA=1
+// stores them component-major, x[cap] y[cap] z[cap] (three dwordx2 per vector, each a contiguous
+// 512-B run).  Same-box A/B (round 3, profiles/round3_ab_queue_layout.txt): the component-major form
+// moves the same PMC bytes per kernel (k_mis_combine 694.6 vs 696.6 GB per profile run) and issues 8
+// more memory instructions in k_extend_brdf -- BRDF-only 5 893 (interleaved) vs 5 637 Msamples/s,
+// MIS 454.8 vs 453.5 -- so interleaved is the default.
+#ifndef MCPT_QUEUE_SOA
+#define MCPT_QUEUE_SOA 0
+#endif
+__host__ __device__ inline size_t idx3(size_t cap, size_t i, int k) {
+    return MCPT_QUEUE_SOA ? (size_t)k * cap + i : 3 * i + (size_t)k;
+}
+template <class T>
+__device__ inline d3 ld3(const T* a, size_t cap, size_t i) {
+    return mk3(a[idx3(cap, i, 0)], a[idx3(cap, i, 1)], a[idx3(cap, i, 2)]);
+}
+__device__ inline void st3(double* a, size_t cap, size_t i, d3 v) {
+    a[idx3(cap, i, 0)] = v.x, a[idx3(cap, i, 1)] = v.y, a[idx3(cap, i, 2)] = v.z;
+}
 struct Queue {
-    double* p;      // [3][cap]  shading point
-    double* n;      // [3][cap]  interpolated normal
-    double* wo;     // [3][cap]
-    double* tp;     // [3][cap]  path throughput
+    double* p;      // 3-vectors (idx3): shading point
+    double* n;      // interpolated normal
+    double* wo;
+    double* tp;     // path throughput
     int* f;         // cap
     int* pixel;     // cap
     int* sample;    // cap
@@ -757,10 +806,10 @@ __device__ inline void queue_push(const Params& P, bool push, const Entry& e, in
         return;
     }
     const size_t s = (size_t)slot;
-    q.p[s] = e.p.x, q.p[q.cap + s] = e.p.y, q.p[2 * (size_t)q.cap + s] = e.p.z;
-    q.n[s] = e.N.x, q.n[q.cap + s] = e.N.y, q.n[2 * (size_t)q.cap + s] = e.N.z;
-    q.wo[s] = wo.x, q.wo[q.cap + s] = wo.y, q.wo[2 * (size_t)q.cap + s] = wo.z;
-    q.tp[s] = tp.x, q.tp[q.cap + s] = tp.y, q.tp[2 * (size_t)q.cap + s] = tp.z;
+    st3(q.p, q.cap, s, e.p);
+    st3(q.n, q.cap, s, e.N);
+    st3(q.wo, q.cap, s, wo);
+    st3(q.tp, q.cap, s, tp);
     q.f[s] = f;
     q.pixel[s] = pixel;
     q.sample[s] = sample;
@@ -847,10 +896,10 @@ __global__ __launch_bounds__(256) void k_queue_move(Queue src, int sb, Queue dst
     const size_t s = (size_t)sb + k, d = (size_t)db + k;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-        dst.p[(size_t)c * dst.cap + d] = src.p[(size_t)c * src.cap + s];
-        dst.n[(size_t)c * dst.cap + d] = src.n[(size_t)c * src.cap + s];
-        dst.wo[(size_t)c * dst.cap + d] = src.wo[(size_t)c * src.cap + s];
-        dst.tp[(size_t)c * dst.cap + d] = src.tp[(size_t)c * src.cap + s];
+        dst.p[idx3(dst.cap, d, c)] = src.p[idx3(src.cap, s, c)];
+        dst.n[idx3(dst.cap, d, c)] = src.n[idx3(src.cap, s, c)];
+        dst.wo[idx3(dst.cap, d, c)] = src.wo[idx3(src.cap, s, c)];
+        dst.tp[idx3(dst.cap, d, c)] = src.tp[idx3(src.cap, s, c)];
     }
     dst.f[d] = src.f[s];
     dst.pixel[d] = src.pixel[s];
@@ -876,8 +925,8 @@ __global__ __launch_bounds__(256) void k_root_points(DScene S, CamFrame cam, con
     }
     const int slot = block_append(q.count, want);
     if (want && slot < q.cap) {
-        q.p[slot] = p.x, q.p[q.cap + slot] = p.y, q.p[2 * (size_t)q.cap + slot] = p.z;
-        q.n[slot] = N.x, q.n[q.cap + slot] = N.y, q.n[2 * (size_t)q.cap + slot] = N.z;
+        st3(q.p, q.cap, slot, p);
+        st3(q.n, q.cap, slot, N);
         q.pixel[slot] = px;
     }
 }
@@ -915,8 +964,8 @@ __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int 
     const bool active = i < n;
     unsigned long long surv = 0, cand = 0, c1 = 0;
     if (active) {
-        const d3 x1 = mk3(qp[i], qp[qs + i], qp[2 * (size_t)qs + i]);
-        const d3 nn = mk3(qn[i], qn[qs + i], qn[2 * (size_t)qs + i]);
+        const d3 x1 = ld3(qp, qs, i);
+        const d3 nn = ld3(qn, qs, i);
         // the reference's literal chain (light_tri_stage: Mylight.cpp:335-413, six acos), so weights,
         // weights_sum (summed in index order below) and the pick are the reference's bit for bit
         auto eval = [&](int li, bool* ok) -> double {
@@ -1204,8 +1253,8 @@ __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, co
         const int node = grab++;
         left--;
         if (node >= n) break;
-        const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
-        const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
+        const d3 x1 = ld3(qp, qs, node);
+        const d3 nn = ld3(qn, qs, node);
         const NodeF nf = node_f(x1, nn, S.light_bound);
         int qcnt = 0, nb = 0, survivors = 0, candidates = 0, culled1 = 0;
         double sacc = 0;  // flagged slivers' band terms (exact pick)
@@ -1710,8 +1759,8 @@ __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S,
     const int node = blockIdx.x * blockDim.x + threadIdx.x;
     const bool act = node < n;
     const int nd = act ? node : n - 1;
-    const d3 x1 = mk3(qp[nd], qp[qs + nd], qp[2 * (size_t)qs + nd]);
-    const d3 nn = mk3(qn[nd], qn[qs + nd], qn[2 * (size_t)qs + nd]);
+    const d3 x1 = ld3(qp, qs, nd);
+    const d3 nn = ld3(qn, qs, nd);
     const NodeF f = node_f(x1, nn, S.light_bound);
     const float cn = (float)(dot(nn, x1) + MCPT_EPS);
     CullLane cl;
@@ -1794,7 +1843,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         const int node = __builtin_amdgcn_readfirstlane(grab++);
         left--;
         if (node >= n) break;
-        const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
+        const d3 x1 = ld3(qp, qs, node);
         auto u_of = [&]() {
             return u_override ? u_override[node]
                               : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
@@ -1829,7 +1878,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                 }
             }
         } else {
-        const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
+        const d3 nn = ld3(qn, qs, node);
         const NodeF nf = node_f(x1, nn, S.light_bound);
         const float cn = (float)dot(nn, x1);
         const v2f nx2{nf.nx, nf.nx}, ny2{nf.ny, nf.ny}, nz2{nf.nz, nf.nz};
@@ -2146,7 +2195,7 @@ __global__ __launch_bounds__(256) void k_prep_band(DScene S, const int* __restri
             if (!(sl > 0.0)) {
                 amb = true;
             } else {
-                const d3 x1 = mk3(qp[i], qp[qs + i], qp[2 * (size_t)qs + i]);
+                const d3 x1 = ld3(qp, qs, i);
                 amb = !(sl > band_base(S, x1, masks ? masks + (size_t)i * mask_stride(nchunks) : nullptr, nchunks));
             }
         }
@@ -2208,8 +2257,8 @@ __global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_
     if (gw == 0 && lane == 0 && stats && cnt) atomicAdd(stats + 10, (unsigned long long)cnt);
     for (int j = gw; j < cnt; j += waves) {
         const int node = list[kExactHead + j];
-        const d3 x1 = mk3(qp[node], qp[qs + node], qp[2 * (size_t)qs + node]);
-        const d3 nn = mk3(qn[node], qn[qs + node], qn[2 * (size_t)qs + node]);
+        const d3 x1 = ld3(qp, qs, node);
+        const d3 nn = ld3(qn, qs, node);
 #if MCPT_BAND_DIAG
         const unsigned long long t0 = wall_clock64();
 #endif
@@ -2505,10 +2554,10 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const d3 p = mk3(cur.p[i], cur.p[cur.cap + i], cur.p[2 * (size_t)cur.cap + i]);
-    const d3 N = mk3(cur.n[i], cur.n[cur.cap + i], cur.n[2 * (size_t)cur.cap + i]);
-    const d3 wo = mk3(cur.wo[i], cur.wo[cur.cap + i], cur.wo[2 * (size_t)cur.cap + i]);
-    const d3 tp = mk3(cur.tp[i], cur.tp[cur.cap + i], cur.tp[2 * (size_t)cur.cap + i]);
+    const d3 p = ld3(cur.p, cur.cap, i);
+    const d3 N = ld3(cur.n, cur.cap, i);
+    const d3 wo = ld3(cur.wo, cur.cap, i);
+    const d3 tp = ld3(cur.tp, cur.cap, i);
     const int f = cur.f[i];
     const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
     const float* m = S.mtl + 7 * S.tri_mat[f];
@@ -2551,10 +2600,10 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
         if (!(fabs(wsum) < MCPT_EPS)) flags |= 4;  // light pdf can only be nonzero with a light set
         w2 = kStale ? brdf_phong(N, wi, wo, kd, ks, sh) : hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh));
     }
-    A.d1[i] = wl.x, A.d1[A.cap + i] = wl.y, A.d1[2 * (size_t)A.cap + i] = wl.z;
-    A.d2[i] = wi.x, A.d2[A.cap + i] = wi.y, A.d2[2 * (size_t)A.cap + i] = wi.z;
-    A.w1[i] = w1.x, A.w1[A.cap + i] = w1.y, A.w1[2 * (size_t)A.cap + i] = w1.z;
-    A.w2[i] = w2.x, A.w2[A.cap + i] = w2.y, A.w2[2 * (size_t)A.cap + i] = w2.z;
+    st3(A.d1, A.cap, i, wl);
+    st3(A.d2, A.cap, i, wi);
+    st3(A.w1, A.cap, i, w1);
+    st3(A.w2, A.cap, i, w2);
     A.c2[2 * i] = pdf, A.c2[2 * i + 1] = dot(wi, N);
     if (kStale) A.s1[i] = s1;
     A.flags[i] = flags;
@@ -2585,8 +2634,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
     unsigned visits = 0, tests = 0;
     if (fl & (1 << set)) {
         const double* d = set == 0 ? A.d1 : A.d2;
-        const d3 ro = mk3(cur.p[i], cur.p[cur.cap + i], cur.p[2 * (size_t)cur.cap + i]);
-        const d3 rd = mk3(d[i], d[A.cap + i], d[2 * (size_t)A.cap + i]);
+        const d3 ro = ld3(cur.p, cur.cap, i);
+        const d3 rd = ld3(d, A.cap, i);
         const float4* leafv = set == 2 ? S.lleaf_v : S.leaf_v;  // uniform per block
         Hit h;
         if (kGrid)
@@ -2750,8 +2799,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                     best = Hit{-1, DBL_MAX, 0, 0};
                     if (A.flags[ii] & (1 << set)) {
                         const double* d = set == 0 ? A.d1 : A.d2;
-                        ro = mk3(cur.p[ii], cur.p[cur.cap + ii], cur.p[2 * (size_t)cur.cap + ii]);
-                        rd = mk3(d[ii], d[A.cap + ii], d[2 * (size_t)A.cap + ii]);
+                        ro = ld3(cur.p, cur.cap, ii);
+                        rd = ld3(d, A.cap, ii);
                         excl = cur.f[ii];
                         if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) {  // reference: UB (Myobj.cpp:463-468)
                             finish();
@@ -2882,14 +2931,14 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
     const size_t o1 = ii, o2 = (size_t)A.cap + ii, ol = 2 * (size_t)A.cap + ii;
     const bool c1 = active && (fl & 1) && A.hf[o1] >= 0;
     const bool c2 = active && (fl & 2) && A.hf[o2] >= 0;
-    const d3 p = mk3(cur.p[ii], cur.p[cur.cap + ii], cur.p[2 * (size_t)cur.cap + ii]);
-    const d3 N = mk3(cur.n[ii], cur.n[cur.cap + ii], cur.n[2 * (size_t)cur.cap + ii]);
+    const d3 p = ld3(cur.p, cur.cap, ii);
+    const d3 N = ld3(cur.n, cur.cap, ii);
     const int li = (c2 && (fl & 4) && A.hf[ol] >= 0) ? S.tri_light[A.hf[ol]] : -1;
     const double own[7] = {p.x, p.y, p.z, N.x, N.y, N.z, cur.wsum[ii]};
-    const d3 d1 = mk3(A.d1[ii], A.d1[A.cap + ii], A.d1[2 * (size_t)A.cap + ii]);
-    const d3 d2 = mk3(A.d2[ii], A.d2[A.cap + ii], A.d2[2 * (size_t)A.cap + ii]);
-    const d3 w1 = mk3(A.w1[ii], A.w1[A.cap + ii], A.w1[2 * (size_t)A.cap + ii]);
-    const d3 w2 = mk3(A.w2[ii], A.w2[A.cap + ii], A.w2[2 * (size_t)A.cap + ii]);
+    const d3 d1 = ld3(A.d1, A.cap, ii);
+    const d3 d2 = ld3(A.d2, A.cap, ii);
+    const d3 w1 = ld3(A.w1, A.cap, ii);
+    const d3 w2 = ld3(A.w2, A.cap, ii);
     const double pdf = A.c2[2 * ii], cosb = A.c2[2 * ii + 1];
     if (!kStale) {  // fresh light pdf (this node's own prep) and forward throughputs
         d3 tp2 = mk3(0, 0, 0);
@@ -3051,10 +3100,10 @@ __global__ __launch_bounds__(256, MCPT_LB_SHADE_GEN) void k_shade_gen(Params P, 
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const d3 p = mk3(cur.p[i], cur.p[cur.cap + i], cur.p[2 * (size_t)cur.cap + i]);
-    const d3 N = mk3(cur.n[i], cur.n[cur.cap + i], cur.n[2 * (size_t)cur.cap + i]);
-    const d3 wo = mk3(cur.wo[i], cur.wo[cur.cap + i], cur.wo[2 * (size_t)cur.cap + i]);
-    const d3 tp = mk3(cur.tp[i], cur.tp[cur.cap + i], cur.tp[2 * (size_t)cur.cap + i]);
+    const d3 p = ld3(cur.p, cur.cap, i);
+    const d3 N = ld3(cur.n, cur.cap, i);
+    const d3 wo = ld3(cur.wo, cur.cap, i);
+    const d3 tp = ld3(cur.tp, cur.cap, i);
     const int f = cur.f[i];
     const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
     const float* m = S.mtl + 7 * S.tri_mat[f];
@@ -3105,10 +3154,10 @@ __global__ __launch_bounds__(256, MCPT_LB_SHADE_GEN) void k_shade_gen(Params P, 
             w2 = mul(hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
         }
     }
-    A.d1[i] = wl.x, A.d1[A.cap + i] = wl.y, A.d1[2 * (size_t)A.cap + i] = wl.z;
-    A.d2[i] = wi.x, A.d2[A.cap + i] = wi.y, A.d2[2 * (size_t)A.cap + i] = wi.z;
-    A.w1[i] = w1.x, A.w1[A.cap + i] = w1.y, A.w1[2 * (size_t)A.cap + i] = w1.z;
-    A.w2[i] = w2.x, A.w2[A.cap + i] = w2.y, A.w2[2 * (size_t)A.cap + i] = w2.z;
+    st3(A.d1, A.cap, i, wl);
+    st3(A.d2, A.cap, i, wi);
+    st3(A.w1, A.cap, i, w1);
+    st3(A.w2, A.cap, i, w2);
     A.hf[2 * (size_t)A.cap + i] = pick >= 0 ? S.light_facet[pick] : -1;
     A.flags[i] = flags;
 }
@@ -3122,14 +3171,14 @@ __global__ __launch_bounds__(256) void k_shade_combine(Params P, Queue cur, int 
     const size_t o1 = ii, o2 = (size_t)A.cap + ii;
     if (active && (fl & 1) && A.hf[o1] >= 0 && A.hf[o1] == A.hf[2 * (size_t)A.cap + ii]) {
         double* px = P.fb + 3 * (size_t)cur.pixel[ii];
-        unsafeAtomicAdd(px + 0, A.w1[ii]);
-        unsafeAtomicAdd(px + 1, A.w1[A.cap + ii]);
-        unsafeAtomicAdd(px + 2, A.w1[2 * (size_t)A.cap + ii]);
+        unsafeAtomicAdd(px + 0, A.w1[idx3(A.cap, ii, 0)]);
+        unsafeAtomicAdd(px + 1, A.w1[idx3(A.cap, ii, 1)]);
+        unsafeAtomicAdd(px + 2, A.w1[idx3(A.cap, ii, 2)]);
     }
     const int h2 = A.hf[o2];
     const bool c = active && (fl & 2) && h2 >= 0 && S.tri_light[h2] < 0;
-    const d3 d2 = mk3(A.d2[ii], A.d2[A.cap + ii], A.d2[2 * (size_t)A.cap + ii]);
-    const d3 w2 = mk3(A.w2[ii], A.w2[A.cap + ii], A.w2[2 * (size_t)A.cap + ii]);
+    const d3 d2 = ld3(A.d2, A.cap, ii);
+    const d3 w2 = ld3(A.w2, A.cap, ii);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
     block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u);
@@ -3140,9 +3189,9 @@ __global__ __launch_bounds__(256) void k_brdf_gen(Params P, Queue cur, int n, Au
     const DScene& S = P.S;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const d3 N = mk3(cur.n[i], cur.n[cur.cap + i], cur.n[2 * (size_t)cur.cap + i]);
-    const d3 wo = mk3(cur.wo[i], cur.wo[cur.cap + i], cur.wo[2 * (size_t)cur.cap + i]);
-    const d3 tp = mk3(cur.tp[i], cur.tp[cur.cap + i], cur.tp[2 * (size_t)cur.cap + i]);
+    const d3 N = ld3(cur.n, cur.cap, i);
+    const d3 wo = ld3(cur.wo, cur.cap, i);
+    const d3 tp = ld3(cur.tp, cur.cap, i);
     const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
     const float* m = S.mtl + 7 * S.tri_mat[cur.f[i]];
     const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
@@ -3155,8 +3204,8 @@ __global__ __launch_bounds__(256) void k_brdf_gen(Params P, Queue cur, int n, Au
         flags = 2;
         w2 = mul(hmul(tp, brdf_phong(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
     }
-    A.d2[i] = wi.x, A.d2[A.cap + i] = wi.y, A.d2[2 * (size_t)A.cap + i] = wi.z;
-    A.w2[i] = w2.x, A.w2[A.cap + i] = w2.y, A.w2[2 * (size_t)A.cap + i] = w2.z;
+    st3(A.d2, A.cap, i, wi);
+    st3(A.w2, A.cap, i, w2);
     A.flags[i] = flags;
 }
 
@@ -3168,8 +3217,8 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
     const size_t o2 = (size_t)A.cap + ii;
     const int h2 = A.hf[o2];
     const bool c = active && (fl & 2) && h2 >= 0;
-    const d3 d2 = mk3(A.d2[ii], A.d2[A.cap + ii], A.d2[2 * (size_t)A.cap + ii]);
-    const d3 w2 = mk3(A.w2[ii], A.w2[A.cap + ii], A.w2[2 * (size_t)A.cap + ii]);
+    const d3 d2 = ld3(A.d2, A.cap, ii);
+    const d3 w2 = ld3(A.w2, A.cap, ii);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
     block_count(P.stats + 2, (active && (fl & 2)) ? 1u : 0u);
@@ -3201,10 +3250,10 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
     const int ii = active ? i : 0;
-    const d3 p = mk3(cur.p[ii], cur.p[cur.cap + ii], cur.p[2 * (size_t)cur.cap + ii]);
-    const d3 N = mk3(cur.n[ii], cur.n[cur.cap + ii], cur.n[2 * (size_t)cur.cap + ii]);
-    const d3 wo = mk3(cur.wo[ii], cur.wo[cur.cap + ii], cur.wo[2 * (size_t)cur.cap + ii]);
-    const d3 tp = mk3(cur.tp[ii], cur.tp[cur.cap + ii], cur.tp[2 * (size_t)cur.cap + ii]);
+    const d3 p = ld3(cur.p, cur.cap, ii);
+    const d3 N = ld3(cur.n, cur.cap, ii);
+    const d3 wo = ld3(cur.wo, cur.cap, ii);
+    const d3 tp = ld3(cur.tp, cur.cap, ii);
     const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
     const uint64_t node = cur.node[ii];
     bool c = false;
@@ -3303,11 +3352,11 @@ struct mcpt_scene {
 
 namespace {
 
-// n 3-vectors [n][3] -> component-major [3][n]
+// n 3-vectors [n][3] -> the kernels' node-input layout (idx3 with stride n)
 std::vector<double> soa3(const double* v, int n) {
     std::vector<double> o(3 * (size_t)n);
     for (int i = 0; i < n; i++)
-        for (int k = 0; k < 3; k++) o[(size_t)k * n + i] = v[3 * (size_t)i + k];
+        for (int k = 0; k < 3; k++) o[idx3((size_t)n, i, k)] = v[3 * (size_t)i + k];
     return o;
 }
 
@@ -4688,7 +4737,7 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
         HIP_OK(hipMemset(dl, 0, 4));
         HIP_OK(hipMemset((int*)dl + n + kExactHead, 0, 4));
     }
-    {  // the kernels read node coordinates component-major (x[n], y[n], z[n], like the wavefront queue)
+    {  // node coordinates in the kernels' 3-vector layout (idx3, like the wavefront queue)
         const std::vector<double> px = soa3(x1, n), pn = soa3(nrm, n);
         HIP_OK(hipMemcpy(dp, px.data(), 24ull * n, hipMemcpyHostToDevice));
         HIP_OK(hipMemcpy(dn, pn.data(), 24ull * n, hipMemcpyHostToDevice));
@@ -5099,7 +5148,7 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     HIP_OK(hipMalloc(&du, 8ull * n));
     HIP_OK(hipMalloc(&dw, 8ull * n));
     HIP_OK(hipMalloc(&dk, 4ull * n));
-    {  // the kernels read node coordinates component-major (x[n], y[n], z[n], like the wavefront queue)
+    {  // node coordinates in the kernels' 3-vector layout (idx3, like the wavefront queue)
         const std::vector<double> px = soa3(x1, n), pn = soa3(nrm, n);
         HIP_OK(hipMemcpy(dp, px.data(), 24ull * n, hipMemcpyHostToDevice));
         HIP_OK(hipMemcpy(dn, pn.data(), 24ull * n, hipMemcpyHostToDevice));
