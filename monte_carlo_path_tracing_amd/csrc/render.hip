@@ -669,6 +669,13 @@ struct Queue {
 #ifndef MCPT_BAND_DIAG
 #define MCPT_BAND_DIAG 0
 #endif
+// MCPT_SEED_BRDF=1 (A/B only): trace the BRDF direction's light-only query (set 2) in its own launch
+// first and start set 1 (the same direction against the full BVH) with its light hit as tlimit.
+// Same-box A/B (round 3, profiles/round3_ab_traversal.txt): MIS 462.8 -> 460.9, Cornell-1M 1 274 ->
+// 1 259 Msamples/s -- the second launch and the smaller grids cost more than the pruning saves.
+#ifndef MCPT_SEED_BRDF
+#define MCPT_SEED_BRDF 0
+#endif
 #ifndef MCPT_EXACT_PICK
 #define MCPT_EXACT_PICK 1
 #endif
@@ -2644,9 +2651,12 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
             // set 0 aims at a sampled light triangle: the generation kernel left that triangle's
             // exact t along the ray in the set-0 hit slot (seed_light_t), so boxes behind the light
             // are pruned from the start
+            // set 1 (the BRDF direction against the full BVH) when set 2 (the same direction against the
+            // light-only BVH) ran first (seeded & 2): its light hit's t, left in the set-1 hit slot, bounds
+            // the closest hit the same way -- the light triangle is in the full BVH too
             float tl0 = FLT_MAX;
-            if (set == 0 && seeded) {
-                const double t0 = A.hbg[2 * (size_t)i];
+            if ((set == 0 && (seeded & 1)) || (set == 1 && (seeded & 2))) {
+                const double t0 = A.hbg[2 * ((size_t)set * A.cap + i)];
                 if (t0 > 0) tl0 = (float)t0 * 1.0001f + 1e-5f;
             }
             h = trace4_ww<kRayTopLds, kCount, kTop, MCPT_FILTER_MIS>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
@@ -2655,6 +2665,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
+        if (set == 2) beta = h.f >= 0 ? h.t : -1.0;  // the seed of set 1 (seeded & 2)
     }
     if (kCount) {
         wave_count2(cnt, visits, cnt + 1, tests);
@@ -2665,6 +2676,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
     if (set < 2) {
         A.hbg[2 * o] = beta;
         A.hbg[2 * o + 1] = gamma;
+    } else if (seeded & 2) {
+        A.hbg[2 * ((size_t)A.cap + i)] = (fl & 2) ? beta : -1.0;  // set 1's slot, read before set 1 writes it
     }
 }
 
@@ -2766,6 +2779,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
         if (set < 2) {
             A.hbg[2 * o] = best.beta;
             A.hbg[2 * o + 1] = best.gamma;
+        } else if (seeded & 2) {  // the seed of set 1 (k_mis_rays)
+            A.hbg[2 * ((size_t)A.cap + ii)] = (A.flags[ii] & 2) && best.f >= 0 ? best.t : -1.0;
         }
         busy = false;
     };
@@ -2813,8 +2828,9 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                             ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
                             oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
                             tlimit = FLT_MAX;
-                            if (set == 0 && seeded) {  // the light triangle's exact t (seed_light_t)
-                                const double t0 = A.hbg[2 * (size_t)ii];
+                            // set 0: the light triangle's exact t (seed_light_t); set 1: set 2's light hit
+                            if ((set == 0 && (seeded & 1)) || (set == 1 && (seeded & 2))) {
+                                const double t0 = A.hbg[2 * ((size_t)set * A.cap + ii)];
                                 if (t0 > 0) tlimit = (float)t0 * 1.0001f + 1e-5f;
                             }
                             sp = 0;
@@ -4272,7 +4288,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (!fused && o->mode == MCPT_MODE_MIS) {
             hipLaunchKernelGGL(stale ? k_mis_gen<true> : k_mis_gen<false>, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            launch_rays(0, 3, 1);
+            if (MCPT_SEED_BRDF && !grid) {  // the light-only BRDF query first: its hit seeds set 1
+                launch_rays(2, 1, 2);
+                launch_rays(0, 2, 3);
+            } else {
+                launch_rays(0, 3, 1);
+            }
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(stale ? k_mis_combine<true> : k_mis_combine<false>, g256, b256, 0, st, P, *cur, ni, aux,
                                *nxt, T, rp);
