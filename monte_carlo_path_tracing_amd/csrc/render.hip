@@ -1157,7 +1157,8 @@ __device__ inline double band_base(const DScene& S, d3 x1, const uint64_t* mrow,
 // before it (none if that is 0: no earlier weight); above, the cumulative weight including it
 // (pl is wave-uniform -- it comes from a ballot -- so the two values are read with v_readlane into
 // SGPRs rather than an LDS permute)
-__device__ inline double readlane_f64(double v, int l) {
+__device__ inline double readlane_f64(double v, int l) {  // l: wave-uniform
+    l = __builtin_amdgcn_readfirstlane(l);
     const unsigned long long b = __double_as_longlong(v);
     return __longlong_as_double(((long long)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l) << 32) |
                                 (unsigned)__builtin_amdgcn_readlane((int)b, l));
@@ -1527,9 +1528,10 @@ __device__ inline void append_masked(uint64_t m, unsigned lo, unsigned hi, unsig
 // scan over the same batch totals and the same batch re-evaluation as the full path, so results
 // are identical.
 struct PrepCache {
-    double* bt;           // [npx][nchunks]
+    double* bt;           // [npx][nchunks] the batch totals' inclusive scan (raw totals when nb > 64)
     unsigned short* lst;  // [npx][lstride] candidate list (light indices, index order)
-    double* w;            // [npx][lstride] candidate weights (-1 = culled by the full stage)
+    double* w;            // [npx][lstride] in-batch inclusive prefix of the candidate weights (wave scan);
+                          // a candidate the full stage culls: its prefix with the sign bit set
     int4* info;           // [npx] (nb, ncand, survivors, 0)
     int lstride;
     int build;            // this launch builds entries of pixel qpixel[node] (qpixel == nullptr: node)
@@ -1937,10 +1939,12 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                         bool ok0, ok1;
                         double w0, w1;
                         prep_weight_f32x2(rw, (int)lst[k0], has1 ? (int)lst[k1] : (int)sentinel, xf, &w0, &w1, &ok0, &ok1);
-                        if (kBuild) {
+                        if (kBuild) {  // in-batch inclusive prefixes, culled with the sign bit (PrepCache::w)
                             const size_t row = (size_t)(qpixel ? qpixel[node] : node) * C.lstride;
-                            if (k0 < ncand) C.w[row + k0] = ok0 ? w0 : -1.0;
-                            if (k1 < ncand) C.w[row + k1] = ok1 ? w1 : -1.0;
+                            const double s0 = wave_incl_scan(ok0 ? w0 : 0.0, lane);
+                            const double s1 = has1 ? wave_incl_scan(ok1 ? w1 : 0.0, lane) : 0.0;
+                            if (k0 < ncand) C.w[row + k0] = ok0 ? s0 : copysign(s0, -1.0);
+                            if (k1 < ncand) C.w[row + k1] = ok1 ? s1 : copysign(s1, -1.0);
                         }
                         w4[i] = w0;
                         w4[i + 1] = w1;
@@ -1956,7 +1960,10 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
                     const int k = 64 * (b0 + i) + lane;
                     double l2;
                     const WeightBx r = prep_weight_buf_bx(rw, (int)lst[k], x1, &l2);  // w = 0 if culled
-                    if (kBuild && k < ncand) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = r.ok ? r.w : -1.0;
+                    if (kBuild) {  // in-batch inclusive prefix, culled with the sign bit (PrepCache::w)
+                        const double sc = wave_incl_scan(r.ok ? r.w : 0.0, lane);
+                        if (k < ncand) C.w[(size_t)(qpixel ? qpixel[node] : node) * C.lstride + k] = r.ok ? sc : copysign(sc, -1.0);
+                    }
                     w4[i] = r.w;
                     // a real branch (SALU only when no lane is culled or a sliver): culled lanes (the
                     // padding included) are counted, slivers add their term to the band
@@ -1989,7 +1996,12 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         if (!kF32 && __ballot(sacc > 0.0)) band_sl = band_sliver(__shfl(wave_incl_scan(sacc, lane), 63));
         if (kBuild) {  // store the entry of this pixel (C.build), with the node's band for k_prep_pick
             const int px = qpixel ? qpixel[node] : node;
-            for (int b = lane; b < nb; b += 64) C.bt[(size_t)px * nchunks + b] = bt[b];
+            if (nb <= 64) {  // the batch totals' inclusive scan -- the same scan k_prep_pick used to redo per root
+                const double cum = wave_incl_scan(lane < nb ? bt[lane] : 0.0, lane);
+                if (lane < nb) C.bt[(size_t)px * nchunks + lane] = cum;
+            } else {  // k_prep_pick sums these sequentially
+                for (int b = lane; b < nb; b += 64) C.bt[(size_t)px * nchunks + b] = bt[b];
+            }
             for (int k = lane; k < ncand; k += 64) C.lst[(size_t)px * C.lstride + k] = lst[k];
             if (lane == 0) {
                 const double band = kF32 ? 0.0 : band_sl + band_base(S, x1, mrow, nchunks);
@@ -2091,17 +2103,18 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
             kb[k] = -1;
             base[k] = 0;
             target[k] = 0;
-            if (nb <= 64) {
-                const double v = lane < nb ? vraw[k] : 0.0;
-                const double cum = wave_incl_scan(v, lane);
-                wsum[k] = __shfl(cum, 63);
+            if (nb <= 64) {  // vraw = the cached inclusive scan of the batch totals (cache build)
+                const double W = nb > 0 ? readlane_f64(vraw[k], nb - 1) : 0.0;
+                const double cum = lane < nb ? vraw[k] : W;
+                wsum[k] = W;
                 if (!(fabs(wsum[k]) < MCPT_EPS)) {
                     target[k] = u * wsum[k];
-                    const uint64_t hitm = __ballot(cum >= target[k] && v > 0);
-                    const uint64_t posm = __ballot(v > 0);
-                    kb[k] = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63 - __clzll((long long)posm);
-                    const double exc = __shfl_up(cum, 1);
-                    base[k] = kb[k] == 0 ? 0.0 : __shfl(exc, kb[k]);
+                    // the first batch whose running total reaches the target (and is positive: for a
+                    // target > 0 that batch's own total is positive, as "cum >= target && v > 0" required;
+                    // for target 0 it is the first positive batch); target <= W, so one exists
+                    const uint64_t hitm = __ballot(lane < nb && cum >= target[k] && cum > 0.0);
+                    kb[k] = hitm ? __ffsll((unsigned long long)hitm) - 1 : -1;
+                    base[k] = kb[k] > 0 ? readlane_f64(cum, kb[k] - 1) : 0.0;
                 }
             } else {  // more than 64 batches (N_L > 4096 with many candidates): sequential search
                 double ws = 0;
@@ -2135,7 +2148,7 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
         for (int k = 0; k < kPickNodes; k++) {
             const int j = 64 * kb[k] + lane;
             const bool act = kb[k] >= 0 && j < inf[k].y;
-            wc[k] = act ? C.w[(size_t)px[k] * C.lstride + j] : -1.0;
+            wc[k] = act ? C.w[(size_t)px[k] * C.lstride + j] : -0.0;  // signed in-batch prefix
         }
         // the picked lane's light index only (one uniform load per root, issued for all roots
         // before waiting) instead of the batch's 64 list entries
@@ -2146,8 +2159,10 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
             pls[k] = -1;
             margin[k] = INFINITY;
             if (kb[k] >= 0) {
-                const bool ok = wc[k] >= 0;
-                const double sc = wave_incl_scan(ok ? wc[k] : 0.0, lane);
+                // the cache build stored each batch's inclusive scan (the scan this pick used to redo):
+                // survivors as is, culled candidates with the sign bit set
+                const bool ok = !signbit(wc[k]);
+                const double sc = fabs(wc[k]);
                 const uint64_t candm = __ballot(ok && (base[k] + sc >= target[k]));
                 const uint64_t okm = __ballot(ok);
                 if (candm) pls[k] = __ffsll((unsigned long long)candm) - 1;
