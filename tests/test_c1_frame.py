@@ -8,9 +8,11 @@
 Per pixel: the GPU's light prep is an fp64 reformulation (Van Oosterom-Strackee excess, rsqrt unit
 vectors) whose weights equal the reference formulas' to ~1e-9.  A light pick whose u * weights_sum
 lies within that rounding band of a cumulative-weight boundary is redone with the reference's literal
-formulas and summation order (k_prep_exact), so every pick is the reference's and
-every pixel must agree to <= 1e-3 (the north star's per-pixel tolerance); the maximum is printed.
-(Before the band, round 2: one C1 MIS pixel at 2.9e-3 from a pick of the adjacent triangle.)"""
+formulas and summation order (k_prep_exact), and the picked triangle's Arvo setup and the stale pdf's
+survival test use the literal chain with a correctly rounded acos, so every pixel
+must agree to <= 1e-3 (the north star's per-pixel tolerance); the maximum is printed.  (Round 2: one C1
+MIS pixel at 2.9e-3 -- the sample point on a sliver light triangle, whose sA is mostly the reference's
+own acos rounding.)"""
 import numpy as np
 import pytest
 

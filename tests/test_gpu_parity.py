@@ -199,6 +199,20 @@ def test_light_prep_exact_fallback_is_the_reference(scene, oscene):
     assert np.array_equal(pe, expect) and np.array_equal(pr, expect)
 
 
+def test_exact_pick_statistics(scene):
+    """the exact-pick bookkeeping of a cached-root MIS render (mcpt_stats, ABI 2.1): some preps reach the
+    per-chunk band test and some of those (plus ambiguous cached roots) the literal fallback, a small
+    fraction of all shading nodes; the fp32 opt-in precision makes no exactness claim and runs none"""
+    cam = mcpt.Camera.reference(200, 150)
+    _, st = mcpt.render(scene, cam, 64, mode="mis", seed=SEED, device=0)
+    print("200x150x64 MIS: %d shading nodes, %d band tests, %d exact preps, root cache build %.2f ms" % (
+        st.shading_nodes, st.prep_band_nodes, st.prep_exact_nodes, 1e3 * st.cache_build_seconds))
+    assert st.prep_band_nodes > 0 and st.prep_exact_nodes > 0
+    assert st.prep_exact_nodes < 1e-2 * st.shading_nodes and st.cache_build_seconds > 0
+    _, s32 = mcpt.render(scene, cam, 64, mode="mis", seed=SEED, device=0, flags=mcpt.RENDER_PRECISION_FP32)
+    assert s32.prep_exact_nodes == 0 and s32.prep_band_nodes == 0
+
+
 OMODE = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF, "shade": po.MODE_SHADE, "shade_area": po.MODE_SHADE_AREA}
 
 
