@@ -318,6 +318,11 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 #ifndef MCPT_NODE_OFFSETS
 #define MCPT_NODE_OFFSETS 0
 #endif
+// MCPT_SLAB_SELECT=1 (A/B only): the near / far float planes selected per axis by the ray's sign after the
+// usual loads: MIS 464.3 -> 463.2, BRDF-only 5 831 -> 5 760 (profiles/round3_ab_traversal.txt)
+#ifndef MCPT_SLAB_SELECT
+#define MCPT_SLAB_SELECT 0
+#endif
 #ifndef MCPT_SLAB_NEARFAR
 #define MCPT_SLAB_NEARFAR 0
 #endif
@@ -372,6 +377,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     // direction's), so they miss without a child-code test.
     const unsigned nx = MCPT_SLAB_NEARFAR && ix < 0 ? 48u : 0u, ny = MCPT_SLAB_NEARFAR && iy < 0 ? 64u : 16u,
                    nz = MCPT_SLAB_NEARFAR && iz < 0 ? 80u : 32u;
+    const bool sx = ix < 0, sy = iy < 0, sz = iz < 0;  // MCPT_SLAB_SELECT
     const unsigned fx = 48u - nx, fy = 80u - ny, fz = 112u - nz;
     // tlimit0: at least the t of a triangle tri_hit accepts (or FLT_MAX) -- boxes beyond it hold no
     // closest hit
@@ -463,12 +469,21 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                 else load_node(nodes + node, lo, hi, chs);
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
+#if MCPT_SLAB_SELECT  // near / far plane per axis by the ray's sign (k_rays_persistent's form, float planes)
+                    const float nxp = sx ? hi[0][k] : lo[0][k], fxp = sx ? lo[0][k] : hi[0][k];
+                    const float nyp = sy ? hi[1][k] : lo[1][k], fyp = sy ? lo[1][k] : hi[1][k];
+                    const float nzp = sz ? hi[2][k] : lo[2][k], fzp = sz ? lo[2][k] : hi[2][k];
+                    const float t0 = fmaxf(fmaxf(fmaf(nxp, ix, -oix), fmaf(nyp, iy, -oiy)), fmaxf(fmaf(nzp, iz, -oiz), 0.0f));
+                    const float t1 = fminf(fminf(fmaf(fxp, ix, -oix), fmaf(fyp, iy, -oiy)), fminf(fmaf(fzp, iz, -oiz), tlimit));
+                    const bool h = chs[k] != kBvh4Empty && t0 <= fmaf(t1, 1.00001f, 1e-6f);
+#else
                     const float tx0 = fmaf(lo[0][k], ix, -oix), tx1 = fmaf(hi[0][k], ix, -oix);
                     const float ty0 = fmaf(lo[1][k], iy, -oiy), ty1 = fmaf(hi[1][k], iy, -oiy);
                     const float tz0 = fmaf(lo[2][k], iz, -oiz), tz1 = fmaf(hi[2][k], iz, -oiz);
                     const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
                     const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
                     const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
+#endif
                     t[k] = h ? t0 : FLT_MAX;
                     code[k] = h ? chs[k] : kDone;
                 }
