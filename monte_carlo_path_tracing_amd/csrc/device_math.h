@@ -205,10 +205,15 @@ __device__ inline int light_tri_stage(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d
     const double cc = fmax(-1.0, fmin(1.0, dot(A, B)));
     if (ca == 1.0 || cb == 1.0 || cc == 1.0) return 3;  // a, b or c < 1e-8
     const d3 uBA = normalized(cross(B, A)), uAC = normalized(cross(A, C)), uCB = normalized(cross(C, B));
-    double alpha = acos_cr(fmax(-1.0, fmin(1.0, -dot(uBA, uAC))));
-    double beta = acos_cr(fmax(-1.0, fmin(1.0, -dot(uCB, uBA))));
-    double gamma = acos_cr(fmax(-1.0, fmin(1.0, -dot(uAC, uCB))));
-    if (alpha < MCPT_EPS || beta < MCPT_EPS || gamma < MCPT_EPS) return 3;
+    // one angle at a time with its test (the same outcome as the reference's three acos and one
+    // test: every failing test returns 3): the branches keep the three acos_cr from interleaving,
+    // which caps the register peak of the kernels that inline this chain
+    const double alpha = acos_cr(fmax(-1.0, fmin(1.0, -dot(uBA, uAC))));
+    if (alpha < MCPT_EPS) return 3;
+    const double beta = acos_cr(fmax(-1.0, fmin(1.0, -dot(uCB, uBA))));
+    if (beta < MCPT_EPS) return 3;
+    const double gamma = acos_cr(fmax(-1.0, fmin(1.0, -dot(uAC, uCB))));
+    if (gamma < MCPT_EPS) return 3;
     double sA = alpha + beta + gamma - MCPT_PI;
     if (sA < 0) return 3;
     double w = sA * lsum;
@@ -532,8 +537,9 @@ __device__ inline void light_weight_f32x2(const LightF32& I, const LightF32& J, 
 // un-normalised edge vectors, normalising by positive lengths cannot change its sign), alpha
 // (the angle at A between the great arcs AB and AC, Mylight.cpp:385) and c = acos(A.B).
 // Returns true if the triangle survives; fills o.
-__device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, d3 n, SphTri* o) {
+__device__ inline bool light_full(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, d3 n, SphTri* o, bool* sliver = nullptr) {
     const SphEx e = sph_excess(sub(p0, x1), sub(p1, x1), sub(p2, x1));
+    if (sliver) *sliver = fma(MCPT_BAND_TAU, e.num, e.den) < 4.0;
     const double w = e.half * lsum2;
     if (!(e.edges_ok & (e.half > 0) & __builtin_amdgcn_class(w, 0x1e0))) return false;
     const d3 A = e.A;

@@ -538,7 +538,8 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     return best;
 }
 
-// MCPT_PICK_LITERAL=0: light_full's form for the picked triangle (A/B of the literal chain's cost)
+// MCPT_PICK_LITERAL=0: light_full's form for the picked triangle (A/B of the literal chain's cost);
+// 2: light_full's form, the literal chain only for a flagged sliver (4 - den > kBandTau num)
 #ifndef MCPT_PICK_LITERAL
 #define MCPT_PICK_LITERAL 1
 #endif
@@ -551,8 +552,17 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
 __device__ inline void pick_sph(const DScene& S, int pick, d3 p, d3 N, SphTri* sph) {
     const double4 ln = S.lt_n[pick];
     const d3 p0 = f3(S.lt_v[3 * pick]), p1 = f3(S.lt_v[3 * pick + 1]), p2 = f3(S.lt_v[3 * pick + 2]);
+#if MCPT_PICK_LITERAL == 2
+    bool sliver = false;
+    const bool ok = light_full(p0, p1, p2, 2.0 * ln.w, p, N, sph, &sliver);
+    if (ok && sliver) {
+        SphTri lit;
+        if (light_tri_stage<true>(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, &lit) == 0) *sph = lit;
+    }
+#else
     if (!MCPT_PICK_LITERAL || light_tri_stage<true>(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, sph) != 0)
         light_full(p0, p1, p2, 2.0 * ln.w, p, N, sph);
+#endif
 }
 
 // x86 cvttsd2si semantics for (int)floor(x) of the reference (out of range -> INT_MIN)
@@ -2593,17 +2603,12 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
     if (i >= n) return;
     const d3 p = ld3(cur.p, cur.cap, i);
     const d3 N = ld3(cur.n, cur.cap, i);
-    const d3 wo = ld3(cur.wo, cur.cap, i);
-    const d3 tp = ld3(cur.tp, cur.cap, i);
-    const int f = cur.f[i];
     const uint64_t key = counter_key(P.seed, (uint64_t)cur.pixel[i], (uint64_t)cur.sample[i], cur.node[i]);
-    const float* m = S.mtl + 7 * S.tri_mat[f];
-    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
-    const double sh = m[6];
     const double wsum = cur.wsum[i];
     const int pick = cur.pick[i];
     int flags = 0;
-    // ---- light branch (main.cpp:443-466) ----
+    // ---- light branch (main.cpp:443-466); the BRDF inputs are loaded after it (the picked light's
+    // literal chain is the register peak: 132 -> 116 VGPRs, 3 -> 4 waves per SIMD) ----
     d3 coord;
     double lprob = 1;
     if (pick >= 0) {
@@ -2618,6 +2623,12 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
         coord = add(mul(N, -1), p);  // Mylight.cpp:427-430
     }
     const d3 wl = normalized(sub(coord, p));
+    const d3 wo = ld3(cur.wo, cur.cap, i);
+    const d3 tp = ld3(cur.tp, cur.cap, i);
+    const int f = cur.f[i];
+    const float* m = S.mtl + 7 * S.tri_mat[f];
+    const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
+    const double sh = m[6];
     d3 w1 = mk3(0, 0, 0);
     double s1 = 0;
     if (dot(wl, N) > 0) {
