@@ -172,11 +172,14 @@ constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB p
 #ifndef MCPT_LB_RAYS
 #define MCPT_LB_RAYS 7
 #endif
+// 4: 128 VGPRs (141 / 140 without: the literal survival chain of state_light_pdf; 44 / 12 B of
+// scratch): k_mis_combine<true> 314 -> 308, k_mis_complete 121 -> 110 ms per profile run, MIS +0.6%
+// (round 3, same box, profiles/round3_ab_exact_pick.txt block 7)
 #ifndef MCPT_LB_COMBINE
-#define MCPT_LB_COMBINE 1
+#define MCPT_LB_COMBINE 4
 #endif
 #ifndef MCPT_LB_COMPLETE
-#define MCPT_LB_COMPLETE 1
+#define MCPT_LB_COMPLETE 4
 #endif
 #ifndef MCPT_LB_SHADE_GEN
 #define MCPT_LB_SHADE_GEN 1
