@@ -13,7 +13,8 @@
 //   k_prep_pk2         WAVE per node  : phase B -- fp64 spherical-triangle weights of the candidates
 //                                       (Mylight.cpp:360-413) in dense 64-wide batches -> weights_sum
 //                                       and the inverse-CDF pick; in build mode fills the cache
-//   k_prep_pick        WAVE per root  : the pick of a root from the root-point cache
+//   k_prep_pick_g      16 LANES per root : the pick of a root from the root-point cache (k_prep_pick,
+//                      a wave per root, for tables of more than 64 chunks)
 //   k_prep / k_prep_lane              : the same prep for huge / tiny light sets
 //   k_mis_gen / k_shade_gen / k_brdf_gen, k_mis_rays (BVH or the reference grid), k_*_combine:
 //                                       light + BRDF samples, their closest hits, MIS weights and the
@@ -2225,6 +2226,170 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
     if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
 }
 
+// k_prep_pick with a 16-lane group per root (nchunks <= 64): the same search over the same cached
+// values, so the same pick, margin and exact-list decision.  k_prep_pick spends a whole wave per root
+// for a batch-total row of nchunks values and a batch of 64 weights, so its 72 VGPRs hold only four
+// roots' chains and the kernel waits on latency at ~2 TB/s (round 3 PMC: 478 B and four dependent
+// hops per root).  Here lane (g, l) of a wave holds entries l, l + 16, l + 32, l + 48 of root g's row
+// and batch -- each 16-lane load is one whole 128-B line -- so a wave keeps 4 * kPickSlots roots in
+// flight, and the batch's 64 list entries (one more line) come with its weights instead of one
+// dependent load after the search.  Cross-lane reads inside a group are ds_bpermute.
+#ifndef MCPT_PICK_SLOTS
+#define MCPT_PICK_SLOTS 2
+#endif
+#ifndef MCPT_PICK_GROUPS
+#define MCPT_PICK_GROUPS 1  // 0: k_prep_pick (wave per root) for every table size (A/B)
+#endif
+#ifndef MCPT_LB_PICKG
+#define MCPT_LB_PICKG 7  // 72 VGPRs at 2 slots without spills
+#endif
+constexpr int kPickSlots = MCPT_PICK_SLOTS;
+__device__ inline int bperm_i32(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ inline double bperm_f64(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// v[k], k uniform within the lane's group: two levels of selects on k's bits (written on the four
+// values rather than the array, which the compiler otherwise turns into an indexed scratch load)
+template <class T>
+__device__ inline T sel4v(T v0, T v1, T v2, T v3, int k) {
+    const T lo = (k & 1) ? v1 : v0, hi = (k & 1) ? v3 : v2;
+    return (k & 2) ? hi : lo;
+}
+template <class T>
+__device__ inline T sel4(const T (&v)[4], int k) { return sel4v(v[0], v[1], v[2], v[3], k); }
+// first set bit of the group's 64 entries (entry 16 k + l is bit l of field g of m[k]); -1 if none
+__device__ inline int group_first(const uint64_t (&m)[4], int g) {
+    int r = -1;
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+        const unsigned f = (unsigned)(m[k] >> (16 * g)) & 0xffffu;
+        r = f ? 16 * k + __ffs(f) - 1 : r;
+    }
+    return r;
+}
+__device__ inline int group_last(const uint64_t (&m)[4], int g) {
+    int r = -1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const unsigned f = (unsigned)(m[k] >> (16 * g)) & 0xffffu;
+        r = f ? 16 * k + 31 - __clz(f) : r;
+    }
+    return r;
+}
+__global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
+                                                     const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                                     double* __restrict__ wsum_out, int* __restrict__ pick_out,
+                                                     unsigned long long* stats, int nchunks, PrepCache C) {
+    constexpr int kR = 4 * kPickSlots;  // roots per wave and iteration
+    static_assert((kR & (kR - 1)) == 0 && kR <= 64, "pick slots");
+    const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & 15, g0 = lane & 48;
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int nq = (nchunks + 15) >> 4;  // row entries per lane (<= 4)
+    unsigned long long cached = 0;
+    for (int n0 = gw * kR; n0 < n; n0 += waves * kR) {
+        // lane r < kR: root n0 + r (coalesced queue loads) and its pick uniform (dim 1)
+        int pxl;
+        double ul;
+        {
+            const int node = min(n0 + (lane & (kR - 1)), n - 1);
+            pxl = qpixel[node];
+            ul = counter_u(counter_key(seed, (uint64_t)pxl, (uint64_t)qsample[node], qnode[node]), 1);
+        }
+        // slot s: group g takes root 4 s + g; its row of batch totals (inclusive scan) and info
+        int px[kPickSlots];
+        int4 inf[kPickSlots];
+        double bv[kPickSlots][4];
+#pragma unroll
+        for (int s = 0; s < kPickSlots; s++) {
+            px[s] = bperm_i32(pxl, 4 * s + g);
+            const double* row = C.bt + (size_t)px[s] * nchunks + gl;
+#pragma unroll
+            for (int k = 0; k < 4; k++) bv[s][k] = k < nq && 16 * k + gl < nchunks ? row[16 * k] : 0.0;
+            inf[s] = C.info[px[s]];
+        }
+        double wsum[kPickSlots], base[kPickSlots], target[kPickSlots];
+        int kb[kPickSlots];
+#pragma unroll
+        for (int s = 0; s < kPickSlots; s++) {
+            const int nb = inf[s].x;
+            const int lw = max(nb - 1, 0);
+            const double W = bperm_f64(sel4(bv[s], lw >> 4), g0 + (lw & 15));
+            wsum[s] = nb > 0 ? W : 0.0;
+            const bool valid = !(fabs(wsum[s]) < MCPT_EPS);
+            target[s] = bperm_f64(ul, 4 * s + g) * wsum[s];
+            uint64_t m[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                m[k] = __ballot(valid && 16 * k + gl < nb && bv[s][k] >= target[s] && bv[s][k] > 0.0);
+            kb[s] = group_first(m, g);
+            const int lb = max(kb[s] - 1, 0);
+            const double b = bperm_f64(sel4(bv[s], lb >> 4), g0 + (lb & 15));
+            base[s] = kb[s] > 0 ? b : 0.0;
+        }
+        // the picked batch's signed in-batch prefixes and its 64 list entries
+        double wc[kPickSlots][4];
+        int lj[kPickSlots][4];
+#pragma unroll
+        for (int s = 0; s < kPickSlots; s++) {
+            const size_t off = (size_t)px[s] * C.lstride + 64 * max(kb[s], 0) + gl;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool act = kb[s] >= 0 && 64 * kb[s] + 16 * k + gl < inf[s].y;
+                wc[s][k] = act ? C.w[off + 16 * k] : -0.0;
+                lj[s][k] = act ? (int)C.lst[off + 16 * k] : -1;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < kPickSlots; s++) {
+            uint64_t cm[4], om[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool ok = !signbit(wc[s][k]);
+                cm[k] = __ballot(ok && (base[s] + fabs(wc[s][k]) >= target[s]));
+                om[k] = __ballot(ok);
+            }
+            int pl = group_first(cm, g);
+            if (pl < 0) pl = group_last(om, g);
+            double margin = INFINITY;
+            int pick = -1;
+            {
+                const int l1 = max(pl, 0), l0 = max(pl - 1, 0);
+                double sc[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) sc[k] = fabs(wc[s][k]);
+                const double s1 = bperm_f64(sel4(sc, l1 >> 4), g0 + (l1 & 15));
+                const double s0 = bperm_f64(sel4(sc, l0 >> 4), g0 + (l0 & 15));
+                const int pk = bperm_i32(sel4(lj[s], l1 >> 4), g0 + (l1 & 15));
+                if (pl >= 0) {  // pick_margin's terms
+                    const double c_hi = base[s] + s1;
+                    const double c_lo = pl > 0 ? base[s] + s0 : base[s];
+                    const double m_lo = c_lo == 0.0 ? INFINITY : target[s] - c_lo;
+                    margin = fmin(m_lo, c_hi - target[s]);
+                    pick = pk;
+                }
+            }
+            const int node = n0 + 4 * s + g;
+            if (gl == 0 && node < n) {
+                wsum_out[node] = wsum[s];
+                pick_out[node] = pick;
+                if (C.exact) {  // exact pick: the band stored by the cache build + this sum's rounding
+                    const double band = (double)__int_as_float(inf[s].w) + band_round(inf[s].y, wsum[s]);
+                    if (!(pick_slack(margin, wsum[s]) > band)) {
+                        const int q = atomicAdd(C.exact, 1);
+                        C.exact[kExactHead + q] = C.exact_off + node;
+                    }
+                }
+            }
+        }
+        cached += (unsigned long long)min(kR, n - n0);
+    }
+    if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
+}
+
 // Exact pick, the band test's second half (lane per listed node): the per-chunk term
 // of the band against the slack of each node band_candidate listed (k_prep_pk2 / k_prep: margin less
 // the slivers' and the rounding terms, not above the whole-table bound), from the node's candidate
@@ -4280,10 +4445,17 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     PrepCache pr = pc;
                     pr.exact = exact_list;
                     pr.exact_off = nc;
-                    const int blocks = std::max(1, std::min((nr + 4 * kPickNodes - 1) / (4 * kPickNodes), 8192));
-                    hipLaunchKernelGGL(k_prep_pick, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
-                                       cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats, nchunks,
-                                       pr);
+                    if (MCPT_PICK_GROUPS && nchunks <= 64) {  // 16 lanes per root
+                        const int blocks = std::max(1, std::min((nr + 16 * kPickSlots - 1) / (16 * kPickSlots), 8192));
+                        hipLaunchKernelGGL(k_prep_pick_g, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
+                                           cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats,
+                                           nchunks, pr);
+                    } else {
+                        const int blocks = std::max(1, std::min((nr + 4 * kPickNodes - 1) / (4 * kPickNodes), 8192));
+                        hipLaunchKernelGGL(k_prep_pick, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
+                                           cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats,
+                                           nchunks, pr);
+                    }
                     HIP_OK(hipGetLastError());
                 }
             } else {
