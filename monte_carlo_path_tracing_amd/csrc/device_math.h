@@ -136,13 +136,17 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
     d3 axis = n;
     double theta, st, ct, sp, cp;
     double phi = 2 * MCPT_PI * k2;
+    // the lobes' acos and sincos(theta) taken once after the lobe-specific argument (the same values:
+    // theta = 0.5 acos(1 - 2 k1) or acos(k1^(1/(sh+1))); a wave with both lobes runs them once)
+    double carg;
+    if (ind == 0) carg = 1 - 2 * k1;
+    else carg = pow(k1, 1 / (sh + 1));
+    theta = acos(fmax(-1.0, fmin(1.0, carg)));
+    if (ind == 0) theta = 0.5 * theta;
+    sincos(theta, &st, &ct);
     if (ind == 0) {
-        theta = 0.5 * acos(fmax(-1.0, fmin(1.0, 1 - 2 * k1)));
-        sincos(theta, &st, &ct);
         pdf *= ct / MCPT_PI;
     } else {
-        theta = acos(fmax(-1.0, fmin(1.0, pow(k1, 1 / (sh + 1)))));
-        sincos(theta, &st, &ct);
         pdf *= (sh + 1) / (2 * MCPT_PI) * pow(k1, sh / (sh + 1));
         axis = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
     }

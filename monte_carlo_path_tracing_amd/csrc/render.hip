@@ -2235,13 +2235,16 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
 // flight, and the batch's 64 list entries (one more line) come with its weights instead of one
 // dependent load after the search.  Cross-lane reads inside a group are ds_bpermute.
 #ifndef MCPT_PICK_SLOTS
-#define MCPT_PICK_SLOTS 2
+#define MCPT_PICK_SLOTS 4  // roots per wave = 4 x slots (A/B: 2 slots at 7 waves 476.8-478.2, 4 slots at 4 waves 480.2-480.5)
+#endif
+#ifndef MCPT_PICK_PREFETCH
+#define MCPT_PICK_PREFETCH 1
 #endif
 #ifndef MCPT_PICK_GROUPS
 #define MCPT_PICK_GROUPS 1  // 0: k_prep_pick (wave per root) for every table size (A/B)
 #endif
 #ifndef MCPT_LB_PICKG
-#define MCPT_LB_PICKG 7  // 72 VGPRs at 2 slots without spills
+#define MCPT_LB_PICKG 4  // 121 VGPRs at 4 slots, no spills
 #endif
 constexpr int kPickSlots = MCPT_PICK_SLOTS;
 __device__ inline int bperm_i32(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
@@ -2290,15 +2293,22 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
     const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int nq = (nchunks + 15) >> 4;  // row entries per lane (<= 4)
     unsigned long long cached = 0;
+    // lane r < kR: root n0 + r (coalesced queue loads), fetched one iteration ahead so that the queue
+    // hop overlaps the previous roots' cache hops (MCPT_PICK_PREFETCH)
+    int f_px = 0, f_smp = 0;
+    uint64_t f_nid = 0;
+    auto fetch = [&](int m0) {
+        const int node = min(m0 + (lane & (kR - 1)), n - 1);
+        f_px = qpixel[node];
+        f_smp = qsample[node];
+        f_nid = qnode[node];
+    };
+    if (MCPT_PICK_PREFETCH && gw * kR < n) fetch(gw * kR);
     for (int n0 = gw * kR; n0 < n; n0 += waves * kR) {
-        // lane r < kR: root n0 + r (coalesced queue loads) and its pick uniform (dim 1)
-        int pxl;
-        double ul;
-        {
-            const int node = min(n0 + (lane & (kR - 1)), n - 1);
-            pxl = qpixel[node];
-            ul = counter_u(counter_key(seed, (uint64_t)pxl, (uint64_t)qsample[node], qnode[node]), 1);
-        }
+        if (!MCPT_PICK_PREFETCH) fetch(n0);
+        const int pxl = f_px;
+        const double ul = counter_u(counter_key(seed, (uint64_t)pxl, (uint64_t)f_smp, f_nid), 1);  // dim 1
+        if (MCPT_PICK_PREFETCH && n0 + waves * kR < n) fetch(n0 + waves * kR);
         // slot s: group g takes root 4 s + g; its row of batch totals (inclusive scan) and info
         int px[kPickSlots];
         int4 inf[kPickSlots];
