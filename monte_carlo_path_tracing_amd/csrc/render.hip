@@ -2681,17 +2681,22 @@ struct Aux {
 // prep state (x, N, weights_sum); then L = L_light + L_brdf with the reference's operation order
 // (main.cpp:464, :491) and the node reports to its parent (the root splats L / spp).  Expansion is
 // unchanged (it needs no weights), so the wavefront stays as wide as before.
+// A slot's fields that k_mis_combine writes together and k_mis_complete reads together share one
+// 128-B record (one line per slot instead of five scattered int arrays plus an 80-B w straddling two
+// lines; slot ids from the free ring are random, so every field touched costs a line):
+//   int [0] par  parent code: slot * 4 + role * 2 (0 light, 1 BRDF child) + need; -1 = root (need: some
+//                ancestor will evaluate a light pdf at this subtree's path-end state)
+//   int [1] pix  pixel (root splat)
+//   int [2] fl   bit0 light child shading, bit1 BRDF child shading, bit2 BRDF child emitter, bit3 BRDF
+//                edge, bit4 this node's path-end state is needed (its own parent code's need bit)
+//   int [3] li   light triangle along the BRDF direction (light-only ray) or -1
+//   double [2, 12)  w: brdf of the light edge [3], its scalar s1, brdf of the BRDF edge [3], pdf, cos, s2
+//   double [12, 15) Lb: BRDF child's radiance (or its emitter's emission)
+constexpr int kSlotRec = 16;  // doubles per slot record
 struct Slots {
-    int* par;      // parent code: slot * 4 + role * 2 (0 light, 1 BRDF child) + need; -1 = root (need:
-                   // some ancestor will evaluate a light pdf at this subtree's path-end state)
-    int* pix;      // pixel (root splat)
-    int* pend;     // shading children still to report
-    int* fl;       // bit0 light child shading, bit1 BRDF child shading, bit2 BRDF child emitter, bit3 BRDF edge,
-                   // bit4 this node's path-end state is needed (its own parent code's need bit)
-    int* li;       // light triangle along the BRDF direction (light-only ray) or -1
-    double* w;     // 10 per slot: brdf of the light edge [3], its scalar s1, brdf of the BRDF edge [3], pdf, cos, s2
+    double* rec;   // kSlotRec doubles per slot (above)
+    int* pend;     // shading children still to report (atomics: its own array)
     double* Ll;    // 3: light child's radiance (or the light edge's finished contribution)
-    double* Lb;    // 3: BRDF child's radiance (or its emitter's emission)
     double* last;  // 14: path-end prep state (x, N, weights_sum) reported by the light / BRDF child
     // Allocation, freeing and the ready lists are split over kSlotShards shards, each with its own
     // counters on its own 64-B line: a single counter word saturates at ~88 atomics/us
@@ -2743,7 +2748,7 @@ __device__ inline void mis_report(const Params& P, const Slots& T, bool act, int
     } else if (act) {
         ps = par >> 2;
         const int role = (par >> 1) & 1;
-        double* dl = (role ? T.Lb : T.Ll) + 3 * (size_t)ps;
+        double* dl = role ? T.rec + kSlotRec * (size_t)ps + 12 : T.Ll + 3 * (size_t)ps;
         dl[0] = L.x, dl[1] = L.y, dl[2] = L.z;
         if (par & 1) {
             double* ds = T.last + 14 * (size_t)ps + 7 * role;
@@ -3202,18 +3207,16 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         mis_report(P, T, active && !hold, pc, pixel, add(Llight, Lbr), own, rp);
         if (active && hold) {
             const size_t q = (size_t)slot;
-            T.par[q] = pc;
-            T.pix[q] = pixel;
             T.pend[q] = (int)lsh + (int)bsh;
-            T.fl[q] = (int)lsh | ((int)bsh << 1) | ((e2.kind == 1) << 2) | ((int)c2 << 3) | ((int)need << 4);
-            T.li[q] = li;
-            double* w = T.w + 10 * q;
+            double* r = T.rec + kSlotRec * q;
+            *reinterpret_cast<int4*>(r) = make_int4(pc, pixel,
+                                                    (int)lsh | ((int)bsh << 1) | ((e2.kind == 1) << 2) | ((int)c2 << 3) | ((int)need << 4),
+                                                    li);
+            double* w = r + 2;
             w[0] = w1.x, w[1] = w1.y, w[2] = w1.z, w[3] = A.s1[ii];
             w[4] = w2.x, w[5] = w2.y, w[6] = w2.z, w[7] = pdf, w[8] = cosb, w[9] = s2;
             if (!lsh) T.Ll[3 * q] = Llight.x, T.Ll[3 * q + 1] = Llight.y, T.Ll[3 * q + 2] = Llight.z;
-            if (e2.kind == 1)
-                T.Lb[3 * q] = S.light_rad[3 * e2.li], T.Lb[3 * q + 1] = S.light_rad[3 * e2.li + 1],
-                T.Lb[3 * q + 2] = S.light_rad[3 * e2.li + 2];
+            if (e2.kind == 1) r[12] = S.light_rad[3 * e2.li], r[13] = S.light_rad[3 * e2.li + 1], r[14] = S.light_rad[3 * e2.li + 2];
         }
         // the light child's path end is needed by this node's stale BRDF-edge pdf, and by whoever
         // needs this node's path end when the light child is on this node's path (no shading BRDF child)
@@ -3232,7 +3235,26 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
 // node reports to its parent (ready list 1 - rp_in) -- one tree level per pass, in step with the
 // wavefront; grid-stride over the device-side count
 // grid: x blocks per shard, y = ready-list shard
-__global__ __launch_bounds__(256, MCPT_LB_COMPLETE) void k_mis_complete(Params P, Slots T, int rp_in) {
+// MCPT_COMPLETE_SPLIT=1 (A/B only): the BRDF edge's stale light pdf (the literal survival chain, the
+// register peak: 141 VGPRs) evaluated by k_mis_lpdf over the same ready list first and left in w[9], so
+// k_mis_complete itself runs at 8 waves/SIMD over twice the grid.  Same-box A/B with the slot records
+// (profiles/round3_ab_slot_rec.txt): MIS 488.0-491.0 split vs 492.0-493.0 not (k_mis_complete 121 ->
+// 74 ms per profile run, but k_mis_lpdf adds 22 ms and a launch per pass)
+#ifndef MCPT_COMPLETE_SPLIT
+#define MCPT_COMPLETE_SPLIT 0
+#endif
+__global__ __launch_bounds__(256, MCPT_LB_COMPLETE) void k_mis_lpdf(Params P, Slots T, int rp_in) {
+    const DScene& S = P.S;
+    const unsigned n = T.ctrl[16 * blockIdx.y + 4 + rp_in];
+    const int* ready = (rp_in ? T.ready1 : T.ready0) + (size_t)blockIdx.y * T.ready_cap;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        double* rc = T.rec + kSlotRec * (size_t)ready[i];
+        const int4 hdr = *reinterpret_cast<const int4*>(rc);
+        if ((hdr.z & 1) && (hdr.z & 8))
+            rc[11] = rc[10] / (rc[9] + state_light_pdf(S, hdr.w, T.last + 14 * (size_t)ready[i])) / MCPT_P_RR;
+    }
+}
+__global__ __launch_bounds__(256, MCPT_COMPLETE_SPLIT ? 8 : MCPT_LB_COMPLETE) void k_mis_complete(Params P, Slots T, int rp_in) {
     const DScene& S = P.S;
     const unsigned n = T.ctrl[16 * blockIdx.y + 4 + rp_in];
     const int* ready = (rp_in ? T.ready1 : T.ready0) + (size_t)blockIdx.y * T.ready_cap;
@@ -3242,8 +3264,10 @@ __global__ __launch_bounds__(256, MCPT_LB_COMPLETE) void k_mis_complete(Params P
         const unsigned i = base + lane_id();
         const bool act = i < n;
         const size_t q = act ? (size_t)ready[i] : 0;
-        const int fl = act ? T.fl[q] : 0;
-        const double* w = T.w + 10 * q;
+        const double* rc = T.rec + kSlotRec * q;
+        const int4 hdr = act ? *reinterpret_cast<const int4*>(rc) : make_int4(-1, 0, 0, -1);
+        const int fl = hdr.z;
+        const double* w = rc + 2;
         const bool lsh = fl & 1, bsh = fl & 2;
         d3 L = mk3(0, 0, 0);
         double stc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -3253,17 +3277,18 @@ __global__ __launch_bounds__(256, MCPT_LB_COMPLETE) void k_mis_complete(Params P
             const d3 Llight = lsh ? mul(hmul(Ll, mk3(w[0], w[1], w[2])), w[3]) : Ll;
             const double* last_l = T.last + 14 * q;
             double s2 = w[9];
-            if (lsh && (fl & 8)) s2 = w[8] / (w[7] + state_light_pdf(S, T.li[q], last_l)) / MCPT_P_RR;  // stale state
+            if (!MCPT_COMPLETE_SPLIT && lsh && (fl & 8))  // stale state (k_mis_lpdf stores it in w[9] when split)
+                s2 = w[8] / (w[7] + state_light_pdf(S, hdr.w, last_l)) / MCPT_P_RR;
             d3 Lbr = mk3(0, 0, 0);
-            if (bsh || (fl & 4)) Lbr = mul(hmul(mk3(T.Lb[3 * q], T.Lb[3 * q + 1], T.Lb[3 * q + 2]), mk3(w[4], w[5], w[6])), s2);
+            if (bsh || (fl & 4)) Lbr = mul(hmul(mk3(rc[12], rc[13], rc[14]), mk3(w[4], w[5], w[6])), s2);
             L = add(Llight, Lbr);
             if (fl & 16) {  // this subtree's path end, for an ancestor
                 const double* st = bsh ? last_l + 7 : last_l;
 #pragma unroll
                 for (int k = 0; k < 7; k++) stc[k] = st[k];
             }
-            par = T.par[q];
-            pix = T.pix[q];
+            par = hdr.x;
+            pix = hdr.y;
         }
         const int fs = wave_shard();
         const int r = wave_append(&T.ctrl[16 * fs + 2], act);  // free the slot
@@ -3905,8 +3930,8 @@ int alloc_aux(DevBuf* b, int cap, Aux& a) {
 // idle: each shard's ring entries [head, tail) are re-packed from 0, its ready list rp keeps its
 // entries; slot ids stay valid).
 constexpr int kSlotArrays = 13;
-int slot_bytes_per(int k) {  // par pix pend fl li | w Ll Lb last
-    static const int b[9] = {4, 4, 4, 4, 4, 80, 24, 24, 112};
+int slot_bytes_per(int k) {  // rec - pend - - - Ll - last (arrays 1, 3, 4, 5, 7 unused)
+    static const int b[9] = {8 * kSlotRec, 0, 4, 0, 0, 0, 24, 0, 112};
     return b[k];
 }
 size_t slot_array_bytes(int k, int rcap) {
@@ -3917,8 +3942,7 @@ size_t slot_array_bytes(int k, int rcap) {
     return kCtrlBytes;
 }
 void slots_view(DevBuf* b, int rcap, Slots& T) {
-    T.par = (int*)b[0].p, T.pix = (int*)b[1].p, T.pend = (int*)b[2].p, T.fl = (int*)b[3].p, T.li = (int*)b[4].p;
-    T.w = (double*)b[5].p, T.Ll = (double*)b[6].p, T.Lb = (double*)b[7].p, T.last = (double*)b[8].p;
+    T.rec = (double*)b[0].p, T.pend = (int*)b[2].p, T.Ll = (double*)b[6].p, T.last = (double*)b[8].p;
     T.ring = (int*)b[9].p, T.ready0 = (int*)b[10].p, T.ready1 = (int*)b[11].p, T.ctrl = (unsigned*)b[12].p;
     T.rcap = rcap;
     T.cap = rcap * kSlotShards;
@@ -4524,7 +4548,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             hipLaunchKernelGGL(stale ? k_mis_combine<true> : k_mis_combine<false>, g256, b256, 0, st, P, *cur, ni, aux,
                                *nxt, T, rp);
             if (stale) {  // one level of the bottom-up reduction per generation
-                hipLaunchKernelGGL(k_mis_complete, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
+                if (MCPT_COMPLETE_SPLIT) hipLaunchKernelGGL(k_mis_lpdf, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
+                hipLaunchKernelGGL(k_mis_complete, dim3(MCPT_COMPLETE_SPLIT ? 64 : 32, kSlotShards), dim3(256), 0, st, P, T, rp);
                 hipLaunchKernelGGL(k_slot_fixup, dim3(1), dim3(kSlotShards), 0, st, T, rp);
                 rp ^= 1;
             }
@@ -4573,7 +4598,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         unsigned pending = 0;
         for (int sh = 0; sh < kSlotShards; sh++) pending += hctrl[16 * sh + 4 + rp];
         if (pending == 0) break;
-        hipLaunchKernelGGL(k_mis_complete, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
+        if (MCPT_COMPLETE_SPLIT) hipLaunchKernelGGL(k_mis_lpdf, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
+        hipLaunchKernelGGL(k_mis_complete, dim3(MCPT_COMPLETE_SPLIT ? 64 : 32, kSlotShards), dim3(256), 0, st, P, T, rp);
         hipLaunchKernelGGL(k_slot_fixup, dim3(1), dim3(kSlotShards), 0, st, T, rp);
         rp ^= 1;
     }
