@@ -379,10 +379,14 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     // form computes, and the per-node min/max pairs go away.  Empty child slots (lo = FLT_MAX,
     // hi = -FLT_MAX, collapse_bvh4) then give t0 >= FLT_MAX > t1 for any |inverse| >= 1 (a unit
     // direction's), so they miss without a child-code test.
+#if MCPT_NODE_OFFSETS
     const unsigned nx = MCPT_SLAB_NEARFAR && ix < 0 ? 48u : 0u, ny = MCPT_SLAB_NEARFAR && iy < 0 ? 64u : 16u,
                    nz = MCPT_SLAB_NEARFAR && iz < 0 ? 80u : 32u;
-    const bool sx = ix < 0, sy = iy < 0, sz = iz < 0;  // MCPT_SLAB_SELECT
     const unsigned fx = 48u - nx, fy = 80u - ny, fz = 112u - nz;
+#endif
+#if MCPT_SLAB_SELECT
+    const bool sx = ix < 0, sy = iy < 0, sz = iz < 0;
+#endif
     // tlimit0: at least the t of a triangle tri_hit accepts (or FLT_MAX) -- boxes beyond it hold no
     // closest hit
     float tlimit = tlimit0;
@@ -429,10 +433,11 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
             float t[4];
             int code[4];
             // 32-bit byte offsets from the (wave-uniform) tree base: one v_or per load
-            const unsigned noff = (unsigned)node * (unsigned)sizeof(BvhNode4);
             // loads + four slab tests, instantiated once per address space so that the two paths
             // join on (t, code) rather than on the 28 loaded dwords (a join on those made the
             // compiler wait for the first loads before issuing the rest)
+#if MCPT_NODE_OFFSETS
+            const unsigned noff = (unsigned)node * (unsigned)sizeof(BvhNode4);
             auto visit = [&](const BvhNode4* base) {
                 const char* b = reinterpret_cast<const char*>(base);
                 auto at = [&](unsigned o) { return *reinterpret_cast<const float4*>(b + (noff + o)); };
@@ -462,7 +467,6 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
             };
             // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch,
             // so each side reads one address space: ds_read from the LDS copy, global loads else)
-#if MCPT_NODE_OFFSETS
             if (kTop > 0 && __all(node < kTop)) visit(top);
             else visit(nodes);
 #else  // A/B: the round-2 loads (a 64-bit node pointer, fixed lo / hi offsets)
@@ -891,8 +895,36 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 // pixel-major with the block's samples of a pixel consecutive (group 1 = sample-major over the frame,
 // group nsamp = fully sample-minor: a pixel's samples leave one point, coherent traversal of a BVH
 // that misses L2)
+// Per-pixel root table (k_root_table, once per call): a root's entry (main.cpp:406-437 at the primary
+// hit) is the same for every sample of its pixel except the Russian roulette draw, so the point, normal
+// and wo (9 doubles) and the kind (-2 nothing: miss or back face, -1 shading, >= 0 emitter li) are
+// computed once per pixel with the same functions, and k_roots only draws RR and appends.
+#ifndef MCPT_ROOT_TABLE
+#define MCPT_ROOT_TABLE 0
+#endif
+struct RootTab {
+    double* pnw;  // [npx][9]: p, N, wo
+    int* kind;    // [npx]
+};
+__global__ __launch_bounds__(256) void k_root_table(DScene S, CamFrame cam, const int* hit_f, const double* hit_tbg, RootTab rt) {
+    const int px = blockIdx.x * blockDim.x + threadIdx.x;
+    if (px >= cam.W * cam.H) return;
+    const int f = hit_f[px];
+    d3 p = mk3(0, 0, 0), N = mk3(0, 0, 0), wo = mk3(0, 0, 0);
+    int kind = -2;
+    if (f >= 0) {
+        wo = mul(cam_dir(cam, px / cam.W, px % cam.W), -1);
+        node_point(S, f, hit_tbg[3 * px + 1], hit_tbg[3 * px + 2], &p, &N);
+        if (!(dot(N, wo) < 0)) kind = S.tri_light[f] >= 0 ? S.tri_light[f] : -1;
+    }
+    double* o = rt.pnw + 9 * (size_t)px;
+    o[0] = p.x, o[1] = p.y, o[2] = p.z, o[3] = N.x, o[4] = N.y, o[5] = N.z, o[6] = wo.x, o[7] = wo.y, o[8] = wo.z;
+    rt.kind[px] = kind;
+}
+
 __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
-                                               int s0, long long rbase, int nroots, Queue q, int group, int nsamp) {
+                                               int s0, long long rbase, int nroots, Queue q, int group, int nsamp,
+                                               RootTab rt) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int npx = cam.W * cam.H;
     bool active = r < nroots;
@@ -902,7 +934,18 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
     if (active) {
         const long long rg = rbase + r;  // root index within the call
         const long long full = (long long)(nsamp / group) * group * npx;  // roots in whole blocks
-        if (rg < full) {
+        if (full < (1ll << 31)) {  // uniform: 32-bit division (a 64-bit one is a long emulated sequence)
+            const unsigned gn = (unsigned)group * (unsigned)npx, ur = (unsigned)rg;
+            if (rg < full) {
+                const unsigned blk = ur / gn, idx = ur - blk * gn;
+                pixel = (int)(idx / (unsigned)group);
+                sample = s0 + (int)blk * group + (int)(idx - (unsigned)pixel * (unsigned)group);
+            } else {
+                const unsigned gt = (unsigned)(nsamp % group), idx = ur - (unsigned)full;
+                pixel = (int)(idx / gt);
+                sample = s0 + (nsamp / group) * group + (int)(idx - (unsigned)pixel * gt);
+            }
+        } else if (rg < full) {
             const long long blk = rg / ((long long)group * npx), idx = rg - blk * group * npx;
             pixel = (int)(idx / group);
             sample = s0 + (int)blk * group + (int)(idx % group);
@@ -914,13 +957,39 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
         }
         f = hit_f[pixel];
         active = f >= 0;
-        if (active) {
+        if (active && !rt.pnw) {
             beta = hit_tbg[3 * pixel + 1];
             gamma = hit_tbg[3 * pixel + 2];
             wo = mul(cam_dir(cam, pixel / cam.W, pixel % cam.W), -1);
         }
     }
-    node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
+    if (!rt.pnw) {
+        node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
+        return;
+    }
+    // entry_eval from the pixel's table row: the same point, normal and kind; RR (dim 0) per sample
+    Entry e{0, -1, mk3(0, 0, 0), mk3(0, 0, 0)};
+    const int kind = active ? rt.kind[pixel] : -2;
+    if (kind >= 0) {
+        e.kind = 1;
+        e.li = kind;
+    } else if (kind == -1) {
+        if (P.mode == MCPT_MODE_SHADE || P.mode == MCPT_MODE_SHADE_AREA) e.kind = 2;
+        else e.kind = counter_u(counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, 1), 0) > MCPT_P_RR ? 0 : 2;
+    }
+    if (e.kind == 2) {
+        const double* t = rt.pnw + 9 * (size_t)pixel;
+        e.p = mk3(t[0], t[1], t[2]);
+        e.N = mk3(t[3], t[4], t[5]);
+        wo = mk3(t[6], t[7], t[8]);
+    } else if (e.kind == 1) {
+        const DScene& S = P.S;
+        double* px = P.fb + 3 * (size_t)pixel;
+        unsafeAtomicAdd(px + 0, S.light_rad[3 * e.li + 0] * P.inv_spp);
+        unsafeAtomicAdd(px + 1, S.light_rad[3 * e.li + 1] * P.inv_spp);
+        unsafeAtomicAdd(px + 2, S.light_rad[3 * e.li + 2] * P.inv_spp);
+    }
+    queue_push(P, e.kind == 2, e, f, wo, mk3(1, 1, 1), pixel, sample, 1, -1, q);
 }
 
 // moves nodes [sb, sb + m) of src to [db, db + m) of dst (every field a generation carries into the
@@ -2282,6 +2351,23 @@ __device__ inline int group_last(const uint64_t (&m)[4], int g) {
     }
     return r;
 }
+// the same first / last searches by a 16-lane row reduction (DPP row_ror butterflies: four VALU each)
+// on per-lane candidate indices instead of decoding the ballot masks lane by lane
+#ifndef MCPT_PICK_DPP
+#define MCPT_PICK_DPP 0
+#endif
+__device__ inline unsigned row_min_u32(unsigned v) {
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false));  // row_ror:4
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false));  // row_ror:2
+    return min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false));  // row_ror:1
+}
+__device__ inline int row_max_i32(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x122, 0xf, 0xf, false));
+    return max(v, __builtin_amdgcn_update_dpp(0, v, 0x121, 0xf, 0xf, false));
+}
 __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
                                                      const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                      double* __restrict__ wsum_out, int* __restrict__ pick_out,
@@ -2331,11 +2417,20 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
             wsum[s] = nb > 0 ? W : 0.0;
             const bool valid = !(fabs(wsum[s]) < MCPT_EPS);
             target[s] = bperm_f64(ul, 4 * s + g) * wsum[s];
-            uint64_t m[4];
+            if (MCPT_PICK_DPP) {
+                unsigned c = 64;
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                m[k] = __ballot(valid && 16 * k + gl < nb && bv[s][k] >= target[s] && bv[s][k] > 0.0);
-            kb[s] = group_first(m, g);
+                for (int k = 3; k >= 0; k--)
+                    c = valid && 16 * k + gl < nb && bv[s][k] >= target[s] && bv[s][k] > 0.0 ? 16 * k + gl : c;
+                c = row_min_u32(c);
+                kb[s] = c < 64 ? (int)c : -1;
+            } else {
+                uint64_t m[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    m[k] = __ballot(valid && 16 * k + gl < nb && bv[s][k] >= target[s] && bv[s][k] > 0.0);
+                kb[s] = group_first(m, g);
+            }
             const int lb = max(kb[s] - 1, 0);
             const double b = bperm_f64(sel4(bv[s], lb >> 4), g0 + (lb & 15));
             base[s] = kb[s] > 0 ? b : 0.0;
@@ -2355,15 +2450,30 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
         }
 #pragma unroll
         for (int s = 0; s < kPickSlots; s++) {
-            uint64_t cm[4], om[4];
+            int pl;
+            if (MCPT_PICK_DPP) {
+                unsigned cf = 64;
+                int cl = -1;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool ok = !signbit(wc[s][k]);
-                cm[k] = __ballot(ok && (base[s] + fabs(wc[s][k]) >= target[s]));
-                om[k] = __ballot(ok);
+                for (int k = 3; k >= 0; k--) {
+                    const bool ok = !signbit(wc[s][k]);
+                    cf = ok && (base[s] + fabs(wc[s][k]) >= target[s]) ? 16 * k + gl : cf;
+                    cl = ok && cl < 0 ? 16 * k + gl : cl;  // the highest k wins
+                }
+                cf = row_min_u32(cf);
+                const int lastv = row_max_i32(cl);  // every lane of the row takes part in the DPP steps
+                pl = cf < 64 ? (int)cf : lastv;
+            } else {
+                uint64_t cm[4], om[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const bool ok = !signbit(wc[s][k]);
+                    cm[k] = __ballot(ok && (base[s] + fabs(wc[s][k]) >= target[s]));
+                    om[k] = __ballot(ok);
+                }
+                pl = group_first(cm, g);
+                if (pl < 0) pl = group_last(om, g);
             }
-            int pl = group_first(cm, g);
-            if (pl < 0) pl = group_last(om, g);
             double margin = INFINITY;
             int pick = -1;
             {
@@ -2795,7 +2905,6 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
     d3 coord;
     double lprob = 1;
     if (pick >= 0) {
-        const double4 ln = S.lt_n[pick];
         SphTri sph;
         pick_sph(S, pick, p, N, &sph);
         const d3 Pd = arvo_sample(sph, counter_u(key, 2), counter_u(key, 3));
@@ -3586,7 +3695,7 @@ struct DeviceState {
     std::vector<void*> allocs;
     hipStream_t stream = nullptr;
     // reusable work buffers
-    DevBuf hit_f, hit_tbg, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[9], sl[13], cache_bt, cache_lst, cache_info, cache_w, masks;
+    DevBuf hit_f, hit_tbg, root_pnw, root_kind, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[9], sl[13], cache_bt, cache_lst, cache_info, cache_w, masks;
     DevBuf exact, exact_scr, slack;  // exact pick: list, k_prep_exact's scratch, per-node slack
     DevBuf lit_slot, lit_pool;        // exact pick: roots' literal sums per pixel (RootLit)
     int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
@@ -4216,7 +4325,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int target = (int)std::max<long long>(target_ll, 1);
     const int cap = (int)std::min<long long>((long long)qf * target + 1024, (1ll << 30));
     int rc;
-    if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) || (rc = ensure(D.stats, 128)) ||
+    if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) ||
+        (MCPT_ROOT_TABLE && ((rc = ensure(D.root_pnw, 72ull * npx)) || (rc = ensure(D.root_kind, 4ull * npx)))) || (rc = ensure(D.stats, 128)) ||
         (rc = ensure(D.work, 256)))
         return rc;
     Queue qa, qb;
@@ -4320,6 +4430,14 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     hipLaunchKernelGGL(grid ? k_primary<true> : k_primary<false>, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock),
                        0, st, D.d, cf, (int*)D.hit_f.p, (double*)D.hit_tbg.p);
     HIP_OK(hipGetLastError());
+    RootTab rtab{};
+    if (MCPT_ROOT_TABLE) {
+        rtab.pnw = (double*)D.root_pnw.p;
+        rtab.kind = (int*)D.root_kind.p;
+        hipLaunchKernelGGL(k_root_table, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
+                           (const double*)D.hit_tbg.p, rtab);
+        HIP_OK(hipGetLastError());
+    }
     if (pc.use) {
         HIP_OK(hipMemsetAsync(qb.count, 0, 4, st));
         hipLaunchKernelGGL(k_root_points, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
@@ -4426,7 +4544,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (rnext < R && n < (unsigned)fill) {  // refill with roots (appended through node_entry)
             const int m = (int)std::min<long long>((long long)fill - n, R - rnext);
             hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
-                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0);
+                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab);
             HIP_OK(hipGetLastError());
             rnext += m;
             if ((rc = read_count(&n))) return rc;
@@ -5156,7 +5274,8 @@ void mcpt_scene_destroy(mcpt_scene* sc) {
         (void)hipSetDevice(D->device);
         for (void* p : D->allocs) (void)hipFree(p);
         std::vector<DevBuf*> bufs = {&D->hit_f, &D->hit_tbg, &D->fb, &D->rank_fb, &D->stats, &D->work, &D->cache_bt, &D->cache_lst,
-                                     &D->cache_info, &D->cache_w, &D->masks, &D->g_start, &D->g_tri};
+                                     &D->cache_info, &D->cache_w, &D->masks, &D->g_start, &D->g_tri, &D->root_pnw,
+                                     &D->root_kind, &D->exact, &D->exact_scr, &D->slack, &D->lit_slot, &D->lit_pool};
         for (int k = 0; k < 14; k++) bufs.insert(bufs.end(), {&D->qa[k], &D->qb[k], &D->qs[k]});
         for (int k = 0; k < 9; k++) bufs.push_back(&D->aux[k]);
         for (int k = 0; k < 13; k++) bufs.push_back(&D->sl[k]);
