@@ -86,18 +86,17 @@ __host__ __device__ inline double acos_newton_corr(double x, double y0) {
 #endif
 }
 
+// Both signs share one libm acos and one correction on |x| (a SIMD wave with lanes of both signs ran
+// two of each when the sign picked a branch); the sign selects only the final combination.
 __host__ __device__ inline double acos_cr(double x) {
     if (x >= 1.0) return 0.0;
     if (x <= -1.0) return 0x1.921fb54442d18p+1;  // pi rounded, = acos(-1)
     if (!(x == x)) return x;
-    if (x >= 0.0) {
-        const double y0 = acos(x);
-        return y0 + acos_newton_corr(x, y0);
-    }
-    const double y0 = acos(-x);
-    const double c = acos_newton_corr(-x, y0);
+    const double ax = fabs(x);
+    const double y0 = acos(ax);
+    const double c = acos_newton_corr(ax, y0);
     const DD d = dd_two_sum(0x1.921fb54442d18p+1, -y0);  // pi_hi - y0, exactly
-    return d.h + ((d.l + 0x1.1a62633145c07p-53) - c);
+    return x >= 0.0 ? y0 + c : d.h + ((d.l + 0x1.1a62633145c07p-53) - c);
 }
 
 }  // namespace mcpt

@@ -899,6 +899,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 // hit) is the same for every sample of its pixel except the Russian roulette draw, so the point, normal
 // and wo (9 doubles) and the kind (-2 nothing: miss or back face, -1 shading, >= 0 emitter li) are
 // computed once per pixel with the same functions, and k_roots only draws RR and appends.
+// MCPT_ROOT_TABLE=1 (A/B only): same-box A/B (profiles/round3_ab_acos_dpp_roottab.txt) left k_roots at
+// 111-112 ms per profile run -- the kernel is bound by its queue writes, not by node_point / the
+// 64-bit index math -- and MIS within noise (470.8 / 468.3 vs 468.7 / 469.6 without)
 #ifndef MCPT_ROOT_TABLE
 #define MCPT_ROOT_TABLE 0
 #endif
@@ -2354,7 +2357,7 @@ __device__ inline int group_last(const uint64_t (&m)[4], int g) {
 // the same first / last searches by a 16-lane row reduction (DPP row_ror butterflies: four VALU each)
 // on per-lane candidate indices instead of decoding the ballot masks lane by lane
 #ifndef MCPT_PICK_DPP
-#define MCPT_PICK_DPP 0
+#define MCPT_PICK_DPP 1
 #endif
 __device__ inline unsigned row_min_u32(unsigned v) {
     v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
