@@ -836,10 +836,36 @@ __device__ inline Entry entry_eval(const Params& P, bool active, int f, double b
     }
     return e;
 }
+// block_append for two kinds of items with ONE atomic: the block's a-items, then its b-items, each in
+// lane order.  Must be called by every thread of the workgroup (it contains barriers).
+__device__ inline int2 block_append2(unsigned* counter, bool wa, bool wb) {
+    __shared__ unsigned s_ca[16], s_cb[16];
+    __shared__ unsigned s_base, s_ta;
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    const uint64_t ma = __ballot(wa), mb = __ballot(wb);
+    if (lane == 0) s_ca[wid] = (unsigned)__popcll(ma), s_cb[wid] = (unsigned)__popcll(mb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned ta = 0, tb = 0;
+        for (int w = 0; w < nw; w++) {
+            const unsigned ca = s_ca[w], cb = s_cb[w];
+            s_ca[w] = ta, s_cb[w] = tb;
+            ta += ca, tb += cb;
+        }
+        s_ta = ta;
+        s_base = ta + tb ? atomicAdd(counter, ta + tb) : 0u;
+    }
+    __syncthreads();
+    const uint64_t below = lane == 0 ? 0ull : (~0ull) >> (64 - lane);
+    const int2 r = make_int2(wa ? (int)(s_base + s_ca[wid] + __popcll(ma & below)) : -1,
+                             wb ? (int)(s_base + s_ta + s_cb[wid] + __popcll(mb & below)) : -1);
+    __syncthreads();  // s_* are reused by the next call
+    return r;
+}
 // appends a shading node to q.  Must be called by ALL threads of the workgroup (block_append).
 __device__ inline void queue_push(const Params& P, bool push, const Entry& e, int f, d3 wo, d3 tp, int pixel, int sample,
-                                  uint64_t node, int par, Queue& q) {
-    const int slot = block_append(q.count, push);
+                                  uint64_t node, int par, Queue& q, int slot_given = -2) {
+    const int slot = slot_given == -2 ? block_append(q.count, push) : slot_given;
     if (!push) return;
     if (slot >= q.cap) {
         atomicOr((unsigned long long*)(P.stats + 4), 1ull);
@@ -899,11 +925,19 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 // hit) is the same for every sample of its pixel except the Russian roulette draw, so the point, normal
 // and wo (9 doubles) and the kind (-2 nothing: miss or back face, -1 shading, >= 0 emitter li) are
 // computed once per pixel with the same functions, and k_roots only draws RR and appends.
-// MCPT_ROOT_TABLE=1 (A/B only): same-box A/B (profiles/round3_ab_acos_dpp_roottab.txt) left k_roots at
-// 111-112 ms per profile run -- the kernel is bound by its queue writes, not by node_point / the
-// 64-bit index math -- and MIS within noise (470.8 / 468.3 vs 468.7 / 469.6 without)
+// MCPT_ROOT_TABLE: roots from the per-pixel table by k_roots_t (kRootsPT roots per thread, one queue
+// atomic per 2 048 roots).  The table alone in k_roots (one atomic per 256 roots) changed nothing
+// (k_roots 111-112 ms per profile run, profiles/round3_ab_acos_dpp_roottab.txt): k_roots was bound by
+// the queue counter's atomic rate; with k_roots_t 112 -> 55 ms, MIS +1.7% same-box
+// (profiles/round3_ab_roots_batched.txt).  0: k_roots (node_entry per root).
 #ifndef MCPT_ROOT_TABLE
-#define MCPT_ROOT_TABLE 0
+#define MCPT_ROOT_TABLE 1
+#endif
+// MCPT_APPEND2=1 (A/B only): k_mis_combine takes both children's queue slots with one atomic per
+// workgroup instead of two -- MIS 488.0-488.5 vs 487.4-489.0 without (profiles/round3_ab_roots_batched.txt):
+// combine is not bound by its queue atomics
+#ifndef MCPT_APPEND2
+#define MCPT_APPEND2 0
 #endif
 struct RootTab {
     double* pnw;  // [npx][9]: p, N, wo
@@ -925,6 +959,101 @@ __global__ __launch_bounds__(256) void k_root_table(DScene S, CamFrame cam, cons
     rt.kind[px] = kind;
 }
 
+// pixel and sample of root rg (the call's root index; order above)
+__device__ inline void root_of(long long rg, int npx, int s0, int group, int nsamp, int* pixel, int* sample) {
+    const long long full = (long long)(nsamp / group) * group * npx;  // roots in whole blocks
+    if (full < (1ll << 31)) {  // uniform: 32-bit division (a 64-bit one is a long emulated sequence)
+        const unsigned gn = (unsigned)group * (unsigned)npx, ur = (unsigned)rg;
+        if (rg < full) {
+            const unsigned blk = ur / gn, idx = ur - blk * gn;
+            *pixel = (int)(idx / (unsigned)group);
+            *sample = s0 + (int)blk * group + (int)(idx - (unsigned)*pixel * (unsigned)group);
+        } else {
+            const unsigned gt = (unsigned)(nsamp % group), idx = ur - (unsigned)full;
+            *pixel = (int)(idx / gt);
+            *sample = s0 + (nsamp / group) * group + (int)(idx - (unsigned)*pixel * gt);
+        }
+    } else if (rg < full) {
+        const long long blk = rg / ((long long)group * npx), idx = rg - blk * group * npx;
+        *pixel = (int)(idx / group);
+        *sample = s0 + (int)blk * group + (int)(idx % group);
+    } else {
+        const int gt = nsamp % group;
+        const long long idx = rg - full;
+        *pixel = (int)(idx / gt);
+        *sample = s0 + (nsamp / group) * group + (int)(idx % gt);
+    }
+}
+
+// Roots from the per-pixel table, kRootsPT per thread: the queue's single counter word takes ~88
+// atomic adds per microsecond (MI355X_MICROARCH.md), and one block_append per 256 roots held k_roots at
+// that rate (~160 k appends, ~1.8 ms per 41 M-root refill).  Here a 256-thread block takes 256 x
+// kRootsPT roots with ONE atomic; sub-batch j (roots base + 256 j + thread) is compacted in order
+// and placed after sub-batches < j, so the queue order equals k_roots' and every store is coalesced.
+constexpr int kRootsPT = 8;
+__global__ __launch_bounds__(256) void k_roots_t(Params P, const int* __restrict__ hit_f, int npx, int s0, long long rbase,
+                                                 int nroots, Queue q, int group, int nsamp, RootTab rt) {
+    __shared__ unsigned s_w[kRootsPT][4];
+    __shared__ unsigned s_base;
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const int base = blockIdx.x * 256 * kRootsPT;
+    int px[kRootsPT], sm[kRootsPT];
+    uint64_t wm[kRootsPT];
+#pragma unroll
+    for (int j = 0; j < kRootsPT; j++) {
+        const int r = base + 256 * j + (int)threadIdx.x;
+        bool want = false;
+        px[j] = 0, sm[j] = 0;
+        if (r < nroots) {
+            root_of(rbase + r, npx, s0, group, nsamp, &px[j], &sm[j]);
+            const int kind = rt.kind[px[j]];
+            if (kind >= 0) {  // emitter: its emission (main.cpp:411-412 with throughput 1)
+                double* fb = P.fb + 3 * (size_t)px[j];
+                unsafeAtomicAdd(fb + 0, P.S.light_rad[3 * kind + 0] * P.inv_spp);
+                unsafeAtomicAdd(fb + 1, P.S.light_rad[3 * kind + 1] * P.inv_spp);
+                unsafeAtomicAdd(fb + 2, P.S.light_rad[3 * kind + 2] * P.inv_spp);
+            } else if (kind == -1) {  // shading node; RR dim 0 (MIS / BRDF), shade() draws it later
+                want = (P.mode == MCPT_MODE_SHADE || P.mode == MCPT_MODE_SHADE_AREA) ||
+                       !(counter_u(counter_key(P.seed, (uint64_t)px[j], (uint64_t)sm[j], 1), 0) > MCPT_P_RR);
+            }
+        }
+        wm[j] = __ballot(want);
+        if (lane == 0) s_w[j][wid] = (unsigned)__popcll(wm[j]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned run = 0;
+        for (int j = 0; j < kRootsPT; j++)
+            for (int w = 0; w < 4; w++) {
+                const unsigned c = s_w[j][w];
+                s_w[j][w] = run;
+                run += c;
+            }
+        s_base = run ? atomicAdd(q.count, run) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRootsPT; j++) {
+        if (!((wm[j] >> lane) & 1)) continue;
+        const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(wm[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)wm[j], 0u));
+        const size_t slot = (size_t)s_base + s_w[j][wid] + rk;
+        if (slot >= (size_t)q.cap) {
+            atomicOr((unsigned long long*)(P.stats + 4), 1ull);
+            continue;
+        }
+        const double* t = rt.pnw + 9 * (size_t)px[j];
+        st3(q.p, q.cap, slot, mk3(t[0], t[1], t[2]));
+        st3(q.n, q.cap, slot, mk3(t[3], t[4], t[5]));
+        st3(q.wo, q.cap, slot, mk3(t[6], t[7], t[8]));
+        st3(q.tp, q.cap, slot, mk3(1, 1, 1));
+        q.f[slot] = hit_f[px[j]];
+        q.pixel[slot] = px[j];
+        q.sample[slot] = sm[j];
+        q.node[slot] = 1;
+        q.par[slot] = -1;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
                                                int s0, long long rbase, int nroots, Queue q, int group, int nsamp,
                                                RootTab rt) {
@@ -935,29 +1064,7 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
     double beta = 0, gamma = 0;
     d3 wo = mk3(0, 0, 0);
     if (active) {
-        const long long rg = rbase + r;  // root index within the call
-        const long long full = (long long)(nsamp / group) * group * npx;  // roots in whole blocks
-        if (full < (1ll << 31)) {  // uniform: 32-bit division (a 64-bit one is a long emulated sequence)
-            const unsigned gn = (unsigned)group * (unsigned)npx, ur = (unsigned)rg;
-            if (rg < full) {
-                const unsigned blk = ur / gn, idx = ur - blk * gn;
-                pixel = (int)(idx / (unsigned)group);
-                sample = s0 + (int)blk * group + (int)(idx - (unsigned)pixel * (unsigned)group);
-            } else {
-                const unsigned gt = (unsigned)(nsamp % group), idx = ur - (unsigned)full;
-                pixel = (int)(idx / gt);
-                sample = s0 + (nsamp / group) * group + (int)(idx - (unsigned)pixel * gt);
-            }
-        } else if (rg < full) {
-            const long long blk = rg / ((long long)group * npx), idx = rg - blk * group * npx;
-            pixel = (int)(idx / group);
-            sample = s0 + (int)blk * group + (int)(idx % group);
-        } else {
-            const int gt = nsamp % group;
-            const long long idx = rg - full;
-            pixel = (int)(idx / gt);
-            sample = s0 + (nsamp / group) * group + (int)(idx % gt);
-        }
+        root_of(rbase + r, npx, s0, group, nsamp, &pixel, &sample);
         f = hit_f[pixel];
         active = f >= 0;
         if (active && !rt.pnw) {
@@ -3335,8 +3442,14 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         const bool need_l = (c2 && li >= 0) || (need && !bsh);
         const bool need_b = need;
         const d3 z = mk3(0, 0, 0);
+#if MCPT_APPEND2  // both children's queue slots from one atomic per workgroup
+        const int2 cs = block_append2(nxt.count, lsh, bsh);
+        queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt, cs.x);
+        queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt, cs.y);
+#else
         queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt);
         queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt);
+#endif
     }
     block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, P.stats + 3,
                 (active && c2) ? 1u : 0u);
@@ -4546,8 +4659,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const unsigned n_children = n;  // [0, n_children) children, [n_children, n) fresh roots
         if (rnext < R && n < (unsigned)fill) {  // refill with roots (appended through node_entry)
             const int m = (int)std::min<long long>((long long)fill - n, R - rnext);
-            hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
-                               (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab);
+            if (rtab.pnw)
+                hipLaunchKernelGGL(k_roots_t, dim3((m + 256 * kRootsPT - 1) / (256 * kRootsPT)), dim3(256), 0, st, P,
+                                   (const int*)D.hit_f.p, npx, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab);
+            else
+                hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
+                                   (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab);
             HIP_OK(hipGetLastError());
             rnext += m;
             if ((rc = read_count(&n))) return rc;
