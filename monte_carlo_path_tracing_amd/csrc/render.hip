@@ -924,7 +924,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 // Per-pixel root table (k_root_table, once per call): a root's entry (main.cpp:406-437 at the primary
 // hit) is the same for every sample of its pixel except the Russian roulette draw, so the point, normal
 // and wo (9 doubles) and the kind (-2 nothing: miss or back face, -1 shading, >= 0 emitter li) are
-// computed once per pixel with the same functions, and k_roots only draws RR and appends.
+// computed once per pixel with the same functions, and k_roots_t only draws RR and appends.
 // MCPT_ROOT_TABLE: roots from the per-pixel table by k_roots_t (kRootsPT roots per thread, one queue
 // atomic per 2 048 roots).  The table alone in k_roots (one atomic per 256 roots) changed nothing
 // (k_roots 111-112 ms per profile run, profiles/round3_ab_acos_dpp_roottab.txt): k_roots was bound by
@@ -1055,8 +1055,7 @@ __global__ __launch_bounds__(256) void k_roots_t(Params P, const int* __restrict
 }
 
 __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
-                                               int s0, long long rbase, int nroots, Queue q, int group, int nsamp,
-                                               RootTab rt) {
+                                               int s0, long long rbase, int nroots, Queue q, int group, int nsamp) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int npx = cam.W * cam.H;
     bool active = r < nroots;
@@ -1067,39 +1066,13 @@ __global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int
         root_of(rbase + r, npx, s0, group, nsamp, &pixel, &sample);
         f = hit_f[pixel];
         active = f >= 0;
-        if (active && !rt.pnw) {
+        if (active) {
             beta = hit_tbg[3 * pixel + 1];
             gamma = hit_tbg[3 * pixel + 2];
             wo = mul(cam_dir(cam, pixel / cam.W, pixel % cam.W), -1);
         }
     }
-    if (!rt.pnw) {
-        node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
-        return;
-    }
-    // entry_eval from the pixel's table row: the same point, normal and kind; RR (dim 0) per sample
-    Entry e{0, -1, mk3(0, 0, 0), mk3(0, 0, 0)};
-    const int kind = active ? rt.kind[pixel] : -2;
-    if (kind >= 0) {
-        e.kind = 1;
-        e.li = kind;
-    } else if (kind == -1) {
-        if (P.mode == MCPT_MODE_SHADE || P.mode == MCPT_MODE_SHADE_AREA) e.kind = 2;
-        else e.kind = counter_u(counter_key(P.seed, (uint64_t)pixel, (uint64_t)sample, 1), 0) > MCPT_P_RR ? 0 : 2;
-    }
-    if (e.kind == 2) {
-        const double* t = rt.pnw + 9 * (size_t)pixel;
-        e.p = mk3(t[0], t[1], t[2]);
-        e.N = mk3(t[3], t[4], t[5]);
-        wo = mk3(t[6], t[7], t[8]);
-    } else if (e.kind == 1) {
-        const DScene& S = P.S;
-        double* px = P.fb + 3 * (size_t)pixel;
-        unsafeAtomicAdd(px + 0, S.light_rad[3 * e.li + 0] * P.inv_spp);
-        unsafeAtomicAdd(px + 1, S.light_rad[3 * e.li + 1] * P.inv_spp);
-        unsafeAtomicAdd(px + 2, S.light_rad[3 * e.li + 2] * P.inv_spp);
-    }
-    queue_push(P, e.kind == 2, e, f, wo, mk3(1, 1, 1), pixel, sample, 1, -1, q);
+    node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
 }
 
 // moves nodes [sb, sb + m) of src to [db, db + m) of dst (every field a generation carries into the
@@ -4664,7 +4637,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                                    (const int*)D.hit_f.p, npx, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab);
             else
                 hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
-                                   (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab);
+                                   (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0);
             HIP_OK(hipGetLastError());
             rnext += m;
             if ((rc = read_count(&n))) return rc;
