@@ -2929,15 +2929,20 @@ __device__ inline double state_light_pdf(const DScene& S, int li, const double* 
 // state st -- to its parent slot; the parent goes to ready list rp once both children have (one
 // append per wave: a single counter word saturates at ~88 atomics/us, MI355X_MICROARCH.md); a root
 // adds L / spp to its pixel.  Every lane of the wave that reaches the call must make it.
+#ifndef MCPT_SPLAT_ZERO_SKIP
+#define MCPT_SPLAT_ZERO_SKIP 1
+#endif
 __device__ inline void mis_report(const Params& P, const Slots& T, bool act, int par, int pixel, d3 L, const double* st,
                                   int rp) {
     bool ready = false;
     int ps = 0;
     if (act && par < 0) {
+        // a zero component adds nothing (the framebuffer is never -0), so its device-scope fp64 atomic
+        // is skipped -- the same image bit for bit
         double* px = P.fb + 3 * (size_t)pixel;
-        unsafeAtomicAdd(px + 0, L.x * P.inv_spp);
-        unsafeAtomicAdd(px + 1, L.y * P.inv_spp);
-        unsafeAtomicAdd(px + 2, L.z * P.inv_spp);
+        if (!MCPT_SPLAT_ZERO_SKIP || L.x != 0.0) unsafeAtomicAdd(px + 0, L.x * P.inv_spp);
+        if (!MCPT_SPLAT_ZERO_SKIP || L.y != 0.0) unsafeAtomicAdd(px + 1, L.y * P.inv_spp);
+        if (!MCPT_SPLAT_ZERO_SKIP || L.z != 0.0) unsafeAtomicAdd(px + 2, L.z * P.inv_spp);
     } else if (act) {
         ps = par >> 2;
         const int role = (par >> 1) & 1;
