@@ -95,8 +95,11 @@ __host__ __device__ inline double acos_cr(double x) {
     const double ax = fabs(x);
     const double y0 = acos(ax);
     const double c = acos_newton_corr(ax, y0);
-    const DD d = dd_two_sum(0x1.921fb54442d18p+1, -y0);  // pi_hi - y0, exactly
-    return x >= 0.0 ? y0 + c : d.h + ((d.l + 0x1.1a62633145c07p-53) - c);
+    // x < 0: (pi_hi - y0) exactly as a two_sum, + pi_lo - c; x >= 0 the same expression with pi and the
+    // signs replaced (two_sum(0, y0) = (y0, 0) exactly, so it is y0 + c): one path, no second result live
+    const bool neg = x < 0.0;
+    const DD d = dd_two_sum(neg ? 0x1.921fb54442d18p+1 : 0.0, neg ? -y0 : y0);
+    return d.h + ((d.l + (neg ? 0x1.1a62633145c07p-53 : 0.0)) + (neg ? -c : c));
 }
 
 }  // namespace mcpt

@@ -1412,7 +1412,10 @@ __device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n, const Nod
 }
 
 constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
-constexpr int kPrepGrab = 4;     // nodes a wave takes per work-counter atomic
+#ifndef MCPT_PREP_GRAB
+#define MCPT_PREP_GRAB 8  // A/B (profiles/round3_ab_launch_params.txt): 4 -> 8 lowers the prep launch 20.65 -> 20.37-20.52 ms
+#endif
+constexpr int kPrepGrab = MCPT_PREP_GRAB;  // nodes a wave takes per work-counter atomic
 
 __global__ __launch_bounds__(256) void k_prep(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                               const double* __restrict__ qn, int qs, const int* __restrict__ qpixel,
