@@ -1412,6 +1412,9 @@ __device__ inline int prep_stage(const DScene& S, int li, d3 x1, d3 n, const Nod
 }
 
 constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
+#ifndef MCPT_LB_EXACT
+#define MCPT_LB_EXACT 4  // k_prep_exact: 4 waves/SIMD (128 VGPRs)
+#endif
 #ifndef MCPT_PREP_GRAB
 #define MCPT_PREP_GRAB 8  // A/B (profiles/round3_ab_launch_params.txt): 4 -> 8 lowers the prep launch 20.65 -> 20.37-20.52 ms
 #endif
@@ -2658,7 +2661,7 @@ struct RootLit {
     double* pool;
     int cap, stride, launch;
 };
-__global__ __launch_bounds__(kExactBlock, 4) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
+__global__ __launch_bounds__(kExactBlock, MCPT_LB_EXACT) void k_prep_exact(DScene S, uint64_t seed, const int* __restrict__ list,
                                                          const double* __restrict__ qp, const double* __restrict__ qn, int qs,
                                                          const int* __restrict__ qpixel, const int* __restrict__ qsample,
                                                          const uint64_t* __restrict__ qnode,
