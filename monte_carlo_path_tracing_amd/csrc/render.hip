@@ -990,7 +990,10 @@ __device__ inline void root_of(long long rg, int npx, int s0, int group, int nsa
 // that rate (~160 k appends, ~1.8 ms per 41 M-root refill).  Here a 256-thread block takes 256 x
 // kRootsPT roots with ONE atomic; sub-batch j (roots base + 256 j + thread) is compacted in order
 // and placed after sub-batches < j, so the queue order equals k_roots' and every store is coalesced.
-constexpr int kRootsPT = 8;
+#ifndef MCPT_ROOTS_PT
+#define MCPT_ROOTS_PT 8
+#endif
+constexpr int kRootsPT = MCPT_ROOTS_PT;
 __global__ __launch_bounds__(256) void k_roots_t(Params P, const int* __restrict__ hit_f, int npx, int s0, long long rbase,
                                                  int nroots, Queue q, int group, int nsamp, RootTab rt) {
     __shared__ unsigned s_w[kRootsPT][4];
