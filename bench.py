@@ -184,6 +184,10 @@ def main():
     ap.add_argument("--debug-flags", type=lambda v: int(v, 0), default=0,
                     help="extra mcpt_render_opts.flags bits of include/mcpt_debug.h (A/B experiments)")
     ap.add_argument("--out", default="", help="optional .bmp of the rendered frame (rank 0)")
+    ap.add_argument("--collective-lib", default="",
+                    help="rehearsal on fewer GPUs than ranks (test infrastructure): the library's reduce goes through this "
+                         "NCCL-API library (tests/collshim/libmcpt_collshim.so, host shared memory) instead of RCCL, ranks "
+                         "share GPUs round-robin and torch.distributed uses gloo")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -194,9 +198,16 @@ def main():
 
     import monte_carlo_path_tracing_amd as mcpt
 
+    rehearsal = bool(args.collective_lib)
+    if rehearsal:
+        mcpt.set_collective_lib(args.collective_lib)
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:  # RCCL refuses two ranks on one GPU: barrier and timing over gloo
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     # the library's RCCL communicator (one rank per process); a 1-rank communicator at N=1
     uid = [mcpt.Comm.unique_id() if rank == 0 else None]
     if world > 1:
@@ -251,7 +262,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     samples = float(W * H) * frame_spp
@@ -389,7 +400,9 @@ def main():
                    "config": args.config, "width": W, "height": H,
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
                    "precision": args.precision, "root_cache": not args.no_root_cache,
-                   "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world,
+                   "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world + (
+                       " [rehearsal: collective %s, ranks sharing GPUs]" % os.path.basename(args.collective_lib)
+                       if rehearsal else ""),
                    "job_spp_per_step": world * S},
         "roofline": roofline,
         "roofline_prep": roof_prep,

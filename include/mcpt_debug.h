@@ -12,10 +12,28 @@ extern "C" {
 /* mcpt_render_opts.flags bits for A/B experiments (the library accepts them; images are unchanged):
  * MCPT_DEBUG_SPLIT_BRDF runs BRDF-only renders as gen / rays / combine kernels instead of the fused
  * k_extend_brdf; MCPT_DEBUG_NO_ROOT_CACHE disables the per-pixel root-point light-prep cache. */
-enum { MCPT_DEBUG_SPLIT_BRDF = 1 << 16, MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17, MCPT_DEBUG_COUNT_TRAVERSAL = 1 << 18 };
+enum {
+    MCPT_DEBUG_SPLIT_BRDF = 1 << 16,
+    MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17,
+    MCPT_DEBUG_COUNT_TRAVERSAL = 1 << 18,
+    MCPT_DEBUG_SHARD_RANKS = 1 << 19
+};
 /* MCPT_DEBUG_COUNT_TRAVERSAL runs the traversal kernel's counting instance, which fills
  * mcpt_stats.node_visits / tri_tests (the events of the traversal roofline; slower, for untimed
- * replays). */
+ * replays).
+ * MCPT_DEBUG_SHARD_RANKS (device lists, mcpt_render_opts.devices): every list entry becomes its own rank
+ * of the ncclCommInitAll communicator, a repeated device included (normally repeated devices are merged
+ * into one rank).  Real RCCL refuses a device twice; with mcpt_debug_set_collective_lib pointing at the
+ * test collective (tests/collshim) it runs the multi-rank group reduce on a one-GPU box. */
+
+/* Test infrastructure: load the NCCL-API collective library at `path` instead of librccl.so.1.  Must
+ * be called before the first communicator of the process (mcpt_comm_unique_id / _init_rank or a device
+ * list render), else MCPT_E_INVALID.  tests/collshim/libmcpt_collshim.so implements the entry points the
+ * library binds (ncclGetUniqueId, ncclCommInitRank, ncclCommInitAll, ncclReduce, ncclGroupStart/End,
+ * ncclCommDestroy, ncclCommAbort, ncclGetErrorString) over host shared memory, so 2-8 processes can
+ * share one GPU -- the multi-rank protocol of mcpt_render_opts.comm then runs in CI as it does over
+ * xGMI.  Not part of the drop-in boundary. */
+int mcpt_debug_set_collective_lib(const char* path);
 
 /* diagnostics: run the light-prep kernel variant `variant` `iters` times on the n points and report
  * the mean device time per launch; outputs like those of mcpt_light_prep, pick = facet.  Variants: -1 auto

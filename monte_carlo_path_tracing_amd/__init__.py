@@ -63,6 +63,7 @@ RENDER_NO_BACKFACE_STATS = 1  # mcpt_render_opts.flags (include/mcpt.h)
 RENDER_FRESH_PDF = 2  # shade_with_mis: the node's own light pdf instead of the reference's stale one
 RENDER_PRECISION_FP32 = 4  # opt-in FP32_STABLE light prep (packed-fp32 weights, fp64 sums); default FP64_LIGHT
 DEBUG_SPLIT_BRDF, DEBUG_NO_ROOT_CACHE, DEBUG_COUNT_TRAVERSAL = 1 << 16, 1 << 17, 1 << 18  # include/mcpt_debug.h
+DEBUG_SHARD_RANKS = 1 << 19  # device lists: every entry its own communicator rank (tests/collshim)
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_uint64)
@@ -92,7 +93,8 @@ EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_cre
            "mcpt_render_opts_init", "mcpt_render", "mcpt_render_device",
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
-DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter", "mcpt_debug_light_prep_exact", "mcpt_debug_light_literal"]  # include/mcpt_debug.h
+DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter", "mcpt_debug_light_prep_exact", "mcpt_debug_light_literal",
+                 "mcpt_debug_set_collective_lib"]  # include/mcpt_debug.h
 
 
 def lib():
@@ -140,7 +142,8 @@ def lib():
         dbg = {"mcpt_debug_prep_bench": [P, I, dp, dp, dp, I, I, C.POINTER(C.c_double), dp, ip],
                "mcpt_debug_tri_filter": [I, fp, dp, dp, fp, ip, fp],
                "mcpt_debug_light_prep_exact": [P, I, dp, dp, dp, dp, ip, ip],
-               "mcpt_debug_light_literal": [P, dp, dp, dp]}
+               "mcpt_debug_light_literal": [P, dp, dp, dp],
+               "mcpt_debug_set_collective_lib": [C.c_char_p]}
         for name, argt in dbg.items():
             if hasattr(L, name):
                 getattr(L, name).argtypes = argt
@@ -169,6 +172,8 @@ class Scene:
 
     def __init__(self, handle):
         self.h = handle
+        # bound now: at interpreter shutdown the module's globals (lib) may already be gone when __del__ runs
+        self._destroy = lib().mcpt_scene_destroy
         f, m, n = C.c_int32(), C.c_int32(), C.c_int32()
         _check(lib().mcpt_scene_counts(self.h, C.byref(f), C.byref(m), C.byref(n)))
         self.nfacets, self.nmaterials, self.nlights = f.value, m.value, n.value
@@ -181,10 +186,11 @@ class Scene:
 
     def close(self):
         if getattr(self, "h", None):
-            lib().mcpt_scene_destroy(self.h)
+            self._destroy(self.h)
             self.h = None
 
-    __del__ = close
+    def __del__(self):
+        self.close()
 
     def arrays(self):
         F, M, NL = self.nfacets, self.nmaterials, self.nlights
@@ -229,6 +235,7 @@ class Comm:
         if len(uid) != COMM_ID_BYTES:
             raise ValueError("comm id must be %d bytes" % COMM_ID_BYTES)
         h = C.c_void_p()
+        self._destroy = lib().mcpt_comm_destroy
         _check(lib().mcpt_comm_init_rank(int(nranks), int(rank), bytes(uid), int(device), C.byref(h)))
         self.h, self.nranks, self.rank = h, int(nranks), int(rank)
 
@@ -240,10 +247,18 @@ class Comm:
 
     def close(self):
         if getattr(self, "h", None):
-            lib().mcpt_comm_destroy(self.h)
+            self._destroy(self.h)
             self.h = None
 
-    __del__ = close
+    def __del__(self):
+        self.close()
+
+
+def set_collective_lib(path):
+    """Test infrastructure (include/mcpt_debug.h): use the NCCL-API library at `path` (the host-memory
+    collective tests/collshim/libmcpt_collshim.so) instead of RCCL for this process's communicators, so
+    several ranks can share one GPU.  Must precede the first Comm / device-list render."""
+    _check(lib().mcpt_debug_set_collective_lib(os.fsencode(path)))
 
 
 def _opts(spp, mode, seed, sample_range, device, samples_per_launch, queue_factor, progress=None, accel="bvh",

@@ -10,12 +10,16 @@
 // Method: one Newton step on cos(y) = x from the libm result y0, with the residual x - cos(y0)
 // evaluated in double-double: x - cos(y0) = (x - 1) + (1 - cos y0), where x - 1 is exact (two_sum)
 // and 1 - cos y0 = z (1/2 - z/24 + z^2/720 - ...) with z = y0^2 as a double-double (the first four
-// coefficients as double-doubles, the rest in double: their terms are < 1e-5 of the sum), so the
-// residual carries ~1e-32 absolute error; y = y0 - residual / sin(y0), sin(y0) = sqrt((1 - x)(1 + x))
+// coefficients as double-doubles, the rest in double: their terms are < 1e-5 of the sum).  The series
+// runs to z^15 / 30!: at the largest z (x = 0, y0 = pi/2, z = 2.47) the first dropped term z^16 / 32!
+// is ~7e-30 absolute (the round-3 form stopped at z^13 / 26!, leaving ~1e-24 = 2^-80 relative there:
+// a misrounding chance of ~1e-8 per argument near 0 instead of ~1e-14 now); elsewhere the truncation is
+// far smaller and the double-double arithmetic's ~1e-32 dominates.  y = y0 - residual / sin(y0),
+// sin(y0) = sqrt((1 - x)(1 + x))
 // (on the GPU through v_rsq_f64: the step is ~1 ulp, so its own few-ulp error is irrelevant).
 // Negative x: acos(x) = pi - acos(-x) with pi as a double-double.  The last step adds a correction of
 // ~1 ulp to y0 in one rounding, so the result is correctly rounded unless the true value lies within
-// ~1e-30 relative of a rounding boundary.
+// ~5e-30 relative of a rounding boundary.
 //
 // Host and device: plain C++ (tools/acos_cr_check.cpp builds it with g++ against mpmath values).
 #pragma once
@@ -55,11 +59,13 @@ __host__ __device__ inline DD dd_add(DD a, DD b) {
     return dd_fast_sum(s.h, s.l + (a.l + b.l));
 }
 
-// y0 = libm acos(x) and a correction c with acos(x) = y0 + c to ~1e-32 absolute, for 0 <= x < 1
+// y0 = libm acos(x) and a correction c with acos(x) = y0 + c to <= ~7e-30 absolute, for 0 <= x < 1
 __host__ __device__ inline double acos_newton_corr(double x, double y0) {
     const DD z = dd_mul(DD{y0, 0.0}, DD{y0, 0.0});
-    // (-1)^k / (2k + 2)!, k = 4..12 in double (Horner in z.h)
-    double t = 0x1.88e85fc6a4e5ap-89;
+    // (-1)^k / (2k + 2)!, k = 4..14 in double (Horner in z.h)
+    double t = 0x1.3932c5047d60ep-108;
+    t = fma(t, z.h, -0x1.0a18a2635085dp-98);
+    t = fma(t, z.h, 0x1.88e85fc6a4e5ap-89);
     t = fma(t, z.h, -0x1.f2cf01972f578p-80);
     t = fma(t, z.h, 0x1.0ce396db7f853p-70);
     t = fma(t, z.h, -0x1.e542ba4020225p-62);

@@ -12,12 +12,17 @@
 //
 // RCCL is resolved with dlopen at first use, not linked: a process that already holds an RCCL
 // (torch's bundled librccl.so.1, same soname) shares it, and single-device renders never load it.
+// mcpt_debug_set_collective_lib (include/mcpt_debug.h) points that dlopen at another library with the
+// same NCCL entry points before the first use -- the test-only host-memory collective of
+// tests/collshim, which lets 2-8 ranks share the one GPU of a test box (RCCL refuses two ranks on one
+// device), so the multi-rank protocol below runs in CI exactly as it does over xGMI.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "mcpt.h"
@@ -34,6 +39,10 @@ struct mcpt_comm {
 namespace mcpt {
 namespace {
 
+std::mutex g_lib_mu;
+std::string g_lib_path;  // mcpt_debug_set_collective_lib; empty: librccl.so.1
+bool g_lib_resolved = false;
+
 struct RcclApi {
     ncclResult_t (*GetUniqueId)(ncclUniqueId*);
     ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
@@ -43,6 +52,7 @@ struct RcclApi {
     ncclResult_t (*GroupStart)();
     ncclResult_t (*GroupEnd)();
     const char* (*GetErrorString)(ncclResult_t);
+    ncclResult_t (*CommAbort)(ncclComm_t);
 };
 
 const RcclApi* rccl() {
@@ -51,8 +61,23 @@ const RcclApi* rccl() {
     static bool ok = false;
     static char why[256] = "";
     std::call_once(once, [] {
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        std::string path;
+        {
+            std::lock_guard<std::mutex> lk(g_lib_mu);
+            g_lib_resolved = true;
+            path = g_lib_path;
+        }
+        void* h = nullptr;
+        if (!path.empty()) {
+            h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+            if (!h) {
+                std::snprintf(why, sizeof why, "cannot load the collective library %s: %s", path.c_str(), dlerror());
+                return;
+            }
+        } else {
+            h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        }
         if (!h) {
             std::snprintf(why, sizeof why, "cannot load RCCL (librccl.so.1): %s", dlerror());
             return;
@@ -71,6 +96,7 @@ const RcclApi* rccl() {
         api.GroupStart = (decltype(api.GroupStart))sym("ncclGroupStart");
         api.GroupEnd = (decltype(api.GroupEnd))sym("ncclGroupEnd");
         api.GetErrorString = (decltype(api.GetErrorString))sym("ncclGetErrorString");
+        api.CommAbort = (decltype(api.CommAbort))sym("ncclCommAbort");
         if (!all) {
             std::snprintf(why, sizeof why, "RCCL library lacks an NCCL entry point");
             return;
@@ -139,8 +165,22 @@ int comm_all_reduce_sum(const std::vector<void*>& comms, const std::vector<int>&
 int comm_rank_reduce_sum(mcpt_comm* c, double* buf, size_t n, hipStream_t st) {
     const RcclApi* A = rccl();
     if (!A) return MCPT_E_DEVICE;
+    if (!c->comm) {
+        set_error("the communicator was aborted after an earlier failure; create a new one");
+        return MCPT_E_DEVICE;
+    }
     RCCL_OK(A, A->Reduce(buf, buf, n, ncclFloat64, ncclSum, 0, c->comm, st));
     return MCPT_OK;
+}
+
+// after a failure that leaves this rank unable to join a collective (the enqueue itself failed): abort
+// the communicator so that RCCL frees its resources; the handle stays allocated (mcpt_comm_destroy)
+void comm_rank_abort(mcpt_comm* c) {
+    const RcclApi* A = rccl();
+    if (A && c && c->comm) {
+        (void)A->CommAbort(c->comm);
+        c->comm = nullptr;
+    }
 }
 
 int comm_rank_info(const mcpt_comm* c, int* nranks, int* rank, int* device) {
@@ -156,6 +196,16 @@ int comm_rank_info(const mcpt_comm* c, int* nranks, int* rank, int* device) {
 using namespace mcpt;
 
 extern "C" {
+
+int mcpt_debug_set_collective_lib(const char* path) {
+    std::lock_guard<std::mutex> lk(g_lib_mu);
+    if (g_lib_resolved) {
+        set_error("the collective library is already resolved (set it before the first communicator)");
+        return MCPT_E_INVALID;
+    }
+    g_lib_path = path ? path : "";
+    return MCPT_OK;
+}
 
 int mcpt_comm_unique_id(uint8_t id[MCPT_COMM_ID_BYTES]) {
     if (!id) {

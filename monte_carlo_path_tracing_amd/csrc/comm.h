@@ -16,5 +16,7 @@ int comm_all_reduce_sum(const std::vector<void*>& comms, const std::vector<int>&
                         const std::vector<hipStream_t>& streams, size_t n);
 // in-place ncclReduce(sum, root rank 0) of this rank's buffer
 int comm_rank_reduce_sum(mcpt_comm* c, double* buf, size_t n, hipStream_t st);
+// ncclCommAbort after a failed enqueue (the handle stays; further reduces fail with MCPT_E_DEVICE)
+void comm_rank_abort(mcpt_comm* c);
 int comm_rank_info(const mcpt_comm* c, int* nranks, int* rank, int* device);
 }  // namespace mcpt

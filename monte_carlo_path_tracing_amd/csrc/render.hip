@@ -311,25 +311,10 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 // they aim at, so the deferred fp64 slots run in nearly every wave), but with the light-ray seed
 // (tlimit known from the start, so the fp32 test also rejects triangles behind the light)
 // 4.04 -> 3.95 ms, shade-area +1.3%
-// Round-3 traversal A/B switches (same-box, profiles/round3_ab_traversal.txt), both off:
-//   MCPT_NODE_OFFSETS=1: node loads as 32-bit byte offsets from the tree base (saddr global loads, one
-//     v_or per load) instead of a 64-bit node pointer: neutral (MIS 447.3 vs 446.0 with it off / on,
-//     BRDF-only 5 499 vs 5 477);
-//   MCPT_SLAB_NEARFAR=1 (needs the offsets): each axis's near / far plane picked once per ray by the
-//     inverse direction's sign, so the slab test has no min/max pairs and no empty-slot test (97 -> 63
-//     VALU per node visit) -- and k_mis_rays 3.81 -> 4.02 ms per launch: the per-lane offsets make
-//     each load instruction touch more distinct lines of the node.
-#ifndef MCPT_NODE_OFFSETS
-#define MCPT_NODE_OFFSETS 0
-#endif
-// MCPT_SLAB_SELECT=1 (A/B only): the near / far float planes selected per axis by the ray's sign after the
-// usual loads: MIS 464.3 -> 463.2, BRDF-only 5 831 -> 5 760 (profiles/round3_ab_traversal.txt)
-#ifndef MCPT_SLAB_SELECT
-#define MCPT_SLAB_SELECT 0
-#endif
-#ifndef MCPT_SLAB_NEARFAR
-#define MCPT_SLAB_NEARFAR 0
-#endif
+// Rejected round-3 traversal variants (same-box, profiles/round3_ab_traversal.txt; removed from the
+// source in round 4): node loads as 32-bit byte offsets (neutral); near / far planes picked once per
+// ray by the inverse direction's sign (97 -> 63 VALU per visit, but k_mis_rays 3.81 -> 4.02 ms); the
+// near / far planes selected after the usual loads (MIS 464.3 -> 463.2, BRDF-only 5 831 -> 5 760).
 #ifndef MCPT_FILTER_MIS
 #define MCPT_FILTER_MIS 1
 #endif
@@ -373,20 +358,6 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     };
     const float ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
     const float oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
-    // near / far plane of each axis picked once per ray by the sign of the inverse direction, as
-    // byte offsets into the node (lo[a] at 16a, hi[a] at 48 + 16a): fma is monotone in the plane
-    // for a fixed inverse, so fma(near) is exactly the fminf of the two slab distances the min/max
-    // form computes, and the per-node min/max pairs go away.  Empty child slots (lo = FLT_MAX,
-    // hi = -FLT_MAX, collapse_bvh4) then give t0 >= FLT_MAX > t1 for any |inverse| >= 1 (a unit
-    // direction's), so they miss without a child-code test.
-#if MCPT_NODE_OFFSETS
-    const unsigned nx = MCPT_SLAB_NEARFAR && ix < 0 ? 48u : 0u, ny = MCPT_SLAB_NEARFAR && iy < 0 ? 64u : 16u,
-                   nz = MCPT_SLAB_NEARFAR && iz < 0 ? 80u : 32u;
-    const unsigned fx = 48u - nx, fy = 80u - ny, fz = 112u - nz;
-#endif
-#if MCPT_SLAB_SELECT
-    const bool sx = ix < 0, sy = iy < 0, sz = iz < 0;
-#endif
     // tlimit0: at least the t of a triangle tri_hit accepts (or FLT_MAX) -- boxes beyond it hold no
     // closest hit
     float tlimit = tlimit0;
@@ -432,44 +403,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
             if (kCount) ++*visits;
             float t[4];
             int code[4];
-            // 32-bit byte offsets from the (wave-uniform) tree base: one v_or per load
-            // loads + four slab tests, instantiated once per address space so that the two paths
-            // join on (t, code) rather than on the 28 loaded dwords (a join on those made the
-            // compiler wait for the first loads before issuing the rest)
-#if MCPT_NODE_OFFSETS
-            const unsigned noff = (unsigned)node * (unsigned)sizeof(BvhNode4);
-            auto visit = [&](const BvhNode4* base) {
-                const char* b = reinterpret_cast<const char*>(base);
-                auto at = [&](unsigned o) { return *reinterpret_cast<const float4*>(b + (noff + o)); };
-                const float4 pnx = at(nx), pfx = at(fx), pny = at(ny), pfy = at(fy), pnz = at(nz), pfz = at(fz);
-                const int4 c4 = *reinterpret_cast<const int4*>(b + (noff + (unsigned)offsetof(BvhNode4, child)));
-                const float nxs[4] = {pnx.x, pnx.y, pnx.z, pnx.w}, fxs[4] = {pfx.x, pfx.y, pfx.z, pfx.w};
-                const float nys[4] = {pny.x, pny.y, pny.z, pny.w}, fys[4] = {pfy.x, pfy.y, pfy.z, pfy.w};
-                const float nzs[4] = {pnz.x, pnz.y, pnz.z, pnz.w}, fzs[4] = {pfz.x, pfz.y, pfz.z, pfz.w};
-                const int chs[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-#if MCPT_SLAB_NEARFAR
-                    const float t0 = fmaxf(fmaxf(fmaf(nxs[k], ix, -oix), fmaf(nys[k], iy, -oiy)), fmaxf(fmaf(nzs[k], iz, -oiz), 0.0f));
-                    const float t1 = fminf(fminf(fmaf(fxs[k], ix, -oix), fmaf(fys[k], iy, -oiy)), fminf(fmaf(fzs[k], iz, -oiz), tlimit));
-                    const bool h = t0 <= fmaf(t1, 1.00001f, 1e-6f);
-#else  // A/B: the round-2 form (lo / hi planes, min / max per pair, empty-slot test); nx.. = lo offsets
-                    const float tx0 = fmaf(nxs[k], ix, -oix), tx1 = fmaf(fxs[k], ix, -oix);
-                    const float ty0 = fmaf(nys[k], iy, -oiy), ty1 = fmaf(fys[k], iy, -oiy);
-                    const float tz0 = fmaf(nzs[k], iz, -oiz), tz1 = fmaf(fzs[k], iz, -oiz);
-                    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
-                    const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
-#endif
-                    t[k] = h ? t0 : FLT_MAX;
-                    code[k] = h ? chs[k] : kDone;  // leaves come pre-packed (pack_leaf_codes)
-                }
-            };
-            // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch,
-            // so each side reads one address space: ds_read from the LDS copy, global loads else)
-            if (kTop > 0 && __all(node < kTop)) visit(top);
-            else visit(nodes);
-#else  // A/B: the round-2 loads (a 64-bit node pointer, fixed lo / hi offsets)
+            // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch)
             {
                 float lo[3][4], hi[3][4];
                 int chs[4];
@@ -477,26 +411,16 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                 else load_node(nodes + node, lo, hi, chs);
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-#if MCPT_SLAB_SELECT  // near / far plane per axis by the ray's sign (k_rays_persistent's form, float planes)
-                    const float nxp = sx ? hi[0][k] : lo[0][k], fxp = sx ? lo[0][k] : hi[0][k];
-                    const float nyp = sy ? hi[1][k] : lo[1][k], fyp = sy ? lo[1][k] : hi[1][k];
-                    const float nzp = sz ? hi[2][k] : lo[2][k], fzp = sz ? lo[2][k] : hi[2][k];
-                    const float t0 = fmaxf(fmaxf(fmaf(nxp, ix, -oix), fmaf(nyp, iy, -oiy)), fmaxf(fmaf(nzp, iz, -oiz), 0.0f));
-                    const float t1 = fminf(fminf(fmaf(fxp, ix, -oix), fmaf(fyp, iy, -oiy)), fminf(fmaf(fzp, iz, -oiz), tlimit));
-                    const bool h = chs[k] != kBvh4Empty && t0 <= fmaf(t1, 1.00001f, 1e-6f);
-#else
                     const float tx0 = fmaf(lo[0][k], ix, -oix), tx1 = fmaf(hi[0][k], ix, -oix);
                     const float ty0 = fmaf(lo[1][k], iy, -oiy), ty1 = fmaf(hi[1][k], iy, -oiy);
                     const float tz0 = fmaf(lo[2][k], iz, -oiz), tz1 = fmaf(hi[2][k], iz, -oiz);
                     const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
                     const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
                     const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
-#endif
                     t[k] = h ? t0 : FLT_MAX;
                     code[k] = h ? chs[k] : kDone;
                 }
             }
-#endif
             // sort (t, code) ascending; misses (FLT_MAX, kDone) sink to the end
             auto cs = [&](int a, int b) {
                 const bool sw = t[b] < t[a];
@@ -546,11 +470,6 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     return best;
 }
 
-// MCPT_PICK_LITERAL=0: light_full's form for the picked triangle (A/B of the literal chain's cost);
-// 2: light_full's form, the literal chain only for a flagged sliver (4 - den > kBandTau num)
-#ifndef MCPT_PICK_LITERAL
-#define MCPT_PICK_LITERAL 1
-#endif
 // The picked triangle's spherical triangle for Arvo's sampler (Mylight.cpp:453-461): the reference's
 // literal chain (light_tri_stage -- sqrt / division unit vectors, correctly rounded acos for
 // alpha, beta, gamma and c, alpha + beta + gamma - pi), so the sampled direction follows the oracle's arithmetic; light_full's
@@ -560,17 +479,8 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
 __device__ inline void pick_sph(const DScene& S, int pick, d3 p, d3 N, SphTri* sph) {
     const double4 ln = S.lt_n[pick];
     const d3 p0 = f3(S.lt_v[3 * pick]), p1 = f3(S.lt_v[3 * pick + 1]), p2 = f3(S.lt_v[3 * pick + 2]);
-#if MCPT_PICK_LITERAL == 2
-    bool sliver = false;
-    const bool ok = light_full(p0, p1, p2, 2.0 * ln.w, p, N, sph, &sliver);
-    if (ok && sliver) {
-        SphTri lit;
-        if (light_tri_stage<true>(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, &lit) == 0) *sph = lit;
-    }
-#else
-    if (!MCPT_PICK_LITERAL || light_tri_stage<true>(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, sph) != 0)
+    if (light_tri_stage<true>(p0, p1, p2, mk3(ln.x, ln.y, ln.z), S.light_sum[pick], p, N, sph) != 0)
         light_full(p0, p1, p2, 2.0 * ln.w, p, N, sph);
-#endif
 }
 
 // x86 cvttsd2si semantics for (int)floor(x) of the reference (out of range -> INT_MIN)
@@ -653,18 +563,10 @@ __device__ inline Hit grid_trace(const DScene& S, d3 ro, d3 rd, int exclude, boo
 // ============================================================================================
 // 3-vectors (the queue's p, n, wo, tp, Aux's directions and throughputs, the prep kernels' node inputs)
 // are interleaved, [cap][3] (node i's y at p[3 i + 1]): a wave's loads of one vector cover 1 536
-// contiguous bytes, fully coalesced, and a vector is one dwordx4 + dwordx2 pair.  MCPT_QUEUE_SOA=1
-// stores them component-major, x[cap] y[cap] z[cap] (three dwordx2 per vector, each a contiguous
-// 512-B run).  Same-box A/B (round 3, profiles/round3_ab_queue_layout.txt): the component-major form
-// moves the same PMC bytes per kernel (k_mis_combine 694.6 vs 696.6 GB per profile run) and issues 8
-// more memory instructions in k_extend_brdf -- BRDF-only 5 893 (interleaved) vs 5 637 Msamples/s,
-// MIS 454.8 vs 453.5 -- so interleaved is the default.
-#ifndef MCPT_QUEUE_SOA
-#define MCPT_QUEUE_SOA 0
-#endif
-__host__ __device__ inline size_t idx3(size_t cap, size_t i, int k) {
-    return MCPT_QUEUE_SOA ? (size_t)k * cap + i : 3 * i + (size_t)k;
-}
+// contiguous bytes, fully coalesced, and a vector is one dwordx4 + dwordx2 pair.  The component-major
+// form (x[cap] y[cap] z[cap]) was measured slower in round 3 (BRDF-only 5 893 interleaved vs 5 637,
+// MIS 454.8 vs 453.5; profiles/round3_ab_queue_layout.txt) and removed.
+__host__ __device__ inline size_t idx3(size_t, size_t i, int k) { return 3 * i + (size_t)k; }
 template <class T>
 __device__ inline d3 ld3(const T* a, size_t cap, size_t i) {
     return mk3(a[idx3(cap, i, 0)], a[idx3(cap, i, 1)], a[idx3(cap, i, 2)]);
@@ -701,13 +603,6 @@ struct Queue {
 // Veach MIS -1.5%, BRDF -5%; profiles/round2b_ab_bvh_quant.txt)
 #ifndef MCPT_BAND_DIAG
 #define MCPT_BAND_DIAG 0
-#endif
-// MCPT_SEED_BRDF=1 (A/B only): trace the BRDF direction's light-only query (set 2) in its own launch
-// first and start set 1 (the same direction against the full BVH) with its light hit as tlimit.
-// Same-box A/B (round 3, profiles/round3_ab_traversal.txt): MIS 462.8 -> 460.9, Cornell-1M 1 274 ->
-// 1 259 Msamples/s -- the second launch and the smaller grids cost more than the pruning saves.
-#ifndef MCPT_SEED_BRDF
-#define MCPT_SEED_BRDF 0
 #endif
 #ifndef MCPT_EXACT_PICK
 #define MCPT_EXACT_PICK 1
@@ -836,36 +731,10 @@ __device__ inline Entry entry_eval(const Params& P, bool active, int f, double b
     }
     return e;
 }
-// block_append for two kinds of items with ONE atomic: the block's a-items, then its b-items, each in
-// lane order.  Must be called by every thread of the workgroup (it contains barriers).
-__device__ inline int2 block_append2(unsigned* counter, bool wa, bool wb) {
-    __shared__ unsigned s_ca[16], s_cb[16];
-    __shared__ unsigned s_base, s_ta;
-    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    const uint64_t ma = __ballot(wa), mb = __ballot(wb);
-    if (lane == 0) s_ca[wid] = (unsigned)__popcll(ma), s_cb[wid] = (unsigned)__popcll(mb);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned ta = 0, tb = 0;
-        for (int w = 0; w < nw; w++) {
-            const unsigned ca = s_ca[w], cb = s_cb[w];
-            s_ca[w] = ta, s_cb[w] = tb;
-            ta += ca, tb += cb;
-        }
-        s_ta = ta;
-        s_base = ta + tb ? atomicAdd(counter, ta + tb) : 0u;
-    }
-    __syncthreads();
-    const uint64_t below = lane == 0 ? 0ull : (~0ull) >> (64 - lane);
-    const int2 r = make_int2(wa ? (int)(s_base + s_ca[wid] + __popcll(ma & below)) : -1,
-                             wb ? (int)(s_base + s_ta + s_cb[wid] + __popcll(mb & below)) : -1);
-    __syncthreads();  // s_* are reused by the next call
-    return r;
-}
 // appends a shading node to q.  Must be called by ALL threads of the workgroup (block_append).
 __device__ inline void queue_push(const Params& P, bool push, const Entry& e, int f, d3 wo, d3 tp, int pixel, int sample,
-                                  uint64_t node, int par, Queue& q, int slot_given = -2) {
-    const int slot = slot_given == -2 ? block_append(q.count, push) : slot_given;
+                                  uint64_t node, int par, Queue& q) {
+    const int slot = block_append(q.count, push);
     if (!push) return;
     if (slot >= q.cap) {
         atomicOr((unsigned long long*)(P.stats + 4), 1ull);
@@ -932,12 +801,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 // (profiles/round3_ab_roots_batched.txt).  0: k_roots (node_entry per root).
 #ifndef MCPT_ROOT_TABLE
 #define MCPT_ROOT_TABLE 1
-#endif
-// MCPT_APPEND2=1 (A/B only): k_mis_combine takes both children's queue slots with one atomic per
-// workgroup instead of two -- MIS 488.0-488.5 vs 487.4-489.0 without (profiles/round3_ab_roots_batched.txt):
-// combine is not bound by its queue atomics
-#ifndef MCPT_APPEND2
-#define MCPT_APPEND2 0
 #endif
 struct RootTab {
     double* pnw;  // [npx][9]: p, N, wo
@@ -2606,10 +2469,13 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
 // of the band against the slack of each node band_candidate listed (k_prep_pk2 / k_prep: margin less
 // the slivers' and the rounding terms, not above the whole-table bound), from the node's candidate
 // words.  Nodes inside the band are appended to the exact list (count in list[0], wave-aggregated).
+// Only nodes [0, nmask) have candidate words (the prep variant that ran wrote them); any other node is
+// tested with every chunk counted as full (band_base without words: 64 candidates per chunk, an upper
+// bound), never with stale words.
 constexpr int kBandBlocks = 128;
 __global__ __launch_bounds__(256) void k_prep_band(DScene S, const int* __restrict__ maybe, const double* __restrict__ slack,
                                                   const double* __restrict__ qp, int qs, const uint64_t* __restrict__ masks,
-                                                  int nchunks, int* __restrict__ list, unsigned long long* stats) {
+                                                  int nmask, int nchunks, int* __restrict__ list, unsigned long long* stats) {
     const int cnt = maybe[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && stats && cnt) atomicAdd(stats + 11, (unsigned long long)cnt);
     for (int j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {  // block-uniform trip count
@@ -2623,7 +2489,7 @@ __global__ __launch_bounds__(256) void k_prep_band(DScene S, const int* __restri
                 amb = true;
             } else {
                 const d3 x1 = ld3(qp, qs, i);
-                amb = !(sl > band_base(S, x1, masks ? masks + (size_t)i * mask_stride(nchunks) : nullptr, nchunks));
+                amb = !(sl > band_base(S, x1, masks && i < nmask ? masks + (size_t)i * mask_stride(nchunks) : nullptr, nchunks));
             }
         }
         const int q = wave_append(reinterpret_cast<unsigned*>(list), amb);
@@ -3081,11 +2947,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
             // set 0 aims at a sampled light triangle: the generation kernel left that triangle's
             // exact t along the ray in the set-0 hit slot (seed_light_t), so boxes behind the light
             // are pruned from the start
-            // set 1 (the BRDF direction against the full BVH) when set 2 (the same direction against the
-            // light-only BVH) ran first (seeded & 2): its light hit's t, left in the set-1 hit slot, bounds
-            // the closest hit the same way -- the light triangle is in the full BVH too
             float tl0 = FLT_MAX;
-            if ((set == 0 && (seeded & 1)) || (set == 1 && (seeded & 2))) {
+            if (set == 0 && (seeded & 1)) {
                 const double t0 = A.hbg[2 * ((size_t)set * A.cap + i)];
                 if (t0 > 0) tl0 = (float)t0 * 1.0001f + 1e-5f;
             }
@@ -3095,7 +2958,6 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
         f = h.f;
         beta = h.beta;
         gamma = h.gamma;
-        if (set == 2) beta = h.f >= 0 ? h.t : -1.0;  // the seed of set 1 (seeded & 2)
     }
     if (kCount) {
         wave_count2(cnt, visits, cnt + 1, tests);
@@ -3106,8 +2968,6 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
     if (set < 2) {
         A.hbg[2 * o] = beta;
         A.hbg[2 * o + 1] = gamma;
-    } else if (seeded & 2) {
-        A.hbg[2 * ((size_t)A.cap + i)] = (fl & 2) ? beta : -1.0;  // set 1's slot, read before set 1 writes it
     }
 }
 
@@ -3209,8 +3069,6 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
         if (set < 2) {
             A.hbg[2 * o] = best.beta;
             A.hbg[2 * o + 1] = best.gamma;
-        } else if (seeded & 2) {  // the seed of set 1 (k_mis_rays)
-            A.hbg[2 * ((size_t)A.cap + ii)] = (A.flags[ii] & 2) && best.f >= 0 ? best.t : -1.0;
         }
         busy = false;
     };
@@ -3258,8 +3116,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                             ix = inv(rd.x), iy = inv(rd.y), iz = inv(rd.z);
                             oix = (float)ro.x * ix, oiy = (float)ro.y * iy, oiz = (float)ro.z * iz;
                             tlimit = FLT_MAX;
-                            // set 0: the light triangle's exact t (seed_light_t); set 1: set 2's light hit
-                            if ((set == 0 && (seeded & 1)) || (set == 1 && (seeded & 2))) {
+                            // set 0: the light triangle's exact t (seed_light_t)
+                            if (set == 0 && (seeded & 1)) {
                                 const double t0 = A.hbg[2 * ((size_t)set * A.cap + ii)];
                                 if (t0 > 0) tlimit = (float)t0 * 1.0001f + 1e-5f;
                             }
@@ -3429,14 +3287,8 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         const bool need_l = (c2 && li >= 0) || (need && !bsh);
         const bool need_b = need;
         const d3 z = mk3(0, 0, 0);
-#if MCPT_APPEND2  // both children's queue slots from one atomic per workgroup
-        const int2 cs = block_append2(nxt.count, lsh, bsh);
-        queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt, cs.x);
-        queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt, cs.y);
-#else
         queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt);
         queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt);
-#endif
     }
     block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, P.stats + 3,
                 (active && c2) ? 1u : 0u);
@@ -3447,26 +3299,9 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
 // node reports to its parent (ready list 1 - rp_in) -- one tree level per pass, in step with the
 // wavefront; grid-stride over the device-side count
 // grid: x blocks per shard, y = ready-list shard
-// MCPT_COMPLETE_SPLIT=1 (A/B only): the BRDF edge's stale light pdf (the literal survival chain, the
-// register peak: 141 VGPRs) evaluated by k_mis_lpdf over the same ready list first and left in w[9], so
-// k_mis_complete itself runs at 8 waves/SIMD over twice the grid.  Same-box A/B with the slot records
-// (profiles/round3_ab_slot_rec.txt): MIS 488.0-491.0 split vs 492.0-493.0 not (k_mis_complete 121 ->
-// 74 ms per profile run, but k_mis_lpdf adds 22 ms and a launch per pass)
-#ifndef MCPT_COMPLETE_SPLIT
-#define MCPT_COMPLETE_SPLIT 0
-#endif
-__global__ __launch_bounds__(256, MCPT_LB_COMPLETE) void k_mis_lpdf(Params P, Slots T, int rp_in) {
-    const DScene& S = P.S;
-    const unsigned n = T.ctrl[16 * blockIdx.y + 4 + rp_in];
-    const int* ready = (rp_in ? T.ready1 : T.ready0) + (size_t)blockIdx.y * T.ready_cap;
-    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        double* rc = T.rec + kSlotRec * (size_t)ready[i];
-        const int4 hdr = *reinterpret_cast<const int4*>(rc);
-        if ((hdr.z & 1) && (hdr.z & 8))
-            rc[11] = rc[10] / (rc[9] + state_light_pdf(S, hdr.w, T.last + 14 * (size_t)ready[i])) / MCPT_P_RR;
-    }
-}
-__global__ __launch_bounds__(256, MCPT_COMPLETE_SPLIT ? 8 : MCPT_LB_COMPLETE) void k_mis_complete(Params P, Slots T, int rp_in) {
+// (round 3: evaluating the stale pdf in a separate kernel so that this one runs at 8 waves/SIMD was
+// measured slower, MIS 488.0-491.0 vs 492.0-493.0; profiles/round3_ab_slot_rec.txt)
+__global__ __launch_bounds__(256, MCPT_LB_COMPLETE) void k_mis_complete(Params P, Slots T, int rp_in) {
     const DScene& S = P.S;
     const unsigned n = T.ctrl[16 * blockIdx.y + 4 + rp_in];
     const int* ready = (rp_in ? T.ready1 : T.ready0) + (size_t)blockIdx.y * T.ready_cap;
@@ -3489,7 +3324,7 @@ __global__ __launch_bounds__(256, MCPT_COMPLETE_SPLIT ? 8 : MCPT_LB_COMPLETE) vo
             const d3 Llight = lsh ? mul(hmul(Ll, mk3(w[0], w[1], w[2])), w[3]) : Ll;
             const double* last_l = T.last + 14 * q;
             double s2 = w[9];
-            if (!MCPT_COMPLETE_SPLIT && lsh && (fl & 8))  // stale state (k_mis_lpdf stores it in w[9] when split)
+            if (lsh && (fl & 8))  // the light child's path-end state
                 s2 = w[8] / (w[7] + state_light_pdf(S, hdr.w, last_l)) / MCPT_P_RR;
             d3 Lbr = mk3(0, 0, 0);
             if (bsh || (fl & 4)) Lbr = mul(hmul(mk3(rc[12], rc[13], rc[14]), mk3(w[4], w[5], w[6])), s2);
@@ -4367,7 +4202,8 @@ int validate_render(const mcpt_render_opts* o) {
         return MCPT_E_INVALID;
     }
     if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
-                     MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL)) {
+                     MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL |
+                     MCPT_DEBUG_SHARD_RANKS)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
@@ -4729,7 +4565,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             prep_launches += timed;
             if (exact_pick) {  // the band's nodes: the reference's literal prep and pick
                 hipLaunchKernelGGL(k_prep_band, dim3(kBandBlocks), dim3(256), 0, st, D.d, maybe_list, slack, cur->p, cur->cap,
-                                   masks, nchunks, exact_list, P.stats);
+                                   masks, nmask, nchunks, exact_list, P.stats);
                 hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D.d.NL)), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
                                    cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
                                    nullptr, P.stats, exact_scr, masks, nmask, nchunks, pc.use ? pc.lst : nullptr,
@@ -4763,18 +4599,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         if (!fused && o->mode == MCPT_MODE_MIS) {
             hipLaunchKernelGGL(stale ? k_mis_gen<true> : k_mis_gen<false>, g256, b256, 0, st, P, *cur, ni, aux);
             HIP_OK(hipEventRecord(D.evr0, st));
-            if (MCPT_SEED_BRDF && !grid) {  // the light-only BRDF query first: its hit seeds set 1
-                launch_rays(2, 1, 2);
-                launch_rays(0, 2, 3);
-            } else {
-                launch_rays(0, 3, 1);
-            }
+            launch_rays(0, 3, 1);
             HIP_OK(hipEventRecord(D.evr1, st));
             hipLaunchKernelGGL(stale ? k_mis_combine<true> : k_mis_combine<false>, g256, b256, 0, st, P, *cur, ni, aux,
                                *nxt, T, rp);
             if (stale) {  // one level of the bottom-up reduction per generation
-                if (MCPT_COMPLETE_SPLIT) hipLaunchKernelGGL(k_mis_lpdf, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
-                hipLaunchKernelGGL(k_mis_complete, dim3(MCPT_COMPLETE_SPLIT ? 64 : 32, kSlotShards), dim3(256), 0, st, P, T, rp);
+                hipLaunchKernelGGL(k_mis_complete, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
                 hipLaunchKernelGGL(k_slot_fixup, dim3(1), dim3(kSlotShards), 0, st, T, rp);
                 rp ^= 1;
             }
@@ -4823,8 +4653,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         unsigned pending = 0;
         for (int sh = 0; sh < kSlotShards; sh++) pending += hctrl[16 * sh + 4 + rp];
         if (pending == 0) break;
-        if (MCPT_COMPLETE_SPLIT) hipLaunchKernelGGL(k_mis_lpdf, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
-        hipLaunchKernelGGL(k_mis_complete, dim3(MCPT_COMPLETE_SPLIT ? 64 : 32, kSlotShards), dim3(256), 0, st, P, T, rp);
+        hipLaunchKernelGGL(k_mis_complete, dim3(32, kSlotShards), dim3(256), 0, st, P, T, rp);
         hipLaunchKernelGGL(k_slot_fixup, dim3(1), dim3(kSlotShards), 0, st, T, rp);
         rp ^= 1;
     }
@@ -4997,18 +4826,34 @@ int multi_progress_cb(void* user, uint64_t dispatched, uint64_t) {
 // order into that device's buffer -- then ONE ncclReduce(sum) into the root devices[0].
 // root_out: the root's framebuffer (device memory on devices[0]); host_out (mcpt_render): when
 // non-null, root_out is the library's buffer, loaded from and stored back to host_out.
+// MCPT_DEBUG_SHARD_RANKS (include/mcpt_debug.h): every list entry is its own rank of the communicator,
+// repeated devices included -- with a collective library that accepts a device twice (tests/collshim)
+// this runs the multi-rank group reduce on a one-GPU box.  Ranks on the same device render one after
+// another (they share its DeviceState) into framebuffers of their own.
 int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* root_out,
                  double* host_out, mcpt_stats* stats) {
     const int nshards = o->num_devices;
-    std::vector<int> uniq;  // distinct devices in order of first appearance; uniq[0] = root
+    const bool per_shard = (o->flags & MCPT_DEBUG_SHARD_RANKS) != 0;
+    std::vector<int> uniq;  // the communicator's ranks: distinct devices in order of first appearance; uniq[0] = root
     std::vector<int> shard_dev(nshards);
     for (int k = 0; k < nshards; k++) {
         const int d = o->devices[k];
-        auto it = std::find(uniq.begin(), uniq.end(), d);
+        auto it = per_shard ? uniq.end() : std::find(uniq.begin(), uniq.end(), d);
         shard_dev[k] = (int)(it - uniq.begin());
         if (it == uniq.end()) uniq.push_back(d);
     }
     const int nu = (int)uniq.size();
+    std::vector<int> lock_of(nu);  // ranks on one device share its state: one lock per device
+    for (int u = 0; u < nu; u++) lock_of[u] = (int)(std::find(uniq.begin(), uniq.end(), uniq[u]) - uniq.begin());
+    std::vector<std::mutex> dev_mu(nu);
+    struct OwnBufs {  // per-rank framebuffers of repeated devices (MCPT_DEBUG_SHARD_RANKS), freed on return
+        std::vector<void*> p;
+        ~OwnBufs() {
+            for (void* q : p)
+                if (q) (void)hipFree(q);
+        }
+    } own;
+    own.p.assign(nu, nullptr);
     const size_t nfb = 3ull * cam->width * cam->height;
     int rc;
     if ((rc = validate_render(o))) return rc;
@@ -5040,6 +4885,7 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
             mp.cancel.store(true);
         };
         int r;
+        std::lock_guard<std::mutex> dev_lock(dev_mu[lock_of[u]]);
         if ((r = get_device_state(sc, uniq[u], &Ds[u]))) return fail(r);
         DeviceState& D = *Ds[u];
         if (hipDeviceSynchronize() != hipSuccess) {  // the caller's buffers may still be written by other streams
@@ -5049,8 +4895,17 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
         if (u == 0 && !host_out) {
             fbs[0] = root_out;
         } else {
-            if ((r = ensure(D.fb, nfb * sizeof(double)))) return fail(r);
-            fbs[u] = (double*)D.fb.p;
+            if (lock_of[u] != u) {  // a repeated device: a buffer of this rank's own
+                if (hipMalloc(&own.p[u], nfb * sizeof(double)) != hipSuccess) {
+                    own.p[u] = nullptr;
+                    set_error("framebuffer of rank %d on device %d: out of memory", u, uniq[u]);
+                    return fail(MCPT_E_DEVICE);
+                }
+                fbs[u] = (double*)own.p[u];
+            } else {
+                if ((r = ensure(D.fb, nfb * sizeof(double)))) return fail(r);
+                fbs[u] = (double*)D.fb.p;
+            }
             const hipError_t e = u == 0 ? hipMemcpyAsync(fbs[0], host_out, nfb * sizeof(double), hipMemcpyHostToDevice, D.stream)
                                         : hipMemsetAsync(fbs[u], 0, nfb * sizeof(double), D.stream);
             if (e != hipSuccess || hipStreamSynchronize(D.stream) != hipSuccess) {
@@ -5136,9 +4991,19 @@ __global__ void k_add_fb(double* __restrict__ dst, const double* __restrict__ sr
 // last slot carries the rank's status (0 ok, 1 failed), so the one reduce also tells rank 0 whether any
 // rank failed; rank 0 then adds the reduced frame to its `out` (or leaves it unchanged and fails).
 // Failures never skip the collective: options are validated identically on every rank before it
-// (validate_render), and a rank whose render fails later (out of memory, spill cap, a cancel from its
-// own progress callback -- cancelling is per rank) zeroes its buffer, sets its status and still joins
-// the reduce, then returns its error.  Other ranks' buffers (`out`) are left unchanged.
+// (validate_render), and every later failure on this rank -- the buffer setup, the render (out of
+// memory, spill cap, a cancel from its own progress callback: cancelling is per rank), zeroing the
+// partial frame -- is recorded and the rank still joins the reduce with the failure flag, then returns
+// its error.  The flag is written by a kernel after the zeroing; if even that cannot be enqueued (a
+// sticky device error) the rank still enqueues the reduce, and its peers see whatever its buffer holds:
+// the one failure mode that can reach rank 0 unflagged is a device that can no longer run kernels, and
+// then its ncclReduce fails to enqueue too.  In that case (the reduce itself cannot be enqueued) the
+// communicator is aborted and the peers block in their reduce: RCCL has no way to release them from
+// one rank.  Other ranks' buffers (`out`) are left unchanged.
+__global__ void k_rank_status(double* fb, size_t nfb, double status) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nfb; i += (size_t)gridDim.x * blockDim.x) fb[i] = 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) fb[nfb] = status;
+}
 int render_rank(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mcpt_render_opts* o, double* out,
                 mcpt_stats* stats) {
     int nranks, rank, device;
@@ -5146,40 +5011,64 @@ int render_rank(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, const mc
     if ((rc = comm_rank_info(o->comm, &nranks, &rank, &device))) return rc;
     if ((rc = validate_render(o))) return rc;  // same outcome on every rank: nobody enters the reduce
     const size_t nfb = 3ull * cam->width * cam->height;
-    if ((rc = ensure(D.rank_fb, (nfb + 1) * sizeof(double)))) return rc;
-    double* fb = (double*)D.rank_fb.p;
-    HIP_OK(hipMemsetAsync(fb, 0, (nfb + 1) * sizeof(double), D.stream));
+    int local = MCPT_OK;
+    std::string lerr;
+    auto fail = [&](int r, const char* what) {
+        if (local) return;
+        local = r;
+        lerr = what ? what : mcpt_last_error();
+        (void)hipGetLastError();
+    };
+    double* fb = nullptr;
+    if ((rc = ensure(D.rank_fb, (nfb + 1) * sizeof(double)))) {
+        // no buffer of our own: the caller's is the only device memory at hand.  Rank 0 cannot lend it
+        // (it is the result); another rank's `out` is left unchanged by contract, so a rank without a
+        // buffer cannot join -- abort instead (below)
+        fail(rc, nullptr);
+    } else {
+        fb = (double*)D.rank_fb.p;
+        if (hipMemsetAsync(fb, 0, (nfb + 1) * sizeof(double), D.stream) != hipSuccess) fail(MCPT_E_DEVICE, "hipMemsetAsync of the rank buffer failed");
+    }
     int s0, s1, a, b;
     job_range(o, &s0, &s1);
     shard_range(s0, s1, rank, nranks, &a, &b);
     mcpt_stats st{};
-    int local = MCPT_OK;
-    std::string lerr;
-    if (a < b) {
+    if (!local && a < b) {
         mcpt_render_opts ok = *o;
         ok.sample_begin = a;
         ok.sample_end = b;
         ok.comm = nullptr;
         ok.device = device;
-        local = render_on_device(sc, D, cam, &ok, fb, &st);
-        if (local) {  // join the reduce anyway, with a zero frame and the failure flag
-            lerr = mcpt_last_error();
-            (void)hipGetLastError();
-            static const double one = 1.0;
-            HIP_OK(hipMemsetAsync(fb, 0, nfb * sizeof(double), D.stream));
-            HIP_OK(hipMemcpyAsync(fb + nfb, &one, sizeof(double), hipMemcpyHostToDevice, D.stream));
-        }
+        const int r = render_on_device(sc, D, cam, &ok, fb, &st);
+        if (r) fail(r, nullptr);
     }
-    HIP_OK(hipEventRecord(D.ev0, D.stream));
-    if ((rc = comm_rank_reduce_sum(o->comm, fb, nfb + 1, D.stream))) return rc;
-    HIP_OK(hipEventRecord(D.ev1, D.stream));
+    if (local && fb) {  // join the reduce anyway, with a zero frame and the failure flag
+        hipLaunchKernelGGL(k_rank_status, dim3(1024), dim3(256), 0, D.stream, fb, nfb, 1.0);
+        (void)hipGetLastError();
+    }
+    int rrc = fb ? MCPT_OK : MCPT_E_DEVICE;
+    if (fb) {
+        (void)hipEventRecord(D.ev0, D.stream);
+        rrc = comm_rank_reduce_sum(o->comm, fb, nfb + 1, D.stream);
+        (void)hipEventRecord(D.ev1, D.stream);
+    }
+    if (rrc) {  // this rank cannot take part in the collective: release what RCCL holds for it
+        const std::string why = mcpt_last_error();
+        comm_rank_abort(o->comm);
+        set_error("rank %d could not join the frame reduce (%s)%s%s; the communicator is aborted", rank, why.c_str(),
+                  local ? " after: " : "", local ? lerr.c_str() : "");
+        return local ? local : rrc;
+    }
     double failed = 0;
-    if (rank == 0) HIP_OK(hipMemcpyAsync(&failed, fb + nfb, sizeof(double), hipMemcpyDeviceToHost, D.stream));
-    HIP_OK(hipEventSynchronize(D.ev1));
-    HIP_OK(hipStreamSynchronize(D.stream));
+    if (rank == 0 && !local) HIP_OK(hipMemcpyAsync(&failed, fb + nfb, sizeof(double), hipMemcpyDeviceToHost, D.stream));
+    const hipError_t se = hipStreamSynchronize(D.stream);
     if (local) {
         set_error("rank %d: %s", rank, lerr.c_str());
         return local;
+    }
+    if (se != hipSuccess) {
+        set_error("rank %d: the frame reduce failed on the device (%s)", rank, hipGetErrorString(se));
+        return MCPT_E_DEVICE;
     }
     if (failed > 0) {
         set_error("%d of %d ranks failed their shard; the frame is not added", (int)failed, nranks);
@@ -5257,8 +5146,8 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
                            cx, (uint64_t*)dm));
         if (exact)
             hipLaunchKernelGGL(k_prep_band, dim3(kBandBlocks), dim3(256), 0, D->stream, D->d, (const int*)cx.maybe,
-                               (const double*)dsl, (const double*)dp, n, (const uint64_t*)dm, prep_chunks(D->d.NL), (int*)dl,
-                               nullptr);
+                               (const double*)dsl, (const double*)dp, n, (const uint64_t*)dm,
+                               prep_writes_masks(D->d, (const uint64_t*)dm) ? n : 0, prep_chunks(D->d.NL), (int*)dl, nullptr);
     }
     if (exact)
         hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D->d.NL)), dim3(kExactBlock), 0, D->stream, D->d, (uint64_t)0,

@@ -246,3 +246,39 @@ def test_malformed_scene_corpus_fails_cleanly(tmp_path):
         except RuntimeError:
             pass
     assert 0 < loaded < len(pairs)
+
+
+_SHIM_LOAD = r"""
+import os, sys
+sys.path.insert(0, os.environ["MCPT_ROOT"])
+import monte_carlo_path_tracing_amd as mcpt
+mcpt.set_collective_lib(os.environ["SHIM"])
+uid = mcpt.Comm.unique_id()  # the shim's ncclGetUniqueId (no GPU involved)
+assert len(uid) == mcpt.COMM_ID_BYTES and uid[:8] == b"MCPTSHIM", uid[:16]
+try:
+    mcpt.set_collective_lib(os.environ["SHIM"])
+    raise SystemExit("second set_collective_lib accepted after the library was resolved")
+except mcpt.MCPTError as e:
+    assert "already resolved" in str(e), e
+# a collective library without the NCCL entry points is refused with a message, not a crash
+print("ok")
+"""
+
+
+def test_collective_lib_override_loads_the_shim(tmp_path):
+    """mcpt_debug_set_collective_lib (include/mcpt_debug.h): the library resolves its NCCL entry points
+    from tests/collshim/libmcpt_collshim.so instead of RCCL (the multi-rank GPU tests' stand-in), and
+    refuses a change once resolved.  The shim's unique id needs no GPU."""
+    shim = ROOT / "tests" / "collshim" / "libmcpt_collshim.so"
+    if not shim.exists():
+        subprocess.run(["make", "-s", "-C", str(shim.parent)], check=True)
+    script = tmp_path / "shim.py"
+    script.write_text(_SHIM_LOAD)
+    import os
+    r = subprocess.run([sys.executable, str(script)], env=dict(os.environ, MCPT_ROOT=str(ROOT), SHIM=str(shim)),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(shim)], capture_output=True, text=True, check=True).stdout
+    for sym in ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommInitAll", "ncclReduce", "ncclGroupStart", "ncclGroupEnd",
+                "ncclCommDestroy", "ncclCommAbort", "ncclGetErrorString"):
+        assert sym in nm, sym

@@ -25,6 +25,7 @@ def main():
         1 - 10.0 ** rng.uniform(-16, -1, n // 4),
         -1 + 10.0 ** rng.uniform(-16, -1, n // 4),
         (2 * rng.integers(0, 2, n // 4) - 1) * 10.0 ** rng.uniform(-300, 0, n // 4),
+        rng.uniform(-0.05, 0.05, n // 4),  # |x| near 0: z = y0^2 largest, the series' truncation largest
         np.array([0.0, -0.0, 0.5, -0.5, 1.0, -1.0, np.nextafter(1, 0), np.nextafter(-1, 0), 1e-300, -1e-300]),
     ])
     with tempfile.TemporaryDirectory() as d:
