@@ -108,9 +108,30 @@ def max_px_rel(g, c):
     return float(np.max(np.where(n > 0, d / np.maximum(n, 1e-300), np.where(d > 0, np.inf, 0.0))))
 
 
-def cpu_baseline(scene_name, W, H, mode, seed, target_s):
-    """The C oracle (oracle/liboracle.so), 1 thread, every 20th pixel in x and y, at an spp chosen
-    so that the run takes about target_s seconds.  Returns (dict, subset image, spp)."""
+def host_cpu_model():
+    """lscpu's "Model name" of this host (from /proc/cpuinfo), or None"""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_threads():
+    """the CPU share to use: OMP_NUM_THREADS (16 on the GPU box), at most the visible CPUs"""
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    return max(1, min(n, 16, os.cpu_count() or 1))
+
+
+def cpu_baseline(scene_name, W, H, mode, seed, full_spp, max_s):
+    """The C oracle (oracle/liboracle.so: the reference's algorithm incl. its uniform grid and O(N_L) light
+    prep per node, fp64) on the stratified pixel subset of BASELINE.md §3 -- every 20th pixel in x and y --
+    at the workload's FULL spp, with the host's CPU share (cpu_threads(): the oracle parallelises over
+    pixels; `cores` says how many).  If that would exceed max_s the spp is reduced and the full-spp time is
+    extrapolated (stated in the record).  Returns (dict, subset image, spp)."""
     from oracle import pyoracle as po
 
     obj, xml, xml_cam = scene_files(scene_name)
@@ -123,29 +144,38 @@ def cpu_baseline(scene_name, W, H, mode, seed, target_s):
     e, _ = po.camera_ray(ocam, 0, 0)
     osc.build_grid(e)
     m = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF, "shade": po.MODE_SHADE, "shade_area": po.MODE_SHADE_AREA}[mode]
+    nt = cpu_threads()
     t = time.perf_counter()
-    osc.render(ocam, m, seed, 1, stride=20, offset=7, nthreads=1)
-    t1 = time.perf_counter() - t
-    spp = int(max(1, min(256, target_s / max(t1, 1e-3))))
+    osc.render(ocam, m, seed, 4, s1=4, stride=20, offset=7, nthreads=nt)  # calibration: 4 spp
+    t4 = time.perf_counter() - t
+    est = t4 / 4 * full_spp
+    spp = full_spp if est <= max_s else int(max(1, min(full_spp, max_s / max(t4 / 4, 1e-6))))
     t = time.perf_counter()
-    img, _ = osc.render(ocam, m, seed, spp, stride=20, offset=7, nthreads=1)
+    img, _ = osc.render(ocam, m, seed, spp, stride=20, offset=7, nthreads=nt)
     dt = time.perf_counter() - t
     npx = len(range(7, H, 20)) * len(range(7, W, 20))
     value = npx * spp / dt / 1e6
-    out = {"value": value, "unit": "Msamples/s", "cores": 1, "kind": "port",
-           "sample": "oracle/mcpt_oracle.c (fp64 C restatement incl. the reference's uniform grid), "
-                     "1 thread, every 20th pixel in x and y of %dx%d (%d px) x %d spp %s = %d camera samples "
-                     "in %.1f s" % (W, H, npx, spp, mode.upper(), npx * spp, dt)}
+    out = {"value": value, "unit": "Msamples/s", "cores": nt, "kind": "port",
+           "host_cpu": host_cpu_model(), "host_cpus_visible": os.cpu_count(),
+           "per_core_value": value / nt, "spp": spp, "full_spp": spp == full_spp,
+           "subset_pixels": npx, "subset_seconds": round(dt, 2),
+           "sample": "oracle/mcpt_oracle.c (fp64 C restatement incl. the reference's uniform grid), %d threads over "
+                     "pixels, every 20th pixel in x and y of %dx%d (%d px = 1/400 of the frame) x %d spp %s = %d camera "
+                     "samples in %.1f s%s" % (nt, W, H, npx, spp, mode.upper(), npx * spp, dt,
+                                              "" if spp == full_spp else
+                                              " (full %d spp extrapolated: %.0f s)" % (full_spp, dt * full_spp / spp))}
+    out["full_frame_seconds_extrapolated"] = dt * (full_spp / spp) * (W * H / npx)
     # The reference itself cannot travel to the GPU box.  Its single-thread speed relative to this
     # restatement was measured on identical frames in the build container (tools/time_reference_cpu.py):
     # the restatement is faster (no std::map facet lookups), so the reference-equivalent baseline is
-    # value / ratio.
+    # value / ratio (per thread: the reference is single-threaded, README.md:418).
     ref = load_json(os.path.join(ROOT, "profiles", "cpu_reference_vs_oracle.json"))
     r = (ref or {}).get("modes", {}).get(mode) if scene_name == "veach" else None
     if r:
         out["oracle_over_reference"] = r["oracle_over_reference"]
-        out["reference_equivalent_value"] = value / r["oracle_over_reference"]
-        out["reference_equivalent_source"] = ("profiles/cpu_reference_vs_oracle.json: compiled reference %.0f vs oracle "
+        out["reference_equivalent_value"] = value / nt / r["oracle_over_reference"]
+        out["reference_equivalent_source"] = ("single thread: per-core value / oracle_over_reference; "
+                                              "profiles/cpu_reference_vs_oracle.json: compiled reference %.0f vs oracle "
                                               "%.0f samples/s, 1 core of '%s', %s" % (
                                                   r["reference_samples_per_s"], r["oracle_samples_per_s"],
                                                   ref.get("host", "?"), r["frame"]))
@@ -171,7 +201,8 @@ def main():
     ap.add_argument("--scene", default="veach", choices=sorted(SCENES),
                     help="veach: the north-star workload (C3); cornell1m: config C5")
     ap.add_argument("--seed", type=int, default=20240430)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget")
+    ap.add_argument("--cpu-seconds", type=float, default=90.0,
+                    help="CPU baseline budget: the full-spp subset runs if it fits, else fewer spp, extrapolated")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and L2 check")
     ap.add_argument("--fresh-pdf", action="store_true",
                     help="MIS with the node's own light pdf (MCPT_RENDER_FRESH_PDF) instead of the reference's stale one")
@@ -379,8 +410,8 @@ def main():
     cpu = None
     l2 = l2max = None
     if world == 1 and not args.no_cpu:
-        log("cpu baseline (~%.0f s) ..." % args.cpu_seconds)
-        cpu, cimg, cspp = cpu_baseline(args.scene, W, H, args.mode, args.seed, args.cpu_seconds)
+        log("cpu baseline (<= ~%.0f s) ..." % args.cpu_seconds)
+        cpu, cimg, cspp = cpu_baseline(args.scene, W, H, args.mode, args.seed, S, args.cpu_seconds)
         g, _ = mcpt.render(scene, cam, cspp, mode=args.mode, seed=args.seed, device=local, flags=mode_flags)
         sub = (slice(7, None, 20), slice(7, None, 20))
         l2 = rel_l2(g[sub], cimg[sub])

@@ -627,6 +627,10 @@ struct Params {
     unsigned long long* stats;   // [0] cached root preps [1] light survivors [2] rays [3] light rays [4] overflow
                                  // [5] prep candidates [6] light-side culls [7] full preps
     int mode;
+    // BRDF-only (k_extend_brdf): root entries (node id 1) carry only facet, pixel and sample; their
+    // point, normal and wo come from the per-pixel root table ([npx][9], k_root_table) and their
+    // throughput is 1 -- so k_roots_t does not copy a per-pixel constant into every sample's entry
+    const double* root_pnw;
 };
 
 __device__ inline int lane_id() { return __lane_id(); }
@@ -857,8 +861,10 @@ __device__ inline void root_of(long long rg, int npx, int s0, int group, int nsa
 #define MCPT_ROOTS_PT 8
 #endif
 constexpr int kRootsPT = MCPT_ROOTS_PT;
+// lite (BRDF-only with P.root_pnw): the entries' point, normal, wo and throughput are not written
+// (k_extend_brdf reads them from the root table)
 __global__ __launch_bounds__(256) void k_roots_t(Params P, const int* __restrict__ hit_f, int npx, int s0, long long rbase,
-                                                 int nroots, Queue q, int group, int nsamp, RootTab rt) {
+                                                 int nroots, Queue q, int group, int nsamp, RootTab rt, int lite) {
     __shared__ unsigned s_w[kRootsPT][4];
     __shared__ unsigned s_base;
     const int lane = lane_id(), wid = threadIdx.x >> 6;
@@ -907,11 +913,13 @@ __global__ __launch_bounds__(256) void k_roots_t(Params P, const int* __restrict
             atomicOr((unsigned long long*)(P.stats + 4), 1ull);
             continue;
         }
-        const double* t = rt.pnw + 9 * (size_t)px[j];
-        st3(q.p, q.cap, slot, mk3(t[0], t[1], t[2]));
-        st3(q.n, q.cap, slot, mk3(t[3], t[4], t[5]));
-        st3(q.wo, q.cap, slot, mk3(t[6], t[7], t[8]));
-        st3(q.tp, q.cap, slot, mk3(1, 1, 1));
+        if (!lite) {
+            const double* t = rt.pnw + 9 * (size_t)px[j];
+            st3(q.p, q.cap, slot, mk3(t[0], t[1], t[2]));
+            st3(q.n, q.cap, slot, mk3(t[3], t[4], t[5]));
+            st3(q.wo, q.cap, slot, mk3(t[6], t[7], t[8]));
+            st3(q.tp, q.cap, slot, mk3(1, 1, 1));
+        }
         q.f[slot] = hit_f[px[j]];
         q.pixel[slot] = px[j];
         q.sample[slot] = sm[j];
@@ -1008,12 +1016,27 @@ __device__ inline void wave_count2(unsigned long long* ca, unsigned a, unsigned 
         if (sb) atomicAdd(cb, sb);
     }
 }
+// Root-point cache of the small-table prep (k_prep_lane's scenes, N_L <= kSmallNL; the large tables'
+// cache is PrepCache): a root's (x1, n) is its pixel's, so its literal running sums are a function of the
+// pixel (main.cpp:563-572 re-traces the same primary ray for every sample).  Per pixel: the running sum
+// after each light (-1 where the light does not survive), weights_sum and the last survivor; a root's
+// pick is then a search of its pixel's row -- the same comparisons on the same values as k_prep_lane's
+// pick loop, so weights_sum and the pick are bit-identical.
+struct SmallCache {
+    double* cum;   // [npx][NL]
+    double* wsum;  // [npx]
+    int* last;     // [npx]
+};
+// kKeep > 0 (N_L <= kKeep): the running sums of pass 1 stay in registers and the pick searches them,
+// instead of re-running the literal chain (six acos per light) up to the picked light.  kBuild: the
+// nodes are root points (qpixel = their pixels); their rows go to the SmallCache, no pick.
+template <int kKeep, bool kBuild>
 __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
                                                    const double* __restrict__ qn, int qs, const int* __restrict__ qpixel,
                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
                                                    const double* __restrict__ u_override, double* __restrict__ wsum_out,
                                                    int* __restrict__ pick_out, int* __restrict__ count_out,
-                                                   unsigned long long* stats) {
+                                                   unsigned long long* stats, SmallCache C) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
     unsigned long long surv = 0, cand = 0, c1 = 0;
@@ -1032,41 +1055,69 @@ __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int 
             *ok = st == 0;
             return st == 0 ? o.w : (double)st;  // culled: 1 or 2 = the cheap stage, 3 = the full stage
         };
+        double* row = kBuild ? C.cum + (size_t)qpixel[i] * S.NL : nullptr;
+        double cw[kKeep > 0 ? kKeep : 1];  // running sum after light li, -1 if it does not survive
         double wsum = 0;
-        for (int li = 0; li < S.NL; li++) {
+        int last = -1;
+        auto visit = [&](int li) {
             bool ok;
             const double r = eval(li, &ok);
             if (ok) {
                 wsum += r;
                 surv++;
+                last = li;
             }
             const bool culled = !ok && (r == 1.0 || r == 2.0);
             c1 += culled && r == 1.0;
             cand += !culled;
-        }
-        int pick = -1;
-        if (!(fabs(wsum) < MCPT_EPS)) {
-            const double u = u_override ? u_override[i]
-                                        : counter_u(counter_key(seed, (uint64_t)qpixel[i], (uint64_t)qsample[i], qnode[i]), 1);
-            const double target = u * wsum;
-            double cum = 0;
-            int last = -1;
+            return ok ? wsum : -1.0;
+        };
+        if (kKeep > 0) {
+#pragma unroll
+            for (int li = 0; li < kKeep; li++) cw[li] = li < S.NL ? visit(li) : -1.0;
+        } else {
             for (int li = 0; li < S.NL; li++) {
-                bool ok;
-                const double r = eval(li, &ok);
-                if (!ok) continue;
-                cum += r;
-                last = li;
-                if (cum >= target) {
-                    pick = li;
-                    break;
-                }
+                const double c = visit(li);
+                if (kBuild) row[li] = c;
             }
-            if (pick < 0) pick = last;
         }
-        wsum_out[i] = wsum;
-        pick_out[i] = pick;
-        if (count_out) count_out[i] = (int)surv;
+        if (kBuild) {
+            if (kKeep > 0) {
+#pragma unroll
+                for (int li = 0; li < kKeep; li++)
+                    if (li < S.NL) row[li] = cw[li];
+            }
+            C.wsum[qpixel[i]] = wsum;
+            C.last[qpixel[i]] = last;
+        } else {
+            int pick = -1;
+            if (!(fabs(wsum) < MCPT_EPS)) {
+                const double u = u_override ? u_override[i]
+                                            : counter_u(counter_key(seed, (uint64_t)qpixel[i], (uint64_t)qsample[i], qnode[i]), 1);
+                const double target = u * wsum;
+                if (kKeep > 0) {  // first survivor whose running sum reaches the target (culled: -1 never does)
+#pragma unroll
+                    for (int li = kKeep - 1; li >= 0; li--)
+                        if (cw[li] >= target) pick = li;
+                } else {
+                    double cum = 0;
+                    for (int li = 0; li < S.NL; li++) {
+                        bool ok;
+                        const double r = eval(li, &ok);
+                        if (!ok) continue;
+                        cum += r;
+                        if (cum >= target) {
+                            pick = li;
+                            break;
+                        }
+                    }
+                }
+                if (pick < 0) pick = last;
+            }
+            wsum_out[i] = wsum;
+            pick_out[i] = pick;
+            if (count_out) count_out[i] = (int)surv;
+        }
     }
     if (stats) {
         const unsigned long long ss = wave_sum_u64(surv), cs = wave_sum_u64(cand), c1s = wave_sum_u64(c1);
@@ -1077,6 +1128,37 @@ __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int 
             if (c1s) atomicAdd(stats + 6, c1s);
             if (full) atomicAdd(stats + 7, full);
         }
+    }
+}
+
+// cached roots of a small-table scene (SmallCache): the pick searches the pixel's row of running sums
+// (lane per root); weights_sum is the cached one
+__global__ __launch_bounds__(256) void k_prep_lane_pick(DScene S, uint64_t seed, int n, const int* __restrict__ qpixel,
+                                                        const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
+                                                        double* __restrict__ wsum_out, int* __restrict__ pick_out,
+                                                        unsigned long long* stats, SmallCache C) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n;
+    if (active) {
+        const int px = qpixel[i];
+        const double wsum = C.wsum[px];
+        int pick = -1;
+        if (!(fabs(wsum) < MCPT_EPS)) {
+            const double target = counter_u(counter_key(seed, (uint64_t)px, (uint64_t)qsample[i], qnode[i]), 1) * wsum;
+            const double* row = C.cum + (size_t)px * S.NL;
+            for (int li = 0; li < S.NL; li++)
+                if (row[li] >= target) {
+                    pick = li;
+                    break;
+                }
+            if (pick < 0) pick = C.last[px];
+        }
+        wsum_out[i] = wsum;
+        pick_out[i] = pick;
+    }
+    if (stats) {
+        const unsigned long long c = __popcll(__ballot(active));
+        if (lane_id() == 0 && c) atomicAdd(stats + 0, c);
     }
 }
 
@@ -3557,12 +3639,15 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = i < n;
     const int ii = active ? i : 0;
-    const d3 p = ld3(cur.p, cur.cap, ii);
-    const d3 N = ld3(cur.n, cur.cap, ii);
-    const d3 wo = ld3(cur.wo, cur.cap, ii);
-    const d3 tp = ld3(cur.tp, cur.cap, ii);
     const int f = cur.f[ii], pixel = cur.pixel[ii], sample = cur.sample[ii];
     const uint64_t node = cur.node[ii];
+    d3 p, N, wo, tp;
+    if (P.root_pnw && node == 1) {  // a root: the per-pixel table (k_roots_t wrote no point / normal / wo)
+        const double* t = P.root_pnw + 9 * (size_t)pixel;
+        p = mk3(t[0], t[1], t[2]), N = mk3(t[3], t[4], t[5]), wo = mk3(t[6], t[7], t[8]), tp = mk3(1, 1, 1);
+    } else {
+        p = ld3(cur.p, cur.cap, ii), N = ld3(cur.n, cur.cap, ii), wo = ld3(cur.wo, cur.cap, ii), tp = ld3(cur.tp, cur.cap, ii);
+    }
     bool c = false;
     unsigned traced = 0, visits = 0, tests = 0;
     Hit h{-1, 0, 0, 0};
@@ -3636,6 +3721,7 @@ struct DeviceState {
     DevBuf hit_f, hit_tbg, root_pnw, root_kind, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[9], sl[13], cache_bt, cache_lst, cache_info, cache_w, masks;
     DevBuf exact, exact_scr, slack;  // exact pick: list, k_prep_exact's scratch, per-node slack
     DevBuf lit_slot, lit_pool;        // exact pick: roots' literal sums per pixel (RootLit)
+    DevBuf sc_cum, sc_wsum, sc_last;  // small-table root-point cache (SmallCache)
     int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
@@ -4102,6 +4188,28 @@ constexpr int kPk2Waves = MCPT_PK2_WAVES;
 inline bool prep_writes_masks(const DScene& d, const uint64_t* masks) {
     return masks && d.NL > kSmallNL && d.NL <= 65535 && 4 * prep_list_wave_bytes(prep_chunks(d.NL)) <= kPrepListMaxLds;
 }
+// k_prep_lane (N_L <= kSmallNL) with its running sums kept in registers up to 16 lights; build: the nodes
+// are root points whose rows go to the SmallCache
+hipError_t launch_prep_lane(const DScene& d, uint64_t seed, int n, const double* qp, const double* qn, int qs,
+                            const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
+                            int* pick, int* count, unsigned long long* stats, hipStream_t st, const SmallCache& C, bool build) {
+    if (n <= 0) return hipSuccess;
+    const dim3 g((n + 255) / 256), b(256);
+#define MCPT_LANE(K)                                                                                                     \
+    do {                                                                                                                 \
+        if (build)                                                                                                       \
+            hipLaunchKernelGGL((k_prep_lane<K, true>), g, b, 0, st, d, seed, n, qp, qn, qs, qpixel, qsample, qnode, u, wsum, \
+                               pick, count, stats, C);                                                                   \
+        else                                                                                                             \
+            hipLaunchKernelGGL((k_prep_lane<K, false>), g, b, 0, st, d, seed, n, qp, qn, qs, qpixel, qsample, qnode, u,      \
+                               wsum, pick, count, stats, C);                                                             \
+    } while (0)
+    if (d.NL <= 4) MCPT_LANE(4);
+    else if (d.NL <= 16) MCPT_LANE(16);
+    else MCPT_LANE(0);
+#undef MCPT_LANE
+    return hipGetLastError();
+}
 hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const double* qp, const double* qn, int qs,
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
@@ -4112,11 +4220,8 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
     if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? 17 : 8) : 0;  // A/B: tools/prep_variants.py
     if (variant != 0 && variant != 8 && variant != 9 && variant != 17) return hipErrorInvalidValue;
-    if (variant == 9) {
-        hipLaunchKernelGGL(k_prep_lane, dim3((n + 255) / 256), dim3(256), 0, st, d, seed, n, qp, qn, qs, qpixel, qsample, qnode,
-                           u, wsum, pick, count, stats);
-        return hipGetLastError();
-    }
+    if (variant == 9) return launch_prep_lane(d, seed, n, qp, qn, qs, qpixel, qsample, qnode, u, wsum, pick, count, stats, st,
+                                              SmallCache{}, false);
     if (variant > 0 && !list_ok) variant = 0;
     if (variant == 17 && !masks) variant = 8;  // the split form needs the candidate-word scratch
     if (cache.build && variant != 8 && variant != 17) return hipErrorInvalidValue;
@@ -4296,6 +4401,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     P.fb = dfb;
     P.stats = (unsigned long long*)D.stats.p;
     P.mode = o->mode;
+    P.root_pnw = nullptr;
     const int nchunks = prep_chunks(D.d.NL);
     const size_t prep_lds = prep_lds_bytes(nchunks);
     if (prep_lds > 160 * 1024) {
@@ -4354,6 +4460,20 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         pc.lstride = lstride;
         pc.use = 1;  // built below, inside the timed region
     }
+    // the small-table prep's root-point cache (SmallCache: N_L <= kSmallNL, e.g. the Cornell scene's
+    // 2-triangle light): (N_L + 1.5) x 8 B per pixel
+    SmallCache scache{};
+    bool small_use = false;
+    if (needs_prep && s1 - s0 >= 2 && !no_cache && D.d.NL > 0 && D.d.NL <= kSmallNL &&
+        (size_t)npx * (8ull * D.d.NL + 12) <= budget) {
+        if ((rc = ensure(D.sc_cum, 8ull * npx * D.d.NL)) || (rc = ensure(D.sc_wsum, 8ull * npx)) ||
+            (rc = ensure(D.sc_last, 4ull * npx)))
+            return rc;
+        scache.cum = (double*)D.sc_cum.p;
+        scache.wsum = (double*)D.sc_wsum.p;
+        scache.last = (int*)D.sc_last.p;
+        small_use = true;
+    }
     RootLit rl{};  // roots' literal sums per pixel (k_prep_exact), up to 2 GiB of entries
     if (exact_pick && pc.use) {
         rl.stride = (lstride + 8 + 7) & ~7;
@@ -4376,8 +4496,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         hipLaunchKernelGGL(k_root_table, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
                            (const double*)D.hit_tbg.p, rtab);
         HIP_OK(hipGetLastError());
+        if (fused) P.root_pnw = rtab.pnw;  // BRDF-only: lite root entries (Params::root_pnw)
     }
-    if (pc.use) {
+    if (pc.use || small_use) {
         HIP_OK(hipMemsetAsync(qb.count, 0, 4, st));
         hipLaunchKernelGGL(k_root_points, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
                            (const double*)D.hit_tbg.p, qb);
@@ -4385,7 +4506,19 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         HIP_OK(hipMemcpyAsync(D.pinned_count, qb.count, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         const int nr = (int)std::min<unsigned>(D.pinned_count[0], (unsigned)cap);
-        if (nr > 0) {
+        if (nr > 0 && small_use) {
+            HIP_OK(hipEventRecord(D.evp0, st));
+            HIP_OK(launch_prep_lane(D.d, o->seed, nr, qb.p, qb.n, qb.cap, qb.pixel, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                    nullptr, P.stats, st, scache, true));
+            HIP_OK(hipEventRecord(D.evp1, st));
+            HIP_OK(hipEventSynchronize(D.evp1));
+            float ms = 0;
+            HIP_OK(hipEventElapsedTime(&ms, D.evp0, D.evp1));
+            prep_ms += ms;
+            cache_ms = ms;
+            prep_launches++;
+            cache_points = (uint64_t)nr;
+        } else if (nr > 0) {
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
             HIP_OK(launch_prep(masks ? 17 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.cap, qb.pixel, nullptr, nullptr, nullptr, nullptr,
@@ -4400,7 +4533,6 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             cache_points = (uint64_t)nr;
         }
         pc.build = 0;
-        pc.use = 1;
         if (rl.slot) {  // a fresh set of per-pixel literal sums for this call's cache
             HIP_OK(hipMemsetAsync(rl.slot, 0, 64, st));
             HIP_OK(hipMemsetAsync(rl.slot + 16, 0xff, 4ull * npx, st));
@@ -4484,7 +4616,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             const int m = (int)std::min<long long>((long long)fill - n, R - rnext);
             if (rtab.pnw)
                 hipLaunchKernelGGL(k_roots_t, dim3((m + 256 * kRootsPT - 1) / (256 * kRootsPT)), dim3(256), 0, st, P,
-                                   (const int*)D.hit_f.p, npx, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab);
+                                   (const int*)D.hit_f.p, npx, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab,
+                                   P.root_pnw ? 1 : 0);
             else
                 hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
                                    (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0);
@@ -4524,7 +4657,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 HIP_OK(hipMemsetAsync(exact_list, 0, 4, st));
                 HIP_OK(hipMemsetAsync(maybe_list, 0, 4, st));
             }
-            if (pc.use) {  // children: full prep; roots: pick from the root-point cache
+            if (pc.use || small_use) {  // children: full prep; roots: pick from the root-point cache
                 const int nc = (int)n_children, nr = ni - nc;
                 if (nc > 0) {
                     nmask = prep_writes_masks(D.d, masks) ? nc : 0;
@@ -4535,7 +4668,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
-                if (nr > 0) {
+                if (nr > 0 && small_use) {
+                    hipLaunchKernelGGL(k_prep_lane_pick, dim3((nr + 255) / 256), dim3(256), 0, st, D.d, o->seed, nr,
+                                       cur->pixel + nc, cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc,
+                                       P.stats, scache);
+                    HIP_OK(hipGetLastError());
+                } else if (nr > 0) {
                     root_off = nc;
                     PrepCache pr = pc;
                     pr.exact = exact_list;
@@ -5271,7 +5409,8 @@ void mcpt_scene_destroy(mcpt_scene* sc) {
         for (void* p : D->allocs) (void)hipFree(p);
         std::vector<DevBuf*> bufs = {&D->hit_f, &D->hit_tbg, &D->fb, &D->rank_fb, &D->stats, &D->work, &D->cache_bt, &D->cache_lst,
                                      &D->cache_info, &D->cache_w, &D->masks, &D->g_start, &D->g_tri, &D->root_pnw,
-                                     &D->root_kind, &D->exact, &D->exact_scr, &D->slack, &D->lit_slot, &D->lit_pool};
+                                     &D->root_kind, &D->exact, &D->exact_scr, &D->slack, &D->lit_slot, &D->lit_pool,
+                                     &D->sc_cum, &D->sc_wsum, &D->sc_last};
         for (int k = 0; k < 14; k++) bufs.insert(bufs.end(), {&D->qa[k], &D->qb[k], &D->qs[k]});
         for (int k = 0; k < 9; k++) bufs.push_back(&D->aux[k]);
         for (int k = 0; k < 13; k++) bufs.push_back(&D->sl[k]);

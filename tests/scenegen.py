@@ -2,6 +2,7 @@
 (scenes/gen_veach_mis.py): a scene without lights, a dense light panel (more than 4096 candidates
 per shading point: the sequential batch-search path) and a very finely tessellated sphere light
 (N_L > 7680: the LDS-queue prep variant, no root cache)."""
+import math
 import os
 import sys
 
@@ -98,3 +99,85 @@ def occluded_room(outdir):
     obj.groups.append(("lamp", "lamp", faces))
     mtls += [("wall", (0.7, 0.7, 0.7), (0.0, 0.0, 0.0), 1.0), ("lamp", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0)]
     return _write(outdir, "room", obj, mtls, [("lamp", (5.0, 5.0, 5.0))], ((0.0, 1.5, 1.8), (0.0, 0.4, 0.0)))
+
+
+# ---- exact-pick stress scenes (the band + literal fallback beyond the stand-in) ----
+
+def sphere_mix(outdir):
+    """Four sphere lights of 8x4, 16x8, 32x16 and 64x32 segments (48 + 224 + 960 + 3968 = 5200 light
+    triangles: more than 4096, so roots take the wave-per-root k_prep_pick), different radii, distances
+    and radiances over the floor and a glossy block."""
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    lights = []
+    for k, (seg, ring, c, r, rad) in enumerate([(8, 4, (-1.6, 1.9, -1.0), 0.35, (3.0, 2.0, 1.0)),
+                                                (16, 8, (1.6, 2.1, -1.2), 0.2, (9.0, 9.0, 12.0)),
+                                                (32, 16, (0.0, 2.6, -1.6), 0.5, (2.0, 2.5, 2.0)),
+                                                (64, 32, (-0.3, 1.5, 1.4), 0.3, (4.0, 3.0, 3.0))]):
+        name = "sph%d" % k
+        obj.sphere(name, name, c, r, seg, ring)
+        mtls.append((name, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0))
+        lights.append((name, rad))
+    return _write(outdir, "sphmix", obj, mtls, lights, CAM)
+
+
+def slivers(outdir, strips=24):
+    """Lights seen nearly edge-on from the floor: vertical light blinds (planes x = const, split into
+    long thin triangles) standing on the floor region, whose planes pass through the floor points next
+    to them -- their spherical triangles are slivers (one vertex angle near pi), where the reference's
+    alpha + beta + gamma - pi is decided by the last bits of its acos; plus a panel tilted 2 degrees
+    off the vertical (near-grazing for the points below it)."""
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    faces = []
+    for xk in (-1.2, -0.4, 0.4, 1.2):
+        for side in (1.0, -1.0):  # two thin layers facing +x and -x
+            x = xk + 0.002 * side
+            n = obj.normal((side, 0.0, 0.0))
+            for s in range(strips):
+                y0, y1 = 0.3 + 1.5 * s / strips, 0.3 + 1.5 * (s + 1) / strips
+                a, b = obj.vert((x, y0, -1.5)), obj.vert((x, y0, 1.5))
+                c, d = obj.vert((x, y1, 1.5)), obj.vert((x, y1, -1.5))
+                tri = [(a, b, c), (a, c, d)]
+                if side < 0:
+                    tri = [(a, c, b), (a, d, c)]
+                faces += [tuple((v, n) for v in t) for t in tri]
+    obj.groups.append(("blinds", "blinds", faces))
+    faces = []
+    t = math.radians(2.0)
+    n = obj.normal((math.cos(t), math.sin(t), 0.0))
+    for s in range(40):  # tilted panel of 80 thin triangles near x = 2.2
+        z0, z1 = -1.5 + 3.0 * s / 40, -1.5 + 3.0 * (s + 1) / 40
+        p = [(2.2 - 1.6 * math.sin(t) * h, 0.2 + 1.6 * math.cos(t) * h, z) for h, z in ((0, z0), (0, z1), (1, z1), (1, z0))]
+        q = [obj.vert(v) for v in p]
+        faces += [((q[0], n), (q[2], n), (q[1], n)), ((q[0], n), (q[3], n), (q[2], n))]
+    obj.groups.append(("tilt", "tilt", faces))
+    mtls += [("blinds", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0), ("tilt", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0)]
+    return _write(outdir, "slivers", obj, mtls, [("blinds", (4.0, 4.0, 4.0)), ("tilt", (6.0, 5.0, 4.0))], CAM)
+
+
+def tiny_far(outdir):
+    """Distant tiny lights: 8x4 spheres of radius 1e-2, 1e-3, 1e-4 and 1e-6 at distances 20-90 above the
+    floor, plus one ordinary light.  Their spherical triangles span ~1e-2 .. 1e-8 rad: the reference's
+    alpha + beta + gamma - pi is mostly its own rounding there (the unit vectors' rounding amplified by
+    distance / edge), and the edge-length culls (< 1e-8 rad, Mylight.cpp:379-382) fire on the smallest."""
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    lights = []
+    k = 0
+    for r in (1e-2, 1e-3, 1e-4, 1e-6):
+        for dist, az in ((20.0, 0.3), (45.0, 1.9), (90.0, 4.0)):
+            name = "tiny%02d" % k
+            c = (dist * 0.3 * math.cos(az), dist, dist * 0.3 * math.sin(az))
+            obj.sphere(name, name, c, r, 8, 4)
+            mtls.append((name, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0))
+            lights.append((name, (4000.0, 3000.0, 2000.0)))
+            k += 1
+    obj.sphere("lamp", "lamp", (1.2, 2.2, -0.8), 0.25, 16, 8)
+    mtls.append(("lamp", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0))
+    lights.append(("lamp", (5.0, 5.0, 5.0)))
+    return _write(outdir, "tinyfar", obj, mtls, lights, CAM)
+
+
+STRESS = {"sphmix": (sphere_mix, 5200), "slivers": (slivers, 8 * 24 * 2 + 80), "tinyfar": (tiny_far, 12 * 48 + 224),
+          "dense": (dense_sphere, 14160)}

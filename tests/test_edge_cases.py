@@ -20,6 +20,13 @@ def rel_l2(g, c):
     return float(np.linalg.norm(g - c) / max(np.linalg.norm(c), 1e-300))
 
 
+def max_px_rel(g, c):
+    """max over pixels of ||g_px - c_px|| / ||c_px|| (pixels black in both count 0)"""
+    d = np.linalg.norm((g - c).reshape(-1, 3), axis=1)
+    n = np.linalg.norm(c.reshape(-1, 3), axis=1)
+    return float(np.max(np.where(n > 0, d / np.maximum(n, 1e-300), np.where(d > 0, np.inf, 0.0))))
+
+
 def pair(obj, xml, W, H, spp, mode):
     s = mcpt.Scene.load(obj, xml)
     g = s.camera()
@@ -66,7 +73,7 @@ def test_no_lights_renders_black(tmp_path, mode):
 def test_more_than_4096_candidates(tmp_path, mode, spp):
     """floor points under a 7200-triangle panel: every panel triangle is a candidate (113 batches)"""
     img, ref, st = pair(*scenegen.light_panel(str(tmp_path)), 16, 12, spp, mode)
-    assert ref.sum() > 0 and rel_l2(img, ref) <= L2_TOL, rel_l2(img, ref)
+    assert ref.sum() > 0 and rel_l2(img, ref) <= L2_TOL and max_px_rel(img, ref) <= L2_TOL, (rel_l2(img, ref), max_px_rel(img, ref))
     assert st.light_evals_candidates > 4096 * st.prep_full_nodes // 2
 
 
@@ -86,7 +93,7 @@ def test_root_cache_pick_paths(tmp_path, nx):
     assert sa.prep_cached_nodes > 0 and sb.prep_cached_nodes == 0
     assert a.sum() > 0 and rel_l2(a, b) <= 1e-12, rel_l2(a, b)
     img, ref, _ = pair(obj, xml, 24, 18, 4, "mis")
-    assert rel_l2(img, ref) <= L2_TOL, rel_l2(img, ref)
+    assert rel_l2(img, ref) <= L2_TOL and max_px_rel(img, ref) <= L2_TOL, (rel_l2(img, ref), max_px_rel(img, ref))
 
 
 @pytest.mark.gpu
@@ -95,7 +102,7 @@ def test_light_table_beyond_the_lds_list(tmp_path, mode):
     """N_L = 14160 > 7680: the LDS-queue prep variant, no root-point cache"""
     img, ref, st = pair(*scenegen.dense_sphere(str(tmp_path)), 16, 12, 4, mode)
     assert st.prep_cached_nodes == 0
-    assert ref.sum() > 0 and rel_l2(img, ref) <= L2_TOL, rel_l2(img, ref)
+    assert ref.sum() > 0 and rel_l2(img, ref) <= L2_TOL and max_px_rel(img, ref) <= L2_TOL, (rel_l2(img, ref), max_px_rel(img, ref))
 
 
 @pytest.mark.gpu
@@ -107,7 +114,7 @@ def test_tiny_and_odd_frames(W, H, spp, mode):
     e, _ = po.camera_ray(po.reference_camera(400, 300), 0, 0)
     o.build_grid(e)
     ref, _ = o.render(po.reference_camera(W, H), OMODE[mode], SEED, spp, nthreads=4)
-    assert img.shape == (H, W, 3) and rel_l2(img, ref) <= L2_TOL
+    assert img.shape == (H, W, 3) and rel_l2(img, ref) <= L2_TOL and max_px_rel(img, ref) <= L2_TOL
     if spp == 1:
         assert st.prep_cached_nodes == 0
 
@@ -155,4 +162,5 @@ def test_supercritical_tree_spills_and_matches_oracle(tmp_path):
     ref, ost = o.render(c, po.MODE_MIS, SEED, 2, nthreads=8)
     assert st.spilled_nodes > 0
     assert st.shading_nodes == st2.shading_nodes == int(ost[1])
-    assert ref.sum() > 0 and rel_l2(img, big) <= 1e-12 and rel_l2(img, ref) <= L2_TOL, (rel_l2(img, big), rel_l2(img, ref))
+    assert ref.sum() > 0 and rel_l2(img, big) <= 1e-12 and rel_l2(img, ref) <= L2_TOL and max_px_rel(img, ref) <= L2_TOL, (
+        rel_l2(img, big), rel_l2(img, ref), max_px_rel(img, ref))

@@ -1,0 +1,116 @@
+"""The exact light pick beyond the Veach stand-in (reference Mylight.cpp:322-482).
+
+The renderer's prep weighs light triangles with its fp64 Van Oosterom-Strackee form and redoes a pick
+with the reference's literal chain (k_prep_exact) whenever its slack lies inside the ambiguity band
+(DESIGN.md §4.3.3), whose constants were calibrated on the stand-in.  These scenes stress it
+(tests/scenegen.py STRESS):
+  * sphmix  -- spheres of 8x4 .. 64x32 segments, N_L = 5200 > 4096 (roots take the wave-per-root
+               k_prep_pick, 82 chunks);
+  * slivers -- light blinds seen edge-on from the floor next to them and a panel 2 degrees off the
+               vertical (spherical slivers, where the reference's sA is decided by its last bits);
+  * tinyfar -- tiny lights (radius 1e-2 .. 1e-6) 20-90 units away: the reference's sA is mostly its
+               own rounding, edge culls fire;
+  * dense   -- one sphere of 14 160 triangles > 7680: the LDS-queue prep (k_prep) without candidate
+               words and without root cache (k_prep_band must not read stale words).
+On each: 2 000 surface points through mcpt_light_prep vs the oracle -- survivor counts and picks EXACT,
+weights_sum within 1e-3 relative (the reference's own rounding noise; the literal fallback's nodes are
+bit-exact up to glibc's misrounded acos) -- and a 64x48 MIS frame vs the oracle at the same seed:
+relative L2 <= 1e-3 and every pixel <= 1e-3 (north star).  tools/band_margin_study.py --stress reports
+each scene's band margin (measured: veach x38, sphmix x11, slivers x2.7, dense x18; tinyfar: the band
+always covers the pick, every node takes the literal fallback).
+"""
+import numpy as np
+import pytest
+
+import monte_carlo_path_tracing_amd as mcpt
+from monte_carlo_path_tracing_amd import rng
+from oracle import pyoracle as po
+import scenegen
+
+pytestmark = pytest.mark.gpu
+SEED = 20240430
+TOL = 1e-3
+
+
+def rel_l2(g, c):
+    return float(np.linalg.norm(g - c) / max(np.linalg.norm(c), 1e-300))
+
+
+def max_px_rel(g, c):
+    d = np.linalg.norm((g - c).reshape(-1, 3), axis=1)
+    n = np.linalg.norm(c.reshape(-1, 3), axis=1)
+    return float(np.max(np.where(n > 0, d / np.maximum(n, 1e-300), np.where(d > 0, np.inf, 0.0))))
+
+
+def surface_points(osc, m, seed=3):
+    """m shading points area-sampled over the non-light facets (interpolated normals), and their u"""
+    v, _, light_of, _ = osc.facets()
+    P = v[:, :9].astype(np.float64).reshape(-1, 3, 3)
+    N = v[:, 9:].astype(np.float64).reshape(-1, 3, 3)
+    r = np.random.default_rng(seed)
+    nonlight = np.nonzero(light_of < 0)[0]
+    area = 0.5 * np.linalg.norm(np.cross(P[nonlight, 1] - P[nonlight, 0], P[nonlight, 2] - P[nonlight, 0]), axis=1)
+    fs = nonlight[r.choice(len(nonlight), m, p=area / area.sum())]
+    b = r.random((m, 2))
+    sw = b.sum(1) > 1
+    b[sw] = 1 - b[sw]
+    X = (1 - b.sum(1))[:, None] * P[fs, 0] + b[:, :1] * P[fs, 1] + b[:, 1:] * P[fs, 2]
+    Nn = (1 - b.sum(1))[:, None] * N[fs, 0] + b[:, :1] * N[fs, 1] + b[:, 1:] * N[fs, 2]
+    Nn /= np.linalg.norm(Nn, axis=1)[:, None]
+    u = np.array([rng.counter_uniform(SEED, k, 0, 1, 1) for k in range(m)])
+    return X, Nn, u
+
+
+@pytest.fixture(scope="module")
+def scenes(tmp_path_factory):
+    d = tmp_path_factory.mktemp("stress")
+    out = {}
+    for name, (make, nl) in scenegen.STRESS.items():
+        obj, xml = make(str(d / name))
+        out[name] = (obj, xml, nl)
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(scenegen.STRESS))
+def test_light_prep_picks_exact(scenes, name):
+    obj, xml, nl = scenes[name]
+    s = mcpt.Scene.load(obj, xml)
+    assert s.nlights == nl
+    osc = po.Scene(obj, xml)
+    X, N, u = surface_points(osc, 2000)
+    ws, cnt, pick = mcpt.light_prep(s, X, N, u)
+    ows = np.zeros(len(X))
+    ocnt = np.zeros(len(X), np.int32)
+    opick = np.zeros(len(X), np.int32)
+    for k in range(len(X)):
+        w, idx, _ = osc.light_prep(X[k], N[k])
+        ows[k], ocnt[k] = w, len(idx)
+        opick[k] = int(osc.light_sample_u(X[k], N[k], u[k], 0.5, 0.5)[0])
+    lit = ocnt > 0
+    rel = np.abs(ws - ows) / np.maximum(np.abs(ows), 1e-300)
+    print("%s: N_L %d, %d of %d points see lights; counts equal %d, picks equal %d; weights_sum max rel diff %.2e" % (
+        name, nl, lit.sum(), len(X), (cnt == ocnt).sum(), (pick == opick).sum(), rel[lit].max() if lit.any() else 0))
+    assert lit.sum() >= 200
+    assert np.array_equal(cnt, ocnt), np.nonzero(cnt != ocnt)[0][:10]
+    assert np.array_equal(pick, opick), np.nonzero(pick != opick)[0][:10]
+    assert rel[lit].max() <= TOL
+
+
+@pytest.mark.parametrize("name", sorted(scenegen.STRESS))
+def test_mis_frame_vs_oracle(scenes, name):
+    obj, xml, _ = scenes[name]
+    s = mcpt.Scene.load(obj, xml)
+    cam = s.camera()
+    cam.width, cam.height = 64, 48
+    img, st = mcpt.render(s, cam, 8, mode="mis", seed=SEED)
+    osc = po.Scene(obj, xml)
+    oc = osc.camera()
+    oc.width, oc.height = 64, 48
+    e, _ = po.camera_ray(oc, 0, 0)
+    osc.build_grid(e)
+    ref, _ = osc.render(oc, po.MODE_MIS, SEED, 8, nthreads=16)
+    l2, mx = rel_l2(img, ref), max_px_rel(img, ref)
+    print("%s 64x48x8 MIS: rel L2 %.3e, max per-pixel %.3e; %d shading nodes, %d band tests, %d exact preps" % (
+        name, l2, mx, st.shading_nodes, st.prep_band_nodes, st.prep_exact_nodes))
+    assert np.isfinite(img).all() and ref.sum() > 0
+    assert l2 <= TOL and mx <= TOL

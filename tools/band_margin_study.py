@@ -1,0 +1,150 @@
+"""Soundness margin of the exact pick's ambiguity band on any scene.
+
+The renderer's light prep weighs candidates with the Van Oosterom-Strackee excess (device_math.h
+sph_excess); the reference with its literal chain (Mylight.cpp:360-413: six acos, alpha + beta + gamma -
+pi).  A pick is taken from the fast weights only when its slack exceeds the band
+
+    band = 8 u sqrt(sum_c n_c m_c^2)                      (per 64-light chunk: n_c candidates,
+                                                           m_c = S_c + K_c (|x1 - c_c| + R_c))
+         + 0.25 u/2 sum_slivers 2 sum L sqrt(2 (4 - den)) / num   (candidates with 4 - den > 1000 num)
+         + (2 ncand + 4096) u W,
+
+with the constants of render.hip (MCPT_BAND_KAPPA, MCPT_BAND_SLIVER, MCPT_BAND_TAU; chunk constants as
+get_device_state builds them).  The band is sound if it bounds the difference of every prefix sum of
+the two weightings.  This script measures, per scene, max over points and prefixes of
+|prefix_fast - prefix_reference| / band (the reference's weights from the oracle, the fast weights in
+numpy long double): below 1 is sound, and 1 / that is the margin.  It also reports the share of points
+whose band exceeds 1e-3 of W (those go to the literal fallback almost whenever they pick).
+Test infrastructure only (loads the oracle).
+
+    python tools/band_margin_study.py [--points N] [obj xml ...]        (default: the Veach stand-in)
+    python tools/band_margin_study.py --stress                          (tests/scenegen.py STRESS scenes)
+"""
+import argparse
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from oracle import pyoracle as po  # noqa: E402
+
+U = 2.0 ** -53
+KAPPA, SLIVER, TAU = 8.0, 0.25, 1000.0
+
+
+def chunk_constants(P, lsum):
+    """per 64-light chunk: centre (float), radius, S, K as get_device_state (render.hip) builds them"""
+    NL = len(P)
+    out = []
+    for c in range((NL + 63) // 64):
+        sl = slice(64 * c, min(NL, 64 * c + 64))
+        pts = P[sl].reshape(-1, 3)
+        ctr = np.float32(0.5 * (pts.min(0) + pts.max(0))).astype(np.float64)
+        R = np.sqrt(((pts - ctr) ** 2).sum(1)).max()
+        e = np.stack([np.linalg.norm(P[sl, (k + 1) % 3] - P[sl, k], axis=1) for k in range(3)], 1).min(1)
+        S = lsum[sl].max()
+        K = np.where(e > 0, lsum[sl] / np.maximum(e, 1e-300), 1e30).max()
+        out.append((ctr, float(np.float32(R * (1 + 1e-6) + 1e-6)), float(np.float32(S * (1 + 1e-6))),
+                    float(np.float32(min(K * (1 + 1e-6), 1e30)))))
+    return out
+
+
+def surface_points(v, light_of, m, rng):
+    P = v[:, :9].astype(np.float64).reshape(-1, 3, 3)
+    N = v[:, 9:].astype(np.float64).reshape(-1, 3, 3)
+    nonlight = np.nonzero(light_of < 0)[0]
+    area = 0.5 * np.linalg.norm(np.cross(P[nonlight, 1] - P[nonlight, 0], P[nonlight, 2] - P[nonlight, 0]), axis=1)
+    fs = nonlight[rng.choice(len(nonlight), m, p=area / area.sum())]
+    b = rng.random((m, 2))
+    sw = b.sum(1) > 1
+    b[sw] = 1 - b[sw]
+    X = (1 - b.sum(1))[:, None] * P[fs, 0] + b[:, :1] * P[fs, 1] + b[:, 1:] * P[fs, 2]
+    Nn = (1 - b.sum(1))[:, None] * N[fs, 0] + b[:, :1] * N[fs, 1] + b[:, 1:] * N[fs, 2]
+    return X, Nn / np.linalg.norm(Nn, axis=1)[:, None]
+
+
+def study(obj, xml, npts, seed=11):
+    s = po.Scene(obj, xml)
+    v, mat, light_of, un = s.facets()
+    lf, la = s.lights()
+    if len(lf) == 0:
+        return None
+    P = v[:, :9].astype(np.float64).reshape(-1, 3, 3)[lf]
+    lsum = la[:, 1] + la[:, 2] + la[:, 3]
+    UN = un[lf]
+    cc = chunk_constants(P, lsum)
+    LP = P.astype(np.longdouble)
+    rng = np.random.default_rng(seed)
+    X, NN = surface_points(v, light_of, npts, rng)
+    worst, wide, used = 0.0, 0, 0
+    for x1, n in zip(X, NN):
+        ws, idx, w = s.light_prep(x1, n)
+        c1 = (UN * (x1 - P[:, 0])).sum(1) <= 1e-8
+        t = np.stack([((P[:, j] - x1) * n).sum(1) for j in range(3)], 0)
+        cand = np.nonzero(~(c1 | (t <= 1e-8).all(0)))[0]
+        if len(cand) == 0:
+            continue
+        used += 1
+        Xl = np.asarray(x1, np.longdouble)
+        a, b, c = LP[cand, 0] - Xl, LP[cand, 1] - Xl, LP[cand, 2] - Xl
+        A = a / np.sqrt((a * a).sum(1))[:, None]
+        B = b / np.sqrt((b * b).sum(1))[:, None]
+        C = c / np.sqrt((c * c).sum(1))[:, None]
+        num = np.abs((A * np.cross(B, C)).sum(1))
+        den = 1 + (A * B).sum(1) + (B * C).sum(1) + (C * A).sum(1)
+        wf = 2 * np.arctan2(num, den) * lsum[cand].astype(np.longdouble)
+        wf = np.where(wf > 0, wf, 0)
+        wr = np.zeros(len(cand), np.longdouble)
+        pos = np.searchsorted(cand, idx)
+        ok = (pos < len(cand)) & (cand[np.minimum(pos, len(cand) - 1)] == idx)
+        wr[pos[ok]] = w[ok]
+        err = np.abs(np.cumsum(wf) - np.cumsum(wr)).max()
+        err = max(float(err), float(abs(wf.sum() - np.longdouble(ws))))
+        b2 = 0.0
+        for ch in np.unique(cand // 64):
+            ctr, R, S, K = cc[ch]
+            m = S + K * (np.linalg.norm(x1 - ctr) + R)
+            b2 += (cand // 64 == ch).sum() * m * m
+        band = KAPPA * U * np.sqrt(b2) * 1.0001
+        numf, denf = num.astype(np.float64), den.astype(np.float64)
+        slv = TAU * numf + denf < 4.0
+        if slv.any():
+            band += SLIVER * 0.5 * U * float(np.sum(np.sqrt(2 * (4 - denf[slv])) / numf[slv] * 1.01 * 2 * lsum[cand][slv]))
+        band += (2 * len(cand) + 4096) * U * abs(ws)
+        worst = max(worst, err / band)
+        wide += band > 1e-3 * abs(ws)
+    return dict(points=used, worst_err_over_band=worst, margin=1.0 / worst if worst > 0 else np.inf,
+                wide_band_share=wide / max(used, 1), nlights=len(lf))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=400)
+    ap.add_argument("--stress", action="store_true")
+    ap.add_argument("files", nargs="*")
+    a = ap.parse_args()
+    scenes = []
+    if a.stress:
+        import scenegen
+        d = tempfile.mkdtemp()
+        for name, (make, _) in scenegen.STRESS.items():
+            scenes.append((name,) + tuple(make(os.path.join(d, name))))
+    for k in range(0, len(a.files), 2):
+        scenes.append((os.path.basename(a.files[k]),) + tuple(a.files[k:k + 2]))
+    if not scenes:
+        scenes = [("veach", os.path.join(ROOT, "scenes/veach-mis/veach-mis.obj"), os.path.join(ROOT, "scenes/veach-mis/veach-mis.xml"))]
+    for name, obj, xml in scenes:
+        r = study(obj, xml, a.points)
+        if r is None:
+            print("%-8s no lights" % name)
+            continue
+        print("%-8s N_L %5d, %4d points: max prefix error / band %.3f (margin x%.1f); band > 1e-3 W on %.3f of points" % (
+            name, r["nlights"], r["points"], r["worst_err_over_band"], r["margin"], r["wide_band_share"]))
+
+
+if __name__ == "__main__":
+    main()
