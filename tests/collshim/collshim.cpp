@@ -41,10 +41,14 @@ namespace {
 
 constexpr char kMagic[8] = {'M', 'C', 'P', 'T', 'S', 'H', 'I', 'M'};
 
+constexpr int kMaxRanks = 64;
 struct Hdr {  // in shared memory, zero-filled by ftruncate
     std::atomic<uint32_t> joined;
     std::atomic<uint32_t> left;
-    std::atomic<uint64_t> posted;  // non-root contributions posted so far (all calls)
+    // posted[r]: the last reduce call whose contribution rank r has posted.  Per rank, not one shared
+    // count: a non-root rank returns from its reduce at once and may post call s + 1 before a slower
+    // peer posts call s, so a total would let the root proceed without the slow peer's segment
+    std::atomic<uint64_t> posted[kMaxRanks];
 };
 static_assert(std::atomic<uint32_t>::is_always_lock_free && std::atomic<uint64_t>::is_always_lock_free,
               "shared-memory atomics must be lock-free");
@@ -131,11 +135,15 @@ ncclResult_t reduce_rank(const Op& o) {
         const hipError_t e = bytes ? hipMemcpy(p, o.send, bytes, hipMemcpyDeviceToHost) : hipSuccess;
         munmap(p, std::max<size_t>(bytes, 8));
         if (e != hipSuccess) return ncclUnhandledCudaError;
-        c->hdr->posted.fetch_add(1);
+        c->hdr->posted[c->rank].store(seq);
         return ncclSuccess;
     }
-    const uint64_t need = seq * (uint64_t)(c->nranks - 1);
-    if (!wait_for([&] { return c->hdr->posted.load() >= need; })) {
+    auto all_posted = [&] {
+        for (int r = 0; r < c->nranks; r++)
+            if (r != o.root && c->hdr->posted[r].load() < seq) return false;
+        return true;
+    };
+    if (!wait_for(all_posted)) {
         std::fprintf(stderr, "collshim: rank %d timed out waiting for reduce %llu\n", c->rank, (unsigned long long)seq);
         return ncclSystemError;
     }
@@ -233,7 +241,8 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
 }
 
 ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int rank) {
-    if (!comm || nranks < 1 || rank < 0 || rank >= nranks || std::memcmp(id.internal, kMagic, sizeof kMagic) != 0)
+    if (!comm || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks ||
+        std::memcmp(id.internal, kMagic, sizeof kMagic) != 0)
         return ncclInvalidArgument;
     auto* c = new Comm();
     c->nranks = nranks;
