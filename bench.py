@@ -329,7 +329,7 @@ def main():
         for n in names:
             head, _, tail = n.partition("*")
             for k, v in pk.items():
-                if (k == n or (tail and k.startswith(head) and k.endswith(tail))) and "valu_issue_frac" in v:
+                if (k == n or (tail and k.startswith(head) and k.endswith(tail))) and v.get("valu_issue_frac") is not None:
                     out[k] = v["valu_issue_frac"]
         return out
     dev_s = max(totals.get("seconds", 0.0), 1e-12)

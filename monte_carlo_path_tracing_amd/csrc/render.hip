@@ -3045,11 +3045,15 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
         wave_count2(cnt, visits, cnt + 1, tests);
         if (i >= n) return;
     }
-    const size_t o = (size_t)set * A.cap + i;
-    A.hf[o] = f;
-    if (set < 2) {
-        A.hbg[2 * o] = beta;
-        A.hbg[2 * o + 1] = gamma;
+    // only a traced set's slots are written (its consumers test the node's flags first), and (beta,
+    // gamma) only for a hit: 4 B per miss instead of 20 B per node and set
+    if (fl & (1 << set)) {
+        const size_t o = (size_t)set * A.cap + i;
+        A.hf[o] = f;
+        if (set < 2 && f >= 0) {
+            A.hbg[2 * o] = beta;
+            A.hbg[2 * o + 1] = gamma;
+        }
     }
 }
 
@@ -3145,10 +3149,10 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
         --sp;
         return sp < kPersistLds ? lds[sp * stride] : spill[sp - kPersistLds];
     };
-    auto finish = [&]() {  // the lane's ray is done: store its hit
+    auto finish = [&]() {  // the lane's traced ray is done: store its hit ((beta, gamma) only for a hit)
         const size_t o = (size_t)set * A.cap + ii;
         A.hf[o] = best.f;
-        if (set < 2) {
+        if (set < 2 && best.f >= 0) {
             A.hbg[2 * o] = best.beta;
             A.hbg[2 * o + 1] = best.gamma;
         }
@@ -3209,7 +3213,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                             busy = true;
                         }
                     } else {
-                        finish();  // this set is not traced for this node: no hit
+                        busy = false;  // this set is not traced for this node: nothing to store
                     }
                 }
             }

@@ -143,3 +143,78 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def fan_study(m=400):
+    """The boundary-edge (fan) form of a group's weight: sum over the candidate triangles of a light group
+    of their spherical excess = sum over the candidate set's boundary edges (a -> b, in the triangle's
+    winding about its outward unique normal) of the signed solid angle of (r, a, b), r = the direction
+    to the group's centre.  Checks the identity against the per-triangle VOS sum and counts the
+    boundary edges per (point, group)."""
+    s = po.Scene("scenes/veach-mis/veach-mis.obj", "scenes/veach-mis/veach-mis.xml")
+    v, mat, light_of, un = s.facets()
+    lf, la = s.lights()
+    P = v[:, :9].astype(np.float64).reshape(-1, 3, 3)[lf]
+    UN = un[lf]
+    NL = len(lf)
+    # orient every triangle CCW about its unique normal
+    cr = np.cross(P[:, 1] - P[:, 0], P[:, 2] - P[:, 0])
+    flip = (cr * UN).sum(1) < 0
+    P[flip] = P[flip][:, [0, 2, 1]]
+    gid = mat[lf]
+    # adjacency by exact vertex positions within a group: edge k of t = (P[t,k] -> P[t,k+1])
+    key = {}
+    for t in range(NL):
+        for k in range(3):
+            a, b = P[t, k].tobytes(), P[t, (k + 1) % 3].tobytes()
+            key[(gid[t], a, b)] = (t, k)
+    nb = -np.ones((NL, 3), np.int64)
+    bad = 0
+    for t in range(NL):
+        for k in range(3):
+            a, b = P[t, k].tobytes(), P[t, (k + 1) % 3].tobytes()
+            o = key.get((gid[t], b, a))
+            if o is None:
+                bad += (gid[t], a, b) in key and False
+            else:
+                nb[t, k] = o[0]
+    print("edges without an opposite twin: %d of %d" % ((nb < 0).sum(), 3 * NL))
+    cam = po.reference_camera(800, 600)
+    e, _ = po.camera_ray(cam, 0, 0)
+    s.build_grid(e)
+    X, N = secondary_points(s, cam, m, np.random.default_rng(5))
+    groups = [np.nonzero(gid == g)[0] for g in np.unique(gid)]
+    ctrs = [P[idx].reshape(-1, 3).mean(0) for idx in groups]
+    worst, nedges, ncand = 0.0, [], []
+    for x1, n in zip(X, N):
+        c1 = (UN * (x1 - P[:, 0])).sum(1) <= 1e-8
+        t = np.stack([((P[:, j] - x1) * n).sum(1) for j in range(3)], 0)
+        cand = ~(c1 | (t <= 1e-8).all(0))
+        for gi, idx in enumerate(groups):
+            ci = idx[cand[idx]]
+            if len(ci) == 0:
+                continue
+            A = P[ci] - x1
+            A /= np.linalg.norm(A, axis=2)[..., None]
+            num = (A[:, 0] * np.cross(A[:, 1], A[:, 2])).sum(1)
+            den = 1 + (A[:, 0] * A[:, 1]).sum(1) + (A[:, 1] * A[:, 2]).sum(1) + (A[:, 2] * A[:, 0]).sum(1)
+            tri = 2 * np.arctan2(np.abs(num), den)
+            r = ctrs[gi] - x1
+            r /= np.linalg.norm(r)
+            tot, ne = 0.0, 0
+            for t_ in ci:
+                for k in range(3):
+                    o = nb[t_, k]
+                    if o >= 0 and cand[o]:
+                        continue
+                    a = P[t_, k] - x1
+                    b = P[t_, (k + 1) % 3] - x1
+                    a /= np.linalg.norm(a)
+                    b /= np.linalg.norm(b)
+                    tot += 2 * np.arctan2(r @ np.cross(a, b), 1 + r @ a + a @ b + b @ r)
+                    ne += 1
+            worst = max(worst, abs(abs(tot) - tri.sum()) / tri.sum())
+            nedges.append(ne)
+            ncand.append(len(ci))
+    print("fan vs per-triangle sum: max rel diff %.2e; boundary edges per (point, group) mean %.1f, candidates %.1f" % (
+        worst, np.mean(nedges), np.mean(ncand)))

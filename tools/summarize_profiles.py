@@ -22,6 +22,9 @@ least 4 cycles, the transcendentals longer: a lower bound, <= 1 up to the GRBM c
 WIDE_LOAD_KERNELS = ("k_prep_pk2", "k_mis_rays", "k_rays_persistent", "k_extend_brdf", "k_primary")
 
 
+MIN_US, MAX_CLOCK_GHZ = 100, 2.5  # valu_issue_frac is reported only for dispatches this long and clocks this plausible
+
+
 def wide(kernel):
     return kernel.startswith(WIDE_LOAD_KERNELS)
 import argparse
@@ -72,6 +75,14 @@ def pmc_latest(tag, summary):
         if k in ks:
             e["avg_us"] = ks[k]["avg_us"]
             e["eff_clock_GHz"] = round(g / 8 / (ks[k]["avg_us"] * 1e-6) / 1e9, 3)
+            # GRBM_GUI_ACTIVE counts the busy cycles around a dispatch, not its own: for kernels of
+            # tens of microseconds it overstates the cycles (an effective clock above the chip's
+            # 2.4 GHz), so the issue fraction is not reported there
+            if e["avg_us"] < MIN_US or e["eff_clock_GHz"] > MAX_CLOCK_GHZ:
+                e["valu_issue_frac"] = None
+                e["valu_issue_frac_note"] = ("dropped: %.1f us per dispatch, effective clock %.2f GHz (reported only "
+                                             "for >= %d us and <= %.1f GHz)" % (e["avg_us"], e["eff_clock_GHz"], MIN_US,
+                                                                                MAX_CLOCK_GHZ))
         out["kernels"][k] = e
     return out
 
