@@ -101,9 +101,10 @@ struct DScene {
                               // area normal in .w, then 2 RadianceRGB::sum() as fp64 bits)
     const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
     // the boundary-edge form of the prep (FanGrp, k_prep_fan)
-    const FanGrp* fan_grp;    // fan_ngroups
-    const int4* fan_nbr;      // NL: the light across edge k (p0 p1, p1 p2, p2 p0) or -1 (a boundary edge); w = group
-    int fan_ngroups;
+    const FanGrp* fan_grp;    // fan_nslots: the eligible groups, ascending (at most kFanMaxGroups)
+    const int2* fan_nbr;      // 64 nchunks: the lights across edges 0, 1 (x), 2 (y) as 16-bit fields, 0xFFFF = none;
+                              // bit 16 of y = flip (the reference vertex order is the negative one)
+    int fan_nslots;
     int fan_on;               // some group is eligible and N_L < 8192 (13-bit light indices in k_prep_fan's list)
     // exact-pick band: per 64-light chunk a bounding sphere (centre, radius) of its
     // vertices and (max sum L, max sum L / shortest edge) of its lights; the same over the whole table
@@ -2253,6 +2254,13 @@ constexpr int kFanMaxGroups = 8;   // groups per node taken through the edge for
 constexpr int kFanMinCand = 48;    // a group with fewer candidates is weighed one by one
 constexpr int kFanSusp = 128;      // LDS room for a node's suspects (more: the literal fallback)
 constexpr double kFanErr = 32.0;   // |rounding of one fan term| <= kFanErr u 2 sum L (unit vectors, dots, atan)
+constexpr int kFanSlotBytes = kFanMaxGroups * (int)sizeof(FanGrp);  // the slot table at the start of the block's LDS
+constexpr int kFanNbrBatch = 8;    // neighbour-table words in flight at once
+__device__ inline double rdlane(double v, int l) {  // lane l's value (l wave-uniform)
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double((long long)(((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l) << 32) |
+                                            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l)));
+}
 __host__ __device__ inline int fan_item_cap(int nchunks) { return 64 * nchunks + 128 * kFanMaxGroups + 64; }
 __host__ __device__ inline int fan_wave_bytes(int nchunks) {
     const int icap = fan_item_cap(nchunks), nbc = icap / 64;
@@ -2289,7 +2297,13 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, ui
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     const int icap = fan_item_cap(nchunks), nbc = icap / 64;
-    char* base_lds = reinterpret_cast<char*>(prep_lds) + (size_t)wib * wave_bytes;
+    // the slots (eligible groups, ascending) in LDS, once per block
+    FanGrp* slots = reinterpret_cast<FanGrp*>(prep_lds);
+    const int nslots = min(S.fan_nslots, kFanMaxGroups);
+    for (int i = threadIdx.x; i < nslots * (int)(sizeof(FanGrp) / 8); i += blockDim.x)
+        reinterpret_cast<double*>(slots)[i] = reinterpret_cast<const double*>(S.fan_grp)[i];
+    __syncthreads();
+    char* base_lds = reinterpret_cast<char*>(prep_lds) + kFanSlotBytes + (size_t)wib * wave_bytes;
     uint64_t* wd = reinterpret_cast<uint64_t*>(base_lds);
     double* bt = reinterpret_cast<double*>(base_lds + nchunks * 8);
     int* seg = reinterpret_cast<int*>(base_lds + nchunks * 8 + nbc * 8);
@@ -2313,90 +2327,115 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, ui
         const d3 x1 = ld3(qp, qs, node);
         const uint64_t* __restrict__ mrow = masks + (size_t)node * mask_stride(nchunks);
         const uint64_t* __restrict__ srow = smasks + (size_t)node * mask_stride(nchunks);
-        for (int c = lane; c < nchunks; c += 64) wd[c] = mrow[c];
+        // the node's words in registers, lane c holding words c and c + 64 (nchunks <= 128 for a fan
+        // scene), and in LDS for the neighbour tests; a word at a wave-uniform index is two readlanes
+        const uint64_t w0 = lane < nchunks ? mrow[lane] : 0ull, w1 = lane + 64 < nchunks ? mrow[lane + 64] : 0ull;
+        const uint64_t sr0 = lane < nchunks ? srow[lane] : 0ull, sr1 = lane + 64 < nchunks ? srow[lane + 64] : 0ull;
+        if (lane < nchunks) wd[lane] = w0;
+        if (lane + 64 < nchunks) wd[lane + 64] = w1;
         for (int b = lane; b < nbc; b += 64) seg[b] = -1;
+        auto word = [&](int c) -> uint64_t {  // c wave-uniform
+            const uint64_t w = c < 64 ? w0 : w1;
+            const int l = c & 63;
+            return ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(w >> 32), l) << 32) |
+                   (unsigned)__builtin_amdgcn_readlane((int)(unsigned)w, l);
+        };
+        const unsigned* wd32 = reinterpret_cast<const unsigned*>(wd);
+        // lane s: slot s's direction r from x1 and whether x1 meets its conditions -- outside the bounding
+        // sphere (every vertex in the open hemisphere around r), and no candidate whose projected edges are
+        // all below ~1e-8 rad (build_fan_tables)
+        d3 rcl = mk3(0.0, 0.0, 1.0);
+        bool okl = false;
+        if (lane < nslots) {
+            const FanGrp& fg = slots[lane];
+            const d3 dv = mk3(fg.c[0] - x1.x, fg.c[1] - x1.y, fg.c[2] - x1.z);
+            const double dist = sqrt(dv.x * dv.x + dv.y * dv.y + dv.z * dv.z);
+            okl = dist > fg.R && fg.lmin > 1e-4 * (dist + fg.R) && nchunks <= 128;
+            if (okl) rcl = funit(dv);
+        }
+        const uint64_t slot_ok = __ballot(okl);
         wave_lds_sync();
         // ---- phase 1: the list ----
-        int nitems = 0, ncand = 0, total = 0;
-        for (int c = 0; c < nchunks; c++) total += __popcll(mrow[c]);
+        int nitems = 0, ncand = 0;
+        const int total = __builtin_amdgcn_readfirstlane(wave_sum_int(__popcll(w0) + __popcll(w1)));
         unsigned fanmask = 0;
-        double facc = 0;  // 2 sum L over this lane's edge items (the fan band term)
+        uint64_t fw0 = 0, fw1 = 0;  // the fan groups' lights (lane-parallel words, as w0 / w1)
+        double facc = 0;            // sum over the edge items of 2 sum L (the fan band term; wave-uniform)
         auto pad64 = [&]() {
             const int up = (nitems + 63) & ~63;
             if (nitems + lane < up) items[nitems + lane] = kPad;
             nitems = up;
         };
-        for (int g = 0; g < S.fan_ngroups; g++) {
-            const FanGrp& fg = S.fan_grp[g];
-            const int f0 = fg.first, f1 = fg.first + fg.count;
-            if (f1 <= f0) continue;
-            const int c0 = f0 >> 6, c1 = (f1 - 1) >> 6;
-            int ng = 0;
-            for (int c = c0; c <= c1; c++) ng += __popcll(mrow[c] & range_bits(c, f0, f1));
+        const unsigned lds_items = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)items);
+        auto append_range = [&](int f0, int f1) {  // candidates of [f0, f1) one by one, in index order
+            int k = 0;
+            for (int c = f0 >> 6; c <= (f1 - 1) >> 6; c++) {
+                const uint64_t m = uniform_u64(word(c) & range_bits(c, f0, f1));
+                if (m == 0) continue;
+                append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_items + 2u * (unsigned)nitems, (unsigned)lane + 64u * (unsigned)c);
+                nitems += __popcll(m);
+                k += __popcll(m);
+            }
+            return k;
+        };
+        int prev = 0;
+        for (int g = 0; g <= nslots; g++) {
+            // the lights between the previous slot and this one (or the table's end): one by one
+            const int f0 = g < nslots ? slots[g].first : S.NL;
+            if (f0 > prev) ncand += append_range(prev, f0);
+            if (g == nslots) break;
+            const int f1 = f0 + slots[g].count;
+            prev = f1;
+            const uint64_t r0 = range_bits(lane, f0, f1), r1 = range_bits(lane + 64, f0, f1);
+            const int ng = __builtin_amdgcn_readfirstlane(wave_sum_int(__popcll(w0 & r0) + __popcll(w1 & r1)));
             if (ng == 0) continue;
             ncand += ng;
-            bool fan = false;
-            if (fg.ok && g < kFanMaxGroups && ng >= kFanMinCand) {
-                const double dx = x1.x - fg.c[0], dy = x1.y - fg.c[1], dz = x1.z - fg.c[2];
-                const double dist = sqrt(dx * dx + dy * dy + dz * dz);
-                // x1 outside the bounding sphere (every vertex in the open hemisphere around r), and no
-                // candidate whose projected edges are all below ~1e-8 rad (build_fan_tables)
-                fan = dist > fg.R && fg.lmin > 1e-4 * (dist + fg.R);
-            }
+            // room: the items left for the candidates after this group (one each) and two paddings;
+            // a ragged candidate set that would not fit is weighed one by one instead
+            const bool fan = ((slot_ok >> g) & 1) && ng >= kFanMinCand && nitems + 64 + 3 * ng <= icap - (total - ncand) - 128;
             if (!fan) {
-                const unsigned lds_items = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)items);
-                for (int c = c0; c <= c1; c++) {
-                    const uint64_t m = uniform_u64(mrow[c] & range_bits(c, f0, f1));
-                    if (m == 0) continue;
-                    append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_items + 2u * (unsigned)nitems, (unsigned)lane + 64u * (unsigned)c);
-                    nitems += __popcll(m);
-                }
+                append_range(f0, f1);
                 continue;
             }
-            const int start = nitems;
             pad64();
             const int b0 = nitems >> 6;
-            // room: the items left for the candidates after this group (one each) and two paddings
-            const int limit = icap - (total - ncand) - 128;
-            bool room = true;
-            double fg_acc = 0;
-            for (int c = c0; c <= c1 && room; c++) {
-                const uint64_t m = mrow[c] & range_bits(c, f0, f1);
-                if (m == 0) continue;
-                if (nitems + 3 * __popcll(m) > limit) {  // a ragged candidate set: weighed one by one instead
-                    room = false;
-                    break;
-                }
-                const int li = 64 * c + lane;
-                const bool mine = (m >> lane) & 1;
-                const int4 nb = mine ? S.fan_nbr[li] : make_int4(0, 0, 0, 0);
-                const unsigned flip = ((unsigned)nb.w >> 30) & 1u;
+            const int c0 = f0 >> 6, c1 = (f1 - 1) >> 6;
+            int nedge = 0;
+            for (int cb = c0; cb <= c1; cb += kFanNbrBatch) {
+                // the neighbour entries of kFanNbrBatch words in flight at once (the table is padded to
+                // whole words; past the group's last word the loads repeat it)
+                int2 q8[kFanNbrBatch];
 #pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    const int o = k == 0 ? nb.x : k == 1 ? nb.y : nb.z;
-                    const bool bnd = mine && (o < 0 || !((wd[o >> 6] >> (o & 63)) & 1ull));
-                    const uint64_t bm = __ballot(bnd);
-                    if (bm == 0) continue;
-                    if (bnd) {
-                        items[nitems + lane_rank(bm)] = (unsigned short)((unsigned)li | ((unsigned)(k + 1) << 13) | (flip << 15));
-                        fg_acc += fg.lsum2;
-                    }
-                    nitems += __popcll(bm);
-                }
-            }
-            if (!room) {  // undo the group's edge items, then its candidates one by one
-                nitems = start;
-                const unsigned lds_items = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)items);
-                for (int c = c0; c <= c1; c++) {
-                    const uint64_t m = uniform_u64(mrow[c] & range_bits(c, f0, f1));
+                for (int q = 0; q < kFanNbrBatch; q++) q8[q] = S.fan_nbr[64 * min(cb + q, c1) + lane];
+#pragma unroll
+                for (int q = 0; q < kFanNbrBatch; q++) {
+                    const int c = cb + q;
+                    if (c > c1) break;
+                    const uint64_t m = uniform_u64(word(c) & range_bits(c, f0, f1));
                     if (m == 0) continue;
-                    append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_items + 2u * (unsigned)nitems, (unsigned)lane + 64u * (unsigned)c);
-                    nitems += __popcll(m);
+                    const unsigned li = 64u * (unsigned)c + (unsigned)lane;
+                    const bool mine = (m >> lane) & 1;
+                    const unsigned tag = li | ((((unsigned)q8[q].y >> 16) & 1u) << 15);
+                    // candidate bits of the three neighbours (0xFFFF: no twin, a boundary edge)
+                    const unsigned o0 = (unsigned)q8[q].x & 0xFFFFu, o1 = (unsigned)q8[q].x >> 16, o2 = (unsigned)q8[q].y & 0xFFFFu;
+                    const unsigned v0 = wd32[(o0 & 0x1FFFu) >> 5], v1 = wd32[(o1 & 0x1FFFu) >> 5], v2 = wd32[(o2 & 0x1FFFu) >> 5];
+                    const bool e0 = mine && (o0 == 0xFFFFu || !((v0 >> (o0 & 31)) & 1u));
+                    const bool e1 = mine && (o1 == 0xFFFFu || !((v1 >> (o1 & 31)) & 1u));
+                    const bool e2 = mine && (o2 == 0xFFFFu || !((v2 >> (o2 & 31)) & 1u));
+                    const uint64_t m0 = __ballot(e0), m1 = __ballot(e1), m2 = __ballot(e2);
+                    if (e0) items[nitems + lane_rank(m0)] = (unsigned short)(tag | (1u << 13));
+                    nitems += __popcll(m0);
+                    if (e1) items[nitems + lane_rank(m1)] = (unsigned short)(tag | (2u << 13));
+                    nitems += __popcll(m1);
+                    if (e2) items[nitems + lane_rank(m2)] = (unsigned short)(tag | (3u << 13));
+                    nitems += __popcll(m2);
+                    nedge += __popcll(m0) + __popcll(m1) + __popcll(m2);
                 }
-                continue;
             }
             fanmask |= 1u << g;
-            facc += fg_acc;
+            fw0 |= r0;
+            fw1 |= r1;
+            facc += (double)nedge * slots[g].lsum2;
             pad64();
             for (int b = b0 + lane; b < (nitems >> 6); b += 64) seg[b] = g;
         }
@@ -2407,20 +2446,25 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, ui
         int nsusp = 0;
         bool force_exact = false;
         if (fanmask) {
-            for (int c = 0; c < nchunks; c++) {
-                const uint64_t m = srow[c] & mrow[c];
-                if (m == 0) continue;
-                const int li = 64 * c + lane;
-                const bool mine = (m >> lane) & 1;
-                const int gi = mine ? (S.fan_nbr[li].w & 0x3fffffff) : 31;
-                const bool inf = mine && gi < 32 && ((fanmask >> gi) & 1u);
-                const uint64_t sm = __ballot(inf);
-                if (nsusp + __popcll(sm) > kFanSusp) {
-                    force_exact = true;
-                    break;
+            const uint64_t s0 = sr0 & w0 & fw0, s1 = sr1 & w1 & fw1;
+            const int ns = __builtin_amdgcn_readfirstlane(wave_sum_int(__popcll(s0) + __popcll(s1)));
+            if (ns > kFanSusp) {
+                force_exact = true;
+            } else if (ns > 0) {
+                const unsigned lds_susp = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)susp);
+                for (int h = 0; h < 2; h++) {
+                    uint64_t nz = __ballot((h ? s1 : s0) != 0);
+                    while (nz) {
+                        const int l = __ffsll((unsigned long long)nz) - 1;
+                        nz &= nz - 1;
+                        const uint64_t sw = h ? s1 : s0;
+                        const uint64_t m = uniform_u64(((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(sw >> 32), l) << 32) |
+                                                       (unsigned)__builtin_amdgcn_readlane((int)(unsigned)sw, l));
+                        append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_susp + 2u * (unsigned)nsusp,
+                                      (unsigned)lane + 64u * (unsigned)(l + 64 * h));
+                        nsusp += __popcll(m);
+                    }
                 }
-                if (inf) susp[nsusp + lane_rank(sm)] = (unsigned short)li;
-                nsusp += __popcll(sm);
             }
         }
         wave_lds_sync();
@@ -2454,8 +2498,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, ui
                     }
                 } else if (it != kPad) {  // a fan group's boundary edge
                     const int li = (int)(it & 0x1fffu), k = (int)((it >> 13) & 3u) - 1;
-                    const FanGrp& fg = S.fan_grp[sg];
-                    const d3 rc = funit(mk3(fg.c[0] - x1.x, fg.c[1] - x1.y, fg.c[2] - x1.z));
+                    const d3 rc = mk3(rdlane(rcl.x, sg), rdlane(rcl.y, sg), rdlane(rcl.z, sg));
                     const v4u a = struct_load_b128(rw, li, 0, 0, 0);
                     const v4u b = struct_load_b128(rw, li, 16, 0, 0);
                     const v4u c = struct_load_b128(rw, li, 32, 0, 0);
@@ -2466,7 +2509,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, ui
                     const d3 p2 = mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y));
                     const d3 pa = k == 0 ? p0 : k == 1 ? p1 : p2, pb = k == 0 ? p1 : k == 1 ? p2 : p0;
                     const double h = fan_half(rc, funit(sub(pa, x1)), funit(sub(pb, x1)));
-                    w4[i] = (it >> 15 ? -h : h) * fg.lsum2;
+                    w4[i] = (it >> 15 ? -h : h) * slots[sg].lsum2;
                     ed++;
                 }
             }
@@ -2572,12 +2615,10 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, ui
                 margin = pick_margin(base, sc, pl, target);
             }
         } else if (kb >= 0) {  // a fan group: its candidates' weights in index order
-            const FanGrp& fg = S.fan_grp[sgk];
-            const int f0 = fg.first, f1 = fg.first + fg.count;
+            const int f0 = slots[sgk].first, f1 = f0 + slots[sgk].count;
             wave_lds_sync();
-            const unsigned lds_items = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)items);
             for (int c = f0 >> 6; c <= (f1 - 1) >> 6; c++) {
-                const uint64_t m = uniform_u64(mrow[c] & range_bits(c, f0, f1));
+                const uint64_t m = uniform_u64(word(c) & range_bits(c, f0, f1));
                 if (m == 0) continue;
                 append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_items + 2u * (unsigned)ncg, (unsigned)lane + 64u * (unsigned)c);
                 ncg += __popcll(m);
@@ -2653,7 +2694,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, ui
         }
         if (C.slack) {
             const double band_sl = __ballot(sacc > 0.0) ? band_sliver(__shfl(wave_incl_scan(sacc, lane), 63)) : 0.0;
-            const double fan_band = fanmask ? kFanErr * kU53 * __shfl(wave_incl_scan(facc, lane), 63) : 0.0;
+            const double fan_band = kFanErr * kU53 * facc;
             double sl = pick_slack(margin, wsum) - (band_sl + fan_band + band_round(ncand + nitems, wsum));
             if (force_exact) sl = -INFINITY;
             if (C.exact_counts && (survivors < ncand || __ballot(ndeg != 0))) sl = -INFINITY;
@@ -4560,10 +4601,21 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     std::vector<int4> fnbr;
     std::vector<float> feps;
     build_fan_tables(s, lv, ln, fgrp, fnbr, feps);
-    d.fan_ngroups = (int)s.group_start.size();
-    d.fan_on = 0;
-    for (int g = 0; g < d.fan_ngroups; g++) d.fan_on |= fgrp[g].ok;
-    if ((rc = upload(*D, fgrp, &d.fan_grp)) || (rc = upload(*D, fnbr, &d.fan_nbr))) return rc;
+    // the device form: the eligible groups (the first kFanMaxGroups of them) as k_prep_fan's slots, and
+    // the neighbour table packed to 8 B per light, padded to whole 64-light words
+    std::vector<FanGrp> fslot;
+    for (const FanGrp& g : fgrp)
+        if (g.ok && g.count > 0 && (int)fslot.size() < kFanMaxGroups) fslot.push_back(g);
+    d.fan_nslots = (int)fslot.size();
+    d.fan_on = d.fan_nslots > 0;
+    if (fslot.empty()) fslot.push_back(FanGrp{});
+    std::vector<int2> fnb(64 * (size_t)std::max(prep_chunks(s.NL), 1), make_int2(-1, 0xFFFF));
+    for (int l = 0; l < s.NL && d.fan_on; l++) {
+        auto f16 = [](int o) { return o < 0 ? 0xFFFFu : (unsigned)o; };
+        fnb[l] = make_int2((int)(f16(fnbr[l].x) | f16(fnbr[l].y) << 16),
+                           (int)(f16(fnbr[l].z) | (((unsigned)fnbr[l].w >> 30) & 1u) << 16));
+    }
+    if ((rc = upload(*D, fslot, &d.fan_grp)) || (rc = upload(*D, fnb, &d.fan_nbr))) return rc;
     std::vector<LightPair> lpr(32 * (size_t)std::max(prep_chunks(s.NL), 1));
     for (size_t q = 0; q < lpr.size(); q++) {
         LightPair& P = lpr[q];
@@ -4889,7 +4941,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
                                d, n, qp, qn, qs, masks, nchunks, stats, smasks);
         const int fb = fan_wave_bytes(nchunks);
         auto kf = fb <= 10 * 1024 ? k_prep_fan<kFanWaves> : k_prep_fan<2>;
-        hipLaunchKernelGGL(kf, dim3(blocks), dim3(256), 4 * fb, st, d, seed, n, qp, qs, qpixel, qsample, qnode, u, wsum, pick,
+        hipLaunchKernelGGL(kf, dim3(blocks), dim3(256), kFanSlotBytes + 4 * fb, st, d, seed, n, qp, qs, qpixel, qsample, qnode, u, wsum, pick,
                            count, stats, nchunks, fb, work, cache, (const uint64_t*)masks, (const uint64_t*)smasks);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
         if (count_c1 || !stats)
