@@ -41,10 +41,6 @@ HBM_PEAK_GBS = 8000.0
 FLOPS_CULL_BACKFACE = 8
 FLOPS_CULL_PLANE = 32
 FLOPS_FULL = 269
-# the boundary-edge light prep weighs a light group by its candidate set's boundary
-# edges: per edge two unit vectors (2 x 15), r.(A x B) (14), 1 + r.A + A.B + B.r (18), atan2 (~12) and
-# the scaling (1) -- only the candidates it weighs one by one cost FLOPS_FULL
-FLOPS_FAN_EDGE = 75
 # algorithmic HBM bytes of one prep node: reads p, N (48 B) + pixel, sample, node id (16 B) for the
 # RNG key; writes weights_sum + pick (12 B).  The light table (240 KB) is L2/MALL resident.
 PREP_BYTES_PER_NODE = 76
@@ -345,14 +341,7 @@ def main():
                                                        "light_evals_candidates"))
         launches = max(totals.get("prep_launches", 0), 1)
         c2 = ev_tot - c1 - cand
-        weighed, edges = totals.get("light_evals_weighed", 0), totals.get("prep_fan_edges", 0)
-        if not weighed and not edges:  # a library without the counters: every candidate weighed
-            weighed = cand
-        # the work the prep's algorithm does: cheap stages for every (node, light), a full-stage weight for
-        # every candidate it weighs one by one, a fan term per boundary edge
-        flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + weighed * FLOPS_FULL + edges * FLOPS_FAN_EDGE
-        # the reference's formulation of the same preps: every candidate weighed (Mylight.cpp:360-413)
-        flops_ref = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
+        flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
         t_launch = prep_s / launches
         achieved = flops / launches / t_launch / 1e12
         nodes = totals.get("prep_full_nodes", 0)
@@ -364,13 +353,11 @@ def main():
                     "profiles/k_prep_hbm_bytes_per_node.json) x this run's %.0f full-prep nodes per launch"
                     % (hb["hbm_bytes_per_node"], nodes / launches))
         alg_gbs = nodes * PREP_BYTES_PER_NODE / prep_s / 1e9
-        fan_nodes = totals.get("prep_fan_nodes", 0)
         roof_prep = {
-            "bound": "valu_fp64", "kernel": "k_prep_cull_lanes+" + ("k_prep_fan" if fan_nodes else "k_prep_pk2"),
-            "achieved": round(achieved, 3),
+            "bound": "valu_fp64", "kernel": "k_prep_cull_lanes+k_prep_pk2", "achieved": round(achieved, 3),
             "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": tsrc,
-            "valu_issue_frac": busy("k_prep_cull_lanes<false>", "k_prep_cull_lanes<false, true>", "k_prep_fan<*>",
+            "valu_issue_frac": busy("k_prep_cull_lanes<false>",
                               "k_prep_pk2<*, false, true, %s>" % ("true" if args.precision == "fp32" else "false")),
             "valu_issue_frac_source": pmc.get("source"),
             "hbm_frac_algorithmic": round(alg_gbs / HBM_PEAK_GBS, 5),
@@ -378,11 +365,7 @@ def main():
             "avg_launch_ms": round(t_launch * 1e3, 3), "launches": launches, "flop_per_launch": flops / launches,
             "share_of_device_time": round(prep_s / dev_s, 3), "hbm_algorithmic_GBs": round(alg_gbs, 3),
             "full_prep_nodes": nodes, "cached_root_nodes": totals.get("prep_cached_nodes", 0),
-            "hbm_peak_GBs": HBM_PEAK_GBS,
-            # the boundary-edge form's work split, and the reference formulation's work per second (every
-            # candidate weighed: NOT a roofline figure -- it may exceed the peak when edges replace weights)
-            "fan_nodes": fan_nodes, "candidates": cand, "weighed": weighed, "fan_edges": edges,
-            "reference_formulation_TFLOPs": round(flops_ref / prep_s / 1e12, 3)}
+            "hbm_peak_GBs": HBM_PEAK_GBS}
     # ---- roofline of the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf) ----
     roof_trace = None
     tr_s, tr_n = totals.get("trace_seconds", 0.0), max(totals.get("trace_launches", 0), 1)

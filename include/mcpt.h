@@ -23,9 +23,7 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 20200 /* 2.2.0: mcpt_stats gains light_evals_weighed, prep_fan_edges and prep_fan_nodes
-                               * (appended: the boundary-edge light prep);
-                               * 2.1.0: mcpt_stats gains prep_exact_nodes, cache_build_seconds and prep_band_nodes
+#define MCPT_VERSION 20100 /* 2.1.0: mcpt_stats gains prep_exact_nodes, cache_build_seconds and prep_band_nodes
                                * (appended);
                                * 2.0.0: mcpt_render_opts carries struct_size (checked first), a device list
                                * and a multi-process communicator; debug entry points moved to mcpt_debug.h */
@@ -185,12 +183,6 @@ typedef struct {
     double cache_build_seconds; /* device time building the per-pixel root-point cache (in prep_seconds) */
     uint64_t prep_band_nodes;   /* light preps whose slack the whole-table band bound could not clear and
                                  * that took the per-chunk band test (prep_exact_nodes of them failed it) */
-    /* the boundary-edge light prep: preps that weighed at least one light group by the
-     * boundary edges of its candidate set, those edges' fan terms, and the candidates weighed one by one
-     * (the groups weighed triangle by triangle, the picked group, sliver suspects) in those preps */
-    uint64_t light_evals_weighed;
-    uint64_t prep_fan_edges;
-    uint64_t prep_fan_nodes;
 } mcpt_stats;
 /* With several devices, `seconds` is the wall time of the whole call (shards + reduce), counts are
  * summed over devices and prep_seconds is summed device time. */

@@ -58,13 +58,6 @@ int mcpt_debug_light_prep_exact(mcpt_scene* scene, int32_t n, const double* x1, 
  * alpha's acos argument, B.C.  For checking the GPU's fp64 sqrt / division / acos against the host's. */
 int mcpt_debug_light_literal(mcpt_scene* scene, const double x1[3], const double normal[3], double* out20);
 
-/* diagnostics (host only, no GPU): the boundary-edge light prep's tables (build_fan_tables, DESIGN.md
- * §4.7) -- *ngroups light groups; with nbr != NULL also, per light, the light across each reference-
- * order edge (p0 p1, p1 p2, p2 p0; -1 = a boundary edge) and its group | flip << 30 (nbr: 4 int32), its
- * sliver-suspect factor (eps), and per group (centre xyz, radius, shortest edge, 2 sum L, first light,
- * count) (grp: 8 doubles) and whether it is eligible (gok).  Lets a CPU test check the fan identity. */
-int mcpt_debug_fan_tables(mcpt_scene* scene, int32_t* ngroups, int32_t* nbr, double* grp, int32_t* gok, float* eps);
-
 /* diagnostics (host only, no GPU): the traversal's fp32 triangle pre-test (tri_filter in render.hip)
  * on n (triangle, ray) pairs -- tri: 9 floats per triangle (a, b, c), ro / rd: 3 doubles per ray,
  * tlim: the traversal's current limit per pair (FLT_MAX: none).  verdict: 0 the reference's fp64 test

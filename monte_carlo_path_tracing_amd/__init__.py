@@ -26,7 +26,7 @@ MODES = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE, "shade_area": 
 ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
 HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
 DEFAULT_SEED = 20240430
-MCPT_VERSION = 20200  # include/mcpt.h MCPT_VERSION this mirror is written against
+MCPT_VERSION = 20100  # include/mcpt.h MCPT_VERSION this mirror is written against
 COMM_ID_BYTES = 128  # MCPT_COMM_ID_BYTES
 
 
@@ -79,8 +79,7 @@ class Stats(C.Structure):
                 ("spilled_nodes", C.c_uint64), ("reduce_seconds", C.c_double), ("devices_used", C.c_int32),
                 ("trace_seconds", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("prep_exact_nodes", C.c_uint64), ("cache_build_seconds", C.c_double),
-                ("prep_band_nodes", C.c_uint64), ("light_evals_weighed", C.c_uint64), ("prep_fan_edges", C.c_uint64),
-                ("prep_fan_nodes", C.c_uint64)]
+                ("prep_band_nodes", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -95,7 +94,7 @@ EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_cre
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
 DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter", "mcpt_debug_light_prep_exact", "mcpt_debug_light_literal",
-                 "mcpt_debug_set_collective_lib", "mcpt_debug_fan_tables"]  # include/mcpt_debug.h
+                 "mcpt_debug_set_collective_lib"]  # include/mcpt_debug.h
 
 
 def lib():
@@ -144,8 +143,7 @@ def lib():
                "mcpt_debug_tri_filter": [I, fp, dp, dp, fp, ip, fp],
                "mcpt_debug_light_prep_exact": [P, I, dp, dp, dp, dp, ip, ip],
                "mcpt_debug_light_literal": [P, dp, dp, dp],
-               "mcpt_debug_set_collective_lib": [C.c_char_p],
-               "mcpt_debug_fan_tables": [P, C.POINTER(I), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]}
+               "mcpt_debug_set_collective_lib": [C.c_char_p]}
         for name, argt in dbg.items():
             if hasattr(L, name):
                 getattr(L, name).argtypes = argt
@@ -367,20 +365,6 @@ def debug_light_literal(scene, x1, normal):
     out = np.zeros((scene.nlights, 20))
     _check(lib().mcpt_debug_light_literal(scene.h, _d(x1, (3,)), _d(normal, (3,)), out.reshape(-1)))
     return out
-
-
-def debug_fan_tables(scene):
-    """Diagnostics (host only): the boundary-edge light prep's tables (include/mcpt_debug.h) as a dict:
-    nbr (N_L x 4: lights across edges p0p1, p1p2, p2p0 or -1; group | flip << 30), eps (N_L), groups
-    (G x 8: centre, radius, shortest edge, 2 sum L, first, count) and ok (G)."""
-    g = C.c_int32()
-    _check(lib().mcpt_debug_fan_tables(scene.h, C.byref(g), None, None, None, None))
-    G, NL = g.value, scene.nlights
-    nbr, eps = np.zeros((max(NL, 1), 4), np.int32), np.zeros(max(NL, 1), np.float32)
-    grp, ok = np.zeros((max(G, 1), 8)), np.zeros(max(G, 1), np.int32)
-    _check(lib().mcpt_debug_fan_tables(scene.h, C.byref(g), nbr.ctypes.data, grp.ctypes.data, ok.ctypes.data,
-                                       eps.ctypes.data))
-    return dict(nbr=nbr[:NL], eps=eps[:NL], groups=grp[:G], ok=ok[:G])
 
 
 def debug_tri_filter(tri, ro, rd, tlim=None):

@@ -33,9 +33,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <map>
 #include <memory>
-#include <tuple>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -60,25 +58,7 @@ struct LightPair {
     float2 nl[3];
     float2 d;      // nl . p0 + 1e-8 of both lights
     float2 p[9];
-    float eps[2];  // the lights' sliver-suspect factors (FanGrp, k_prep_cull_lanes<.., kSusp>); 0 for padding
-    float pad[4];
-};
-
-// Boundary-edge ("fan") form of the light prep (k_prep_fan), per light group (one
-// <light mtlname> material: a contiguous run of the light table with one sum L).  The candidates of a
-// group are its triangles passing the cheap stages; their spherical triangles, each oriented positively,
-// form a 2-chain whose interior edges cancel, so the sum of their solid angles equals the sum over the
-// candidate set's BOUNDARY edges (an edge whose neighbour across it is not a candidate) of the signed
-// solid angle of the fan triangle (r, a, b), r = the direction to the group's centre (Van Oosterom-
-// Strackee; exact as long as every vertex lies in the open hemisphere around r, i.e. x1 outside the
-// group's bounding sphere).  A group whose mesh is a consistently oriented surface with nondegenerate
-// triangles is eligible; neighbours come from bit-identical vertex positions.
-struct FanGrp {
-    double c[3];   // bounding-sphere centre
-    double R;      // radius (rounded up)
-    double lmin;   // shortest edge of the group
-    double lsum2;  // 2 sum L (one value for the whole group)
-    int first, count, ok, pad;
+    float pad[6];
 };
 
 struct DScene {
@@ -100,12 +80,6 @@ struct DScene {
     const float4* lt_f;       // NL*4: fp32 records of MCPT_RENDER_PRECISION_FP32 (LightF32: p0, p1, p2 with the
                               // area normal in .w, then 2 RadianceRGB::sum() as fp64 bits)
     const struct LightPair* lt_pair;  // 32*nchunks light pairs for k_prep_cull_lanes (scalar loads)
-    // the boundary-edge form of the prep (FanGrp, k_prep_fan)
-    const FanGrp* fan_grp;    // fan_nslots: the eligible groups, ascending (at most kFanMaxGroups)
-    const int2* fan_nbr;      // 64 nchunks: the lights across edges 0, 1 (x), 2 (y) as 16-bit fields, 0xFFFF = none;
-                              // bit 16 of y = flip (the reference vertex order is the negative one)
-    int fan_nslots;
-    int fan_on;               // some group is eligible and N_L < 8192 (13-bit light indices in k_prep_fan's list)
     // exact-pick band: per 64-light chunk a bounding sphere (centre, radius) of its
     // vertices and (max sum L, max sum L / shortest edge) of its lights; the same over the whole table
     const float4* chunk_sph;  // nchunks
@@ -1863,36 +1837,21 @@ struct CullLane {
 };
 
 // one chunk (64 lights, two halves of 32) of the cull for this lane's node: the candidate word
-// (bit j = light 64 c + j).  kSusp: also the sliver-suspect word *sword (build_fan_tables: bit j set
-// if s <= eps_j D^3 / D'^2 (+ the rounding bound), D / D' the largest / smallest distance from x1 to
-// the chunk's bounding sphere -- every light where x1 lies inside it; k_prep_fan ANDs it with the
-// candidate word)
-template <bool kCountC1, bool kSusp = false>
+// (bit j = light 64 c + j)
+template <bool kCountC1>
 __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const LightPair* __restrict__ T, int c,
-                                      float err, uint64_t actm, bool act, d3 x1, d3 nn, unsigned long long& c1,
-                                      uint64_t* sword = nullptr) {
-    unsigned word[2], sw2[2];
-    v2f thrT{0.f, 0.f};
-    if (kSusp) {
-        const float4 sp = S.chunk_sph[c];
-        const float dx = (float)x1.x - sp.x, dy = (float)x1.y - sp.y, dz = (float)x1.z - sp.z;
-        const float dist = __builtin_sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
-        const float Dp = dist - sp.w * 1.001f - 1e-6f, Dm = dist + sp.w * 1.001f + 1e-6f;
-        const float T3 = Dp > 0.f ? Dm * Dm * Dm / (Dp * Dp) * 1.001f : __builtin_inff();
-        thrT = v2f{T3, T3};
-    }
+                                      float err, uint64_t actm, bool act, d3 x1, d3 nn, unsigned long long& c1) {
+    unsigned word[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const LightPair* __restrict__ Th = T + 32 * c + 16 * h;
-        unsigned w = 0, c1w = 0, sw = 0;
+        unsigned w = 0, c1w = 0;
         float amin = __builtin_inff();  // min over the 32 lights of min(|s|, |min(s, max t)|)
         // pairs holding real lights (the table's last chunk is partial: N_L = 3012 leaves 4 of 64)
         const int qend = kCountC1 ? 16 : min(16, max(0, (S.NL - (64 * c + 32 * h) + 1) >> 1));
         auto pair = [&](int q) {
             v2f s1, t[3];
             cl.eval(Th[q], &s1, t);
-            v2f thr2{0.f, 0.f};
-            if (kSusp) thr2 = __builtin_elementwise_fma(v2f{Th[q].eps[0], Th[q].eps[1]}, thrT, v2f{err, err});
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 const float sv = s1[e];
@@ -1901,8 +1860,6 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
                 amin = min3_abs_raw(amin, sv, mn);
                 if (kCountC1) c1w += __popcll(__ballot(sv < -err) & actm);  // statistic only
                 w = shift_in(w, __ballot(mn > err));
-                // s + 1e-8 = nl . (x1 - p0): flagged at or below eps D^3 / D'^2 + err (the rounding bound)
-                if (kSusp) sw = shift_in(sw, __ballot(!(sv > thr2[e])));
             }
         };
         if (qend == 16) {
@@ -1911,7 +1868,6 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
         } else {  // the padding lights' bits stay clear; light j's bit back at 31 - j
             for (int q = 0; q < qend; q++) pair(q);
             w = qend == 0 ? 0u : w << (32 - 2 * qend);
-            if (kSusp) sw = qend == 0 ? 0u : sw << (32 - 2 * qend);
         }
         if (__ballot(amin <= err) & actm) {  // rare: the reference's exact fp64 stages for the ambiguous (node, light) pairs
             for (int q = 0; q < 16; q++) {
@@ -1929,7 +1885,6 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
                         st = light_cheap_stage(mk3(pc(0), pc(1), pc(2)), mk3(pc(3), pc(4), pc(5)),
                                                mk3(pc(6), pc(7), pc(8)), mk3(ln.x, ln.y, ln.z), x1, nn);
                         if (st == 0) w |= 1u << (31 - (2 * q + e));
-                        if (kSusp) sw |= 1u << (31 - (2 * q + e));  // |s| within err of the threshold: suspect
                     }
                     if (kCountC1) c1w += __popcll(__ballot(st == 1));  // uniform: every lane of the wave
                 }
@@ -1937,17 +1892,14 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
         }
         c1 += c1w;
         word[h] = __builtin_bitreverse32(w);
-        sw2[h] = __builtin_bitreverse32(sw);
     }
-    if (kSusp) *sword = ((uint64_t)sw2[1] << 32) | sw2[0];
     return ((uint64_t)word[1] << 32) | word[0];
 }
 
-template <bool kCountC1, bool kSusp = false>
+template <bool kCountC1>
 __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
                                                          const double* __restrict__ qn, int qs, uint64_t* __restrict__ masks,
-                                                         int nchunks, unsigned long long* stats,
-                                                         uint64_t* __restrict__ smasks = nullptr) {
+                                                         int nchunks, unsigned long long* stats) {
     const int node = blockIdx.x * blockDim.x + threadIdx.x;
     const bool act = node < n;
     const int nd = act ? node : n - 1;
@@ -1974,31 +1926,22 @@ __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S,
     const int per = (bursts + gridDim.y - 1) / gridDim.y;
     const int pb = blockIdx.y * per, pe = min(bursts, pb + per);
     uint4* __restrict__ row = reinterpret_cast<uint4*>(masks + (size_t)nd * mask_stride(nchunks));
-    uint4* __restrict__ srow = kSusp ? reinterpret_cast<uint4*>(smasks + (size_t)nd * mask_stride(nchunks)) : nullptr;
     for (int p = pb; p < pe; p++) {
-        uint64_t w[kCullBurst], sw[kCullBurst];
+        uint64_t w[kCullBurst];
 #pragma unroll
         for (int i = 0; i < kCullBurst; i++) {
             const int c = kCullBurst * p + i;
-            sw[i] = 0;
-            w[i] = c < nchunks ? cull_chunk<kCountC1, kSusp>(S, cl, T, c, err, actm, act, x1, nn, c1, &sw[i]) : 0ull;
+            w[i] = c < nchunks ? cull_chunk<kCountC1>(S, cl, T, c, err, actm, act, x1, nn, c1) : 0ull;
         }
         if (act)
 #pragma unroll
-            for (int i = 0; i < kCullBurst; i += 2) {
+            for (int i = 0; i < kCullBurst; i += 2)
                 row[(kCullBurst * p + i) / 2] = make_uint4((unsigned)w[i], (unsigned)(w[i] >> 32), (unsigned)w[i + 1],
                                                            (unsigned)(w[i + 1] >> 32));
-                if (kSusp)
-                    srow[(kCullBurst * p + i) / 2] = make_uint4((unsigned)sw[i], (unsigned)(sw[i] >> 32), (unsigned)sw[i + 1],
-                                                                (unsigned)(sw[i + 1] >> 32));
-            }
     }
     // zero words past the last burst up to the row's last whole line (k_prep_pk2 reads whole lines)
     if (act && pe == bursts)
-        for (int p = bursts * kCullBurst / 2; p < mask_stride(nchunks) / 2; p++) {
-            row[p] = make_uint4(0, 0, 0, 0);
-            if (kSusp) srow[p] = make_uint4(0, 0, 0, 0);
-        }
+        for (int p = bursts * kCullBurst / 2; p < mask_stride(nchunks) / 2; p++) row[p] = make_uint4(0, 0, 0, 0);
     // padding lights (index >= N_L, d = 1e30) were counted as light-side culled by every active lane
     if (kCountC1 && pe == bursts) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
@@ -2226,497 +2169,6 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             if (cand_acc) atomicAdd(stats + 5, cand_acc);
             if (c1_acc) atomicAdd(stats + 6, c1_acc);
             if (full_acc) atomicAdd(stats + 7, full_acc);
-            if (cand_acc) atomicAdd(stats + 16, cand_acc);  // every candidate weighed (light_evals_weighed)
-        }
-    }
-}
-
-// ---- the boundary-edge ("fan") full prep ------------------------------------------
-// One wave per node, like k_prep_pk2<.., mask-in> (candidate words from k_prep_cull_lanes<.., kSusp>),
-// but a light group (FanGrp) whose mesh is eligible and lies wholly outside the node's tangent-plane
-// neighbourhood test below is weighed as ONE segment: the sum over its candidates' boundary edges of the
-// fan term half(r, A, B) * 2 sum L (fan_half) -- the same sum of sA * sum L as its candidates' weights,
-// up to rounding -- so the candidates' own weights are evaluated only in the group the pick lands in.
-// Other groups' candidates are weighed one by one as in k_prep_pk2, in index order.
-//   phase 1  the list: individual candidates (light index) and edge items (light | (k + 1) << 13 |
-//            flip << 15; k = the edge (p_k, p_k+1) of the reference order, flip = that order is not
-//            the positive one), a fan group's items in whole batches of their own (seg[b] = group);
-//   phase 2  sliver suspects of fan groups (k_prep_cull_lanes' suspect words): their weights are
-//            evaluated only for the band (the sliver term) -- a suspect the fp64 form culls sends the
-//            node to the literal fallback (its area is inside the fan sum, the reference may drop it);
-//   phase 3  batch totals (a fan group's batches summed in order into one segment), the inverse-CDF
-//            search over segments (prep_select's), and inside a picked fan group its candidates'
-//            weights in index order (a batch search and the in-batch scan), offset by the prefix of
-//            the segments before it.
-// The band gains the fan terms' rounding (kFanErr u 2 sum L per edge); everything else is k_prep_pk2's
-// (the chunk term over all candidates still bounds the reference's own noise against the exact sums).
-constexpr int kFanMaxGroups = 8;   // groups per node taken through the edge form (more: one by one)
-constexpr int kFanMinCand = 48;    // a group with fewer candidates is weighed one by one
-constexpr int kFanSusp = 128;      // LDS room for a node's suspects (more: the literal fallback)
-constexpr double kFanErr = 32.0;   // |rounding of one fan term| <= kFanErr u 2 sum L (unit vectors, dots, atan)
-constexpr int kFanSlotBytes = kFanMaxGroups * (int)sizeof(FanGrp);  // the slot table at the start of the block's LDS
-constexpr int kFanNbrBatch = 8;    // neighbour-table words in flight at once
-__device__ inline double rdlane(double v, int l) {  // lane l's value (l wave-uniform)
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    return __longlong_as_double((long long)(((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l) << 32) |
-                                            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l)));
-}
-__host__ __device__ inline int fan_item_cap(int nchunks) { return 64 * nchunks + 128 * kFanMaxGroups + 64; }
-__host__ __device__ inline int fan_wave_bytes(int nchunks) {
-    const int icap = fan_item_cap(nchunks), nbc = icap / 64;
-    return (nchunks * 8 + nbc * 8 + nbc * 4 + icap * 2 + kFanSusp * 2 + 15) / 16 * 16;
-}
-// half the signed solid angle of the spherical triangle (r, A, B) of unit vectors (Van Oosterom-Strackee)
-__device__ inline double fan_half(d3 r, d3 A, d3 B) {
-    const double num = fdot(r, fcross(A, B));
-    const double den = 1.0 + fdot(r, A) + fdot(A, B) + fdot(B, r);
-    const double h = atan2_pos_prep(fabs(num), den);
-    return num < 0 ? -h : h;
-}
-__device__ inline uint64_t uniform_u64(uint64_t x) {  // a wave-uniform value into SGPRs
-    return ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
-           (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)x);
-}
-__device__ inline uint64_t range_bits(int c, int f0, int f1) {  // bits of word c for lights [f0, f1)
-    const int lo = max(f0 - 64 * c, 0), hi = min(f1 - 64 * c, 64);
-    if (hi <= lo) return 0ull;
-    const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
-    return up & ~((1ull << lo) - 1);
-}
-template <int kMinWavesPerSimd>
-__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_fan(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
-                                                                    int qs, const int* __restrict__ qpixel,
-                                                                    const int* __restrict__ qsample, const uint64_t* __restrict__ qnode,
-                                                                    const double* __restrict__ u_override, double* __restrict__ wsum_out,
-                                                                    int* __restrict__ pick_out, int* __restrict__ count_out,
-                                                                    unsigned long long* stats, int nchunks, int wave_bytes,
-                                                                    unsigned* __restrict__ work, PrepCache C,
-                                                                    const uint64_t* __restrict__ masks,
-                                                                    const uint64_t* __restrict__ smasks) {
-    extern __shared__ double prep_lds[];
-    const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
-    const int icap = fan_item_cap(nchunks), nbc = icap / 64;
-    // the slots (eligible groups, ascending) in LDS, once per block
-    FanGrp* slots = reinterpret_cast<FanGrp*>(prep_lds);
-    const int nslots = min(S.fan_nslots, kFanMaxGroups);
-    for (int i = threadIdx.x; i < nslots * (int)(sizeof(FanGrp) / 8); i += blockDim.x)
-        reinterpret_cast<double*>(slots)[i] = reinterpret_cast<const double*>(S.fan_grp)[i];
-    __syncthreads();
-    char* base_lds = reinterpret_cast<char*>(prep_lds) + kFanSlotBytes + (size_t)wib * wave_bytes;
-    uint64_t* wd = reinterpret_cast<uint64_t*>(base_lds);
-    double* bt = reinterpret_cast<double*>(base_lds + nchunks * 8);
-    int* seg = reinterpret_cast<int*>(base_lds + nchunks * 8 + nbc * 8);
-    unsigned short* items = reinterpret_cast<unsigned short*>(base_lds + nchunks * 8 + nbc * 12);
-    unsigned short* susp = items + icap;
-    const int ngroups4 = (nchunks + 3) / 4;
-    const __amdgpu_buffer_rsrc_t rw = light_record_rsrc(S, ngroups4);
-    constexpr unsigned short kPad = 0xFFFF;
-    unsigned long long cand_acc = 0, full_acc = 0, eval_acc = 0, edge_acc = 0, fan_acc = 0, surv_acc = 0;
-    int grab = 0, left = 0;
-    while (true) {
-        if (left == 0) {
-            unsigned b = 0;
-            if (lane == 0) b = atomicAdd(work, (unsigned)kPrepGrab);
-            grab = __shfl((int)b, 0);
-            left = kPrepGrab;
-        }
-        const int node = __builtin_amdgcn_readfirstlane(grab++);
-        left--;
-        if (node >= n) break;
-        const d3 x1 = ld3(qp, qs, node);
-        const uint64_t* __restrict__ mrow = masks + (size_t)node * mask_stride(nchunks);
-        const uint64_t* __restrict__ srow = smasks + (size_t)node * mask_stride(nchunks);
-        // the node's words in registers, lane c holding words c and c + 64 (nchunks <= 128 for a fan
-        // scene), and in LDS for the neighbour tests; a word at a wave-uniform index is two readlanes
-        const uint64_t w0 = lane < nchunks ? mrow[lane] : 0ull, w1 = lane + 64 < nchunks ? mrow[lane + 64] : 0ull;
-        const uint64_t sr0 = lane < nchunks ? srow[lane] : 0ull, sr1 = lane + 64 < nchunks ? srow[lane + 64] : 0ull;
-        if (lane < nchunks) wd[lane] = w0;
-        if (lane + 64 < nchunks) wd[lane + 64] = w1;
-        for (int b = lane; b < nbc; b += 64) seg[b] = -1;
-        auto word = [&](int c) -> uint64_t {  // c wave-uniform
-            const uint64_t w = c < 64 ? w0 : w1;
-            const int l = c & 63;
-            return ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(w >> 32), l) << 32) |
-                   (unsigned)__builtin_amdgcn_readlane((int)(unsigned)w, l);
-        };
-        const unsigned* wd32 = reinterpret_cast<const unsigned*>(wd);
-        // lane s: slot s's direction r from x1 and whether x1 meets its conditions -- outside the bounding
-        // sphere (every vertex in the open hemisphere around r), and no candidate whose projected edges are
-        // all below ~1e-8 rad (build_fan_tables)
-        d3 rcl = mk3(0.0, 0.0, 1.0);
-        bool okl = false;
-        if (lane < nslots) {
-            const FanGrp& fg = slots[lane];
-            const d3 dv = mk3(fg.c[0] - x1.x, fg.c[1] - x1.y, fg.c[2] - x1.z);
-            const double dist = sqrt(dv.x * dv.x + dv.y * dv.y + dv.z * dv.z);
-            okl = dist > fg.R && fg.lmin > 1e-4 * (dist + fg.R) && nchunks <= 128;
-            if (okl) rcl = funit(dv);
-        }
-        const uint64_t slot_ok = __ballot(okl);
-        wave_lds_sync();
-        // ---- phase 1: the list ----
-        int nitems = 0, ncand = 0;
-        const int total = __builtin_amdgcn_readfirstlane(wave_sum_int(__popcll(w0) + __popcll(w1)));
-        unsigned fanmask = 0;
-        uint64_t fw0 = 0, fw1 = 0;  // the fan groups' lights (lane-parallel words, as w0 / w1)
-        double facc = 0;            // sum over the edge items of 2 sum L (the fan band term; wave-uniform)
-        auto pad64 = [&]() {
-            const int up = (nitems + 63) & ~63;
-            if (nitems + lane < up) items[nitems + lane] = kPad;
-            nitems = up;
-        };
-        const unsigned lds_items = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)items);
-        auto append_range = [&](int f0, int f1) {  // candidates of [f0, f1) one by one, in index order
-            int k = 0;
-            for (int c = f0 >> 6; c <= (f1 - 1) >> 6; c++) {
-                const uint64_t m = uniform_u64(word(c) & range_bits(c, f0, f1));
-                if (m == 0) continue;
-                append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_items + 2u * (unsigned)nitems, (unsigned)lane + 64u * (unsigned)c);
-                nitems += __popcll(m);
-                k += __popcll(m);
-            }
-            return k;
-        };
-        int prev = 0;
-        for (int g = 0; g <= nslots; g++) {
-            // the lights between the previous slot and this one (or the table's end): one by one
-            const int f0 = g < nslots ? slots[g].first : S.NL;
-            if (f0 > prev) ncand += append_range(prev, f0);
-            if (g == nslots) break;
-            const int f1 = f0 + slots[g].count;
-            prev = f1;
-            const uint64_t r0 = range_bits(lane, f0, f1), r1 = range_bits(lane + 64, f0, f1);
-            const int ng = __builtin_amdgcn_readfirstlane(wave_sum_int(__popcll(w0 & r0) + __popcll(w1 & r1)));
-            if (ng == 0) continue;
-            ncand += ng;
-            // room: the items left for the candidates after this group (one each) and two paddings;
-            // a ragged candidate set that would not fit is weighed one by one instead
-            const bool fan = ((slot_ok >> g) & 1) && ng >= kFanMinCand && nitems + 64 + 3 * ng <= icap - (total - ncand) - 128;
-            if (!fan) {
-                append_range(f0, f1);
-                continue;
-            }
-            pad64();
-            const int b0 = nitems >> 6;
-            const int c0 = f0 >> 6, c1 = (f1 - 1) >> 6;
-            int nedge = 0;
-            for (int cb = c0; cb <= c1; cb += kFanNbrBatch) {
-                // the neighbour entries of kFanNbrBatch words in flight at once (the table is padded to
-                // whole words; past the group's last word the loads repeat it)
-                int2 q8[kFanNbrBatch];
-#pragma unroll
-                for (int q = 0; q < kFanNbrBatch; q++) q8[q] = S.fan_nbr[64 * min(cb + q, c1) + lane];
-#pragma unroll
-                for (int q = 0; q < kFanNbrBatch; q++) {
-                    const int c = cb + q;
-                    if (c > c1) break;
-                    const uint64_t m = uniform_u64(word(c) & range_bits(c, f0, f1));
-                    if (m == 0) continue;
-                    const unsigned li = 64u * (unsigned)c + (unsigned)lane;
-                    const bool mine = (m >> lane) & 1;
-                    const unsigned tag = li | ((((unsigned)q8[q].y >> 16) & 1u) << 15);
-                    // candidate bits of the three neighbours (0xFFFF: no twin, a boundary edge)
-                    const unsigned o0 = (unsigned)q8[q].x & 0xFFFFu, o1 = (unsigned)q8[q].x >> 16, o2 = (unsigned)q8[q].y & 0xFFFFu;
-                    const unsigned v0 = wd32[(o0 & 0x1FFFu) >> 5], v1 = wd32[(o1 & 0x1FFFu) >> 5], v2 = wd32[(o2 & 0x1FFFu) >> 5];
-                    const bool e0 = mine && (o0 == 0xFFFFu || !((v0 >> (o0 & 31)) & 1u));
-                    const bool e1 = mine && (o1 == 0xFFFFu || !((v1 >> (o1 & 31)) & 1u));
-                    const bool e2 = mine && (o2 == 0xFFFFu || !((v2 >> (o2 & 31)) & 1u));
-                    const uint64_t m0 = __ballot(e0), m1 = __ballot(e1), m2 = __ballot(e2);
-                    if (e0) items[nitems + lane_rank(m0)] = (unsigned short)(tag | (1u << 13));
-                    nitems += __popcll(m0);
-                    if (e1) items[nitems + lane_rank(m1)] = (unsigned short)(tag | (2u << 13));
-                    nitems += __popcll(m1);
-                    if (e2) items[nitems + lane_rank(m2)] = (unsigned short)(tag | (3u << 13));
-                    nitems += __popcll(m2);
-                    nedge += __popcll(m0) + __popcll(m1) + __popcll(m2);
-                }
-            }
-            fanmask |= 1u << g;
-            fw0 |= r0;
-            fw1 |= r1;
-            facc += (double)nedge * slots[g].lsum2;
-            pad64();
-            for (int b = b0 + lane; b < (nitems >> 6); b += 64) seg[b] = g;
-        }
-        const int nitem_real = nitems;
-        pad64();
-        const int nb = nitems >> 6;
-        // ---- phase 2: sliver suspects of the fan groups ----
-        int nsusp = 0;
-        bool force_exact = false;
-        if (fanmask) {
-            const uint64_t s0 = sr0 & w0 & fw0, s1 = sr1 & w1 & fw1;
-            const int ns = __builtin_amdgcn_readfirstlane(wave_sum_int(__popcll(s0) + __popcll(s1)));
-            if (ns > kFanSusp) {
-                force_exact = true;
-            } else if (ns > 0) {
-                const unsigned lds_susp = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)susp);
-                for (int h = 0; h < 2; h++) {
-                    uint64_t nz = __ballot((h ? s1 : s0) != 0);
-                    while (nz) {
-                        const int l = __ffsll((unsigned long long)nz) - 1;
-                        nz &= nz - 1;
-                        const uint64_t sw = h ? s1 : s0;
-                        const uint64_t m = uniform_u64(((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(sw >> 32), l) << 32) |
-                                                       (unsigned)__builtin_amdgcn_readlane((int)(unsigned)sw, l));
-                        append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_susp + 2u * (unsigned)nsusp,
-                                      (unsigned)lane + 64u * (unsigned)(l + 64 * h));
-                        nsusp += __popcll(m);
-                    }
-                }
-            }
-        }
-        wave_lds_sync();
-        // ---- phase 3a: batch totals ----
-        int nbad = 0, ndeg = 0;
-        double sacc = 0;
-        unsigned long long ev = 0, ed = 0;
-        for (int b0 = 0; b0 < nb; b0 += 4) {
-            double w4[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                w4[i] = 0.0;
-                if (b0 + i >= nb) continue;  // wave-uniform
-                const int sg = __builtin_amdgcn_readfirstlane(seg[b0 + i]);
-                const unsigned it = items[64 * (b0 + i) + lane];
-                if (sg < 0) {  // candidates weighed one by one (k_prep_pk2's arithmetic)
-                    if (it != kPad) {
-                        double l2;
-                        const WeightBx r = prep_weight_buf_bx(rw, (int)it, x1, &l2);
-                        w4[i] = r.w;
-                        ev++;
-                        if (!r.ok | r.sliver) {
-                            if (!r.ok) {
-                                nbad++;
-                            } else {
-                                const double t = sliver_term(r.num, r.den) * l2;
-                                sacc += t;
-                                if (2.0 * r.w < 64.0 * kU53 * t) ndeg++;
-                            }
-                        }
-                    }
-                } else if (it != kPad) {  // a fan group's boundary edge
-                    const int li = (int)(it & 0x1fffu), k = (int)((it >> 13) & 3u) - 1;
-                    const d3 rc = mk3(rdlane(rcl.x, sg), rdlane(rcl.y, sg), rdlane(rcl.z, sg));
-                    const v4u a = struct_load_b128(rw, li, 0, 0, 0);
-                    const v4u b = struct_load_b128(rw, li, 16, 0, 0);
-                    const v4u c = struct_load_b128(rw, li, 32, 0, 0);
-                    const v4u d = struct_load_b128(rw, li, 48, 0, 0);
-                    const v4u e = struct_load_b128(rw, li, 64, 0, 0);
-                    const d3 p0 = mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y));
-                    const d3 p1 = mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w));
-                    const d3 p2 = mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y));
-                    const d3 pa = k == 0 ? p0 : k == 1 ? p1 : p2, pb = k == 0 ? p1 : k == 1 ? p2 : p0;
-                    const double h = fan_half(rc, funit(sub(pa, x1)), funit(sub(pb, x1)));
-                    w4[i] = (it >> 15 ? -h : h) * slots[sg].lsum2;
-                    ed++;
-                }
-            }
-            const double t = batch_totals4(w4[0], w4[1], w4[2], w4[3]);
-            if ((lane & 15) == 15 && b0 + (lane >> 4) < nb) bt[b0 + (lane >> 4)] = t;
-        }
-        // ---- phase 2b: the suspects' band terms ----
-        int nbad_s = 0;
-        for (int s0 = 0; s0 < nsusp; s0 += 64) {
-            const bool act = s0 + lane < nsusp;
-            if (act) {
-                double l2;
-                const WeightBx r = prep_weight_buf_bx(rw, (int)susp[s0 + lane], x1, &l2);
-                ev++;
-                if (!r.ok) {
-                    nbad_s++;
-                } else if (r.sliver) {
-                    const double t = sliver_term(r.num, r.den) * l2;
-                    sacc += t;
-                    if (2.0 * r.w < 64.0 * kU53 * t) ndeg++;
-                }
-            }
-        }
-        if (__ballot(nbad_s != 0)) force_exact = true;  // a suspect the fp64 form culls: the literal fallback
-        wave_lds_sync();
-        // ---- phase 3b: segments and the search ----
-        double v = 0.0;
-        if (lane < nb && nb <= 64) {
-            const int sg = seg[lane];
-            if (sg < 0) {
-                v = bt[lane];
-            } else if (lane == 0 || seg[lane - 1] != sg) {  // the group's first batch carries its sum
-                for (int b = lane; b < nb && seg[b] == sg; b++) v += bt[b];
-            }
-        }
-        double wsum = 0, target = 0, base = 0;
-        int kb = -1;
-        if (nb <= 64) {
-            const double cum = wave_incl_scan(v, lane);
-            wsum = __shfl(cum, 63);
-            if (!(fabs(wsum) < MCPT_EPS)) {
-                const double u = u_override ? u_override[node]
-                                            : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-                target = u * wsum;
-                const uint64_t hitm = __ballot(cum >= target && v > 0);
-                const uint64_t posm = __ballot(v > 0);
-                kb = hitm ? __ffsll((unsigned long long)hitm) - 1 : (posm ? 63 - __clzll((long long)posm) : -1);
-                const double exc = __shfl_up(cum, 1);
-                base = kb <= 0 ? 0.0 : __shfl(exc, kb);
-            }
-        } else {  // more than 64 batches: the segments sequentially (wave-uniform)
-            int lastpos = -1;
-            double lastbase = 0, cum = 0;
-            for (int b = 0; b < nb;) {  // wsum
-                const int sg = seg[b];
-                if (sg < 0) {
-                    wsum += bt[b];
-                    b++;
-                } else {
-                    double sv = 0;
-                    while (b < nb && seg[b] == sg) sv += bt[b++];
-                    wsum += sv;
-                }
-            }
-            if (!(fabs(wsum) < MCPT_EPS)) {
-                const double u = u_override ? u_override[node]
-                                            : counter_u(counter_key(seed, (uint64_t)qpixel[node], (uint64_t)qsample[node], qnode[node]), 1);
-                target = u * wsum;
-                for (int b = 0; b < nb && kb < 0;) {
-                    const int sg = seg[b];
-                    const int b1 = b;
-                    double sv = 0;
-                    if (sg < 0) sv = bt[b++];
-                    else
-                        while (b < nb && seg[b] == sg) sv += bt[b++];
-                    const double nxt = cum + sv;
-                    if (sv > 0) lastpos = b1, lastbase = cum;
-                    if (nxt >= target && sv > 0) kb = b1, base = cum;
-                    cum = nxt;
-                }
-                if (kb < 0) kb = lastpos, base = lastbase;
-            }
-        }
-        int pick = -1;
-        double margin = INFINITY;
-        int sgk = kb >= 0 ? __builtin_amdgcn_readfirstlane(seg[kb]) : -1;
-        int ncg = 0;
-        if (kb >= 0 && sgk < 0) {  // an individual batch: prep_select's in-batch scan
-            const int k = 64 * kb + lane;
-            const unsigned it = k < nitem_real ? items[k] : kPad;
-            bool ok = false;
-            double w = 0;
-            if (it != kPad) w = prep_weight_buf(rw, (int)it, x1, &ok);
-            w = ok ? w : 0.0;
-            const double sc = wave_incl_scan(w, lane);
-            const uint64_t candm = __ballot(ok && (base + sc >= target));
-            const uint64_t okm = __ballot(ok);
-            int pl = -1;
-            if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-            else if (okm) pl = 63 - __clzll((long long)okm);
-            if (pl >= 0) {
-                pick = __shfl((int)it, pl);
-                margin = pick_margin(base, sc, pl, target);
-            }
-        } else if (kb >= 0) {  // a fan group: its candidates' weights in index order
-            const int f0 = slots[sgk].first, f1 = f0 + slots[sgk].count;
-            wave_lds_sync();
-            for (int c = f0 >> 6; c <= (f1 - 1) >> 6; c++) {
-                const uint64_t m = uniform_u64(word(c) & range_bits(c, f0, f1));
-                if (m == 0) continue;
-                append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_items + 2u * (unsigned)ncg, (unsigned)lane + 64u * (unsigned)c);
-                ncg += __popcll(m);
-            }
-            const int nb2 = (ncg + 63) >> 6;
-            if (ncg + lane < 64 * nb2) items[ncg + lane] = kPad;
-            wave_lds_sync();
-            for (int b0 = 0; b0 < nb2; b0 += 4) {
-                double w4[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    w4[i] = 0.0;
-                    if (b0 + i >= nb2) continue;
-                    const unsigned it = items[64 * (b0 + i) + lane];
-                    if (it != kPad) {
-                        bool ok;
-                        const double w = prep_weight_buf(rw, (int)it, x1, &ok);
-                        w4[i] = ok ? w : 0.0;
-                        ev++;
-                    }
-                }
-                const double t = batch_totals4(w4[0], w4[1], w4[2], w4[3]);
-                if ((lane & 15) == 15 && b0 + (lane >> 4) < nb2) bt[b0 + (lane >> 4)] = t;
-            }
-            wave_lds_sync();
-            int kb2 = -1;
-            double base2 = base;
-            if (nb2 <= 64) {
-                const double v2 = lane < nb2 ? bt[lane] : 0.0;
-                const double cum2 = wave_incl_scan(v2, lane);
-                const uint64_t hitm = __ballot(base + cum2 >= target && v2 > 0);
-                const uint64_t posm = __ballot(v2 > 0);
-                kb2 = hitm ? __ffsll((unsigned long long)hitm) - 1 : (posm ? 63 - __clzll((long long)posm) : -1);
-                const double exc2 = __shfl_up(cum2, 1);
-                const double e2 = __shfl(exc2, max(kb2, 0));
-                base2 = kb2 <= 0 ? base : base + e2;
-            } else {
-                double cum2 = 0, lastb = base;
-                int lastpos = -1;
-                for (int b = 0; b < nb2; b++) {
-                    const double nxt = cum2 + bt[b];
-                    if (bt[b] > 0) lastpos = b, lastb = base + cum2;
-                    if (kb2 < 0 && base + nxt >= target && bt[b] > 0) kb2 = b, base2 = base + cum2;
-                    cum2 = nxt;
-                }
-                if (kb2 < 0) kb2 = lastpos, base2 = lastb;
-            }
-            if (kb2 >= 0) {
-                const unsigned it = items[64 * kb2 + lane];
-                bool ok = false;
-                double w = 0;
-                if (it != kPad) w = prep_weight_buf(rw, (int)it, x1, &ok);
-                w = ok ? w : 0.0;
-                const double sc = wave_incl_scan(w, lane);
-                const uint64_t candm = __ballot(ok && (base2 + sc >= target));
-                const uint64_t okm = __ballot(ok);
-                int pl = -1;
-                if (candm) pl = __ffsll((unsigned long long)candm) - 1;
-                else if (okm) pl = 63 - __clzll((long long)okm);
-                if (pl >= 0) {
-                    pick = __shfl((int)it, pl);
-                    margin = pick_margin(base2, sc, pl, target);
-                }
-            }
-        }
-        // survivors: the one-by-one candidates' culls; a fan group's other candidates survive the
-        // reference's full stage (build_fan_tables), its suspects were checked in phase 2b
-        const int survivors = ncand - wave_sum_int(nbad);
-        if (lane == 0) {
-            wsum_out[node] = wsum;
-            pick_out[node] = pick;
-            if (count_out) count_out[node] = survivors;
-        }
-        if (C.slack) {
-            const double band_sl = __ballot(sacc > 0.0) ? band_sliver(__shfl(wave_incl_scan(sacc, lane), 63)) : 0.0;
-            const double fan_band = kFanErr * kU53 * facc;
-            double sl = pick_slack(margin, wsum) - (band_sl + fan_band + band_round(ncand + nitems, wsum));
-            if (force_exact) sl = -INFINITY;
-            if (C.exact_counts && (survivors < ncand || __ballot(ndeg != 0))) sl = -INFINITY;
-            if (lane == 0) band_candidate(S, C.slack, C.maybe, C.exact_off + node, sl, x1, ncand);
-        }
-        cand_acc += ncand;
-        full_acc++;
-        surv_acc += survivors;
-        fan_acc += fanmask ? 1 : 0;
-        eval_acc += ev;
-        edge_acc += ed;
-        wave_lds_sync();
-    }
-    if (stats) {
-        const unsigned long long e1 = wave_sum_u64(eval_acc), e2 = wave_sum_u64(edge_acc);
-        if (lane == 0) {
-            if (surv_acc) atomicAdd(stats + 1, surv_acc);
-            if (cand_acc) atomicAdd(stats + 5, cand_acc);
-            if (full_acc) atomicAdd(stats + 7, full_acc);
-            if (e1) atomicAdd(stats + 16, e1);
-            if (e2) atomicAdd(stats + 17, e2);
-            if (fan_acc) atomicAdd(stats + 18, fan_acc);
         }
     }
 }
@@ -4274,7 +3726,6 @@ struct DeviceState {
     DevBuf exact, exact_scr, slack;  // exact pick: list, k_prep_exact's scratch, per-node slack
     DevBuf lit_slot, lit_pool;        // exact pick: roots' literal sums per pixel (RootLit)
     DevBuf sc_cum, sc_wsum, sc_last;  // small-table root-point cache (SmallCache)
-    DevBuf smasks;                    // sliver-suspect words of the boundary-edge prep (k_prep_fan)
     int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
@@ -4392,123 +3843,6 @@ int prep_chunks(int NL);
 // the device's scene state, created (scene, light tables and BVHs uploaded) on first use.  Thread-safe
 // for distinct devices: render_multi's workers create theirs concurrently (the lookup and the insertion
 // hold devs_mu, the uploads do not)
-// the fan tables of the light groups (FanGrp), the neighbour table and every light's sliver-suspect
-// factor eps_l: a candidate can be a band sliver (4 - den > tau num, device_math.h) only if
-// s = nl.(x1 - p0) < eps_l D^3 / D'^2 with eps_l = (sum of squared edges) / (4 tau area) and D / D' the
-// largest / smallest distance from x1 to the light (num = 2 area s / (|a||b||c|) >= 2 area s / D^3,
-// 4 - den <= sum l^2 / (2 D'^2)); k_prep_cull_lanes<.., kSusp> flags those candidates, with D and D'
-// from the chunk's bounding sphere.  Every reference full-stage cull of a candidate (an edge or vertex
-// angle below 1e-8 rad, sA <= 0) implies a sliver there, except an edge below 1e-8 rad on a triangle
-// whose projected edges are ALL tiny -- excluded per node by lmin / (|x1 - c| + R) > 1e-4.
-constexpr int kFanMaxLights = 8191;
-void build_fan_tables(const HostScene& s, const std::vector<float4>& lv, const std::vector<double4>& ln,
-                      std::vector<FanGrp>& grp, std::vector<int4>& nbr, std::vector<float>& eps) {
-    const int NL = s.NL, G = (int)s.group_start.size();
-    grp.assign(std::max(G, 1), FanGrp{});
-    nbr.assign(std::max(NL, 1), make_int4(-1, -1, -1, -1));
-    eps.assign(std::max(NL, 1), 0.0f);
-    auto P = [&](int l, int k) { return lv[3 * l + k]; };
-    auto bits = [](float4 v) {
-        uint32_t x, y, z;
-        std::memcpy(&x, &v.x, 4), std::memcpy(&y, &v.y, 4), std::memcpy(&z, &v.z, 4);
-        return std::make_tuple(x, y, z);
-    };
-    for (int l = 0; l < NL; l++) {
-        double e2 = 0, cr[3];
-        double a[3], b[3];
-        for (int k = 0; k < 3; k++) {
-            const float4 p = P(l, k), q = P(l, (k + 1) % 3);
-            const double dx = (double)q.x - p.x, dy = (double)q.y - p.y, dz = (double)q.z - p.z;
-            e2 += dx * dx + dy * dy + dz * dz;
-        }
-        const float4 p0 = P(l, 0), p1 = P(l, 1), p2 = P(l, 2);
-        a[0] = (double)p1.x - p0.x, a[1] = (double)p1.y - p0.y, a[2] = (double)p1.z - p0.z;
-        b[0] = (double)p2.x - p0.x, b[1] = (double)p2.y - p0.y, b[2] = (double)p2.z - p0.z;
-        cr[0] = a[1] * b[2] - a[2] * b[1], cr[1] = a[2] * b[0] - a[0] * b[2], cr[2] = a[0] * b[1] - a[1] * b[0];
-        const double area = 0.5 * std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
-        eps[l] = area > 0 ? (float)std::min(e2 / (4.0 * MCPT_BAND_TAU * area) * 1.05, 1e30) : 1e30f;
-    }
-    for (int g = 0; g < G; g++) {
-        FanGrp& fg = grp[g];
-        fg.first = s.group_start[g];
-        fg.count = s.group_count[g];
-        fg.ok = fg.count >= 16 && NL <= kFanMaxLights;
-        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, lmin = 1e300;
-        std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::vector<int>> edges;
-        for (int l = fg.first; l < fg.first + fg.count; l++) {
-            if (ln[l].w != ln[fg.first].w) fg.ok = 0;  // one sum L per group
-            const float4 p0 = P(l, 0), p1 = P(l, 1), p2 = P(l, 2);
-            const double a[3] = {(double)p1.x - p0.x, (double)p1.y - p0.y, (double)p1.z - p0.z};
-            const double b[3] = {(double)p2.x - p0.x, (double)p2.y - p0.y, (double)p2.z - p0.z};
-            const double cr[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
-            const double orient = cr[0] * ln[l].x + cr[1] * ln[l].y + cr[2] * ln[l].z;
-            if (!(std::fabs(orient) > 0) || !(eps[l] < 1e29f)) fg.ok = 0;  // degenerate triangle
-            for (int k = 0; k < 3; k++) {
-                const float4 p = P(l, k), q = P(l, (k + 1) % 3);
-                for (int ax = 0; ax < 3; ax++) {
-                    const double v = ax == 0 ? p.x : ax == 1 ? p.y : p.z;
-                    lo[ax] = std::min(lo[ax], v), hi[ax] = std::max(hi[ax], v);
-                }
-                const double dx = (double)q.x - p.x, dy = (double)q.y - p.y, dz = (double)q.z - p.z;
-                lmin = std::min(lmin, std::sqrt(dx * dx + dy * dy + dz * dz));
-                // undirected key (smaller endpoint first); the entry records (light, edge, direction)
-                auto kp = bits(p), kq = bits(q);
-                const bool fwd = kp < kq;
-                const auto lo_k = fwd ? kp : kq, hi_k = fwd ? kq : kp;
-                // direction about the unique normal: the oriented traversal of (p -> q)
-                const int dir = (orient > 0) == fwd ? 1 : -1;
-                edges[std::tuple_cat(lo_k, hi_k)].push_back(((l * 3 + k) << 1) | (dir > 0 ? 1 : 0));
-            }
-        }
-        // twins: exactly two triangles on the edge, traversing it in opposite directions once each is
-        // oriented by its unique normal; anything else stays a boundary edge (evaluated, never cancelled)
-        for (auto& kv : edges) {
-            const std::vector<int>& e = kv.second;
-            if (e.size() != 2 || (e[0] & 1) == (e[1] & 1)) continue;
-            const int l0 = (e[0] >> 1) / 3, k0 = (e[0] >> 1) % 3, l1 = (e[1] >> 1) / 3, k1 = (e[1] >> 1) % 3;
-            if (l0 == l1) continue;
-            (&nbr[l0].x)[k0] = l1;
-            (&nbr[l1].x)[k1] = l0;
-        }
-        // w: the group, and bit 30 = flip: the reference vertex order is not the positive one.  A front
-        // face (nl . (x1 - p0) > 0) has A . (B x C) = -2 area nl_geo . (x1 - p0) / (|a||b||c|), so the
-        // reference order is positive (A . (B x C) > 0) exactly when (p1 - p0) x (p2 - p0) opposes nl
-        for (int l = fg.first; l < fg.first + fg.count; l++) {
-            const float4 p0 = P(l, 0), p1 = P(l, 1), p2 = P(l, 2);
-            const double a[3] = {(double)p1.x - p0.x, (double)p1.y - p0.y, (double)p1.z - p0.z};
-            const double b[3] = {(double)p2.x - p0.x, (double)p2.y - p0.y, (double)p2.z - p0.z};
-            const double cr[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
-            const double orient = cr[0] * ln[l].x + cr[1] * ln[l].y + cr[2] * ln[l].z;
-            nbr[l].w = g | (orient > 0 ? (1 << 30) : 0);
-        }
-        double R = 0;
-        for (int ax = 0; ax < 3; ax++) fg.c[ax] = 0.5 * (lo[ax] + hi[ax]);
-        for (int l = fg.first; l < fg.first + fg.count; l++)
-            for (int k = 0; k < 3; k++) {
-                const float4 p = P(l, k);
-                const double dx = p.x - fg.c[0], dy = p.y - fg.c[1], dz = p.z - fg.c[2];
-                R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz));
-            }
-        fg.R = R * (1 + 1e-9) + 1e-12;
-        fg.lmin = lmin;
-        fg.lsum2 = 2.0 * ln[fg.first].w;
-    }
-}
-
-// the light table as the kernels read it: vertices (.w = float(unique normal) component) and
-// (unique normal, sum L) per light
-void light_vertex_tables(const HostScene& s, std::vector<float4>& lv, std::vector<double4>& ln) {
-    lv.assign(3 * std::max(s.NL, 1), make_float4(0, 0, 0, 0));
-    ln.assign(std::max(s.NL, 1), make_double4(0, 0, 0, 0));
-    for (int l = 0; l < s.NL; l++) {
-        const int f = s.light_facet[l];
-        for (int k = 0; k < 3; k++)
-            lv[3 * l + k] = make_float4(s.pos[9 * f + 3 * k], s.pos[9 * f + 3 * k + 1], s.pos[9 * f + 3 * k + 2],
-                                        (float)s.unique_n[3 * f + k]);
-        ln[l] = make_double4(s.unique_n[3 * f], s.unique_n[3 * f + 1], s.unique_n[3 * f + 2], s.light_sum[l]);
-    }
-}
-
 int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if (device < 0) HIP_OK(hipGetDevice(&device));
     {
@@ -4540,13 +3874,18 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, s.light_rad, &d.light_rad))) return rc;
     if ((rc = upload(*D, s.light_sum, &d.light_sum))) return rc;
     if ((rc = upload(*D, s.light_facet, &d.light_facet))) return rc;
-    std::vector<float4> lv;
-    std::vector<double4> ln;
-    light_vertex_tables(s, lv, ln);
-    for (int l = 0; l < s.NL; l++)
-        for (int k = 0; k < 3; k++)
+    std::vector<float4> lv(3 * std::max(s.NL, 1));
+    std::vector<double4> ln(std::max(s.NL, 1));
+    for (int l = 0; l < s.NL; l++) {
+        const int f = s.light_facet[l];
+        for (int k = 0; k < 3; k++) {
+            lv[3 * l + k] = tv[3 * f + k];
+            lv[3 * l + k].w = (float)s.unique_n[3 * f + k];
             d.light_bound = std::max({d.light_bound, std::fabs(lv[3 * l + k].x), std::fabs(lv[3 * l + k].y),
                                       std::fabs(lv[3 * l + k].z)});
+        }
+        ln[l] = make_double4(s.unique_n[3 * f], s.unique_n[3 * f + 1], s.unique_n[3 * f + 2], s.light_sum[l]);
+    }
     if ((rc = upload(*D, lv, &d.lt_v))) return rc;
     if ((rc = upload(*D, ln, &d.lt_n))) return rc;
     {  // select_a_point_from_lights tables (MCPT_MODE_SHADE_AREA): running sums in table order, as the oracle
@@ -4597,25 +3936,6 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
         lf[4 * (size_t)l + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
         lf[4 * (size_t)l + 2] = make_float4(e2[2], (float)(2.0 * ln[l].w), 0, 0);
     }
-    std::vector<FanGrp> fgrp;
-    std::vector<int4> fnbr;
-    std::vector<float> feps;
-    build_fan_tables(s, lv, ln, fgrp, fnbr, feps);
-    // the device form: the eligible groups (the first kFanMaxGroups of them) as k_prep_fan's slots, and
-    // the neighbour table packed to 8 B per light, padded to whole 64-light words
-    std::vector<FanGrp> fslot;
-    for (const FanGrp& g : fgrp)
-        if (g.ok && g.count > 0 && (int)fslot.size() < kFanMaxGroups) fslot.push_back(g);
-    d.fan_nslots = (int)fslot.size();
-    d.fan_on = d.fan_nslots > 0;
-    if (fslot.empty()) fslot.push_back(FanGrp{});
-    std::vector<int2> fnb(64 * (size_t)std::max(prep_chunks(s.NL), 1), make_int2(-1, 0xFFFF));
-    for (int l = 0; l < s.NL && d.fan_on; l++) {
-        auto f16 = [](int o) { return o < 0 ? 0xFFFFu : (unsigned)o; };
-        fnb[l] = make_int2((int)(f16(fnbr[l].x) | f16(fnbr[l].y) << 16),
-                           (int)(f16(fnbr[l].z) | (((unsigned)fnbr[l].w >> 30) & 1u) << 16));
-    }
-    if ((rc = upload(*D, fslot, &d.fan_grp)) || (rc = upload(*D, fnb, &d.fan_nbr))) return rc;
     std::vector<LightPair> lpr(32 * (size_t)std::max(prep_chunks(s.NL), 1));
     for (size_t q = 0; q < lpr.size(); q++) {
         LightPair& P = lpr[q];
@@ -4634,7 +3954,6 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
             nl[2 + h] = (float)ln[l].y;
             nl[4 + h] = (float)ln[l].z;
             dd[h] = (float)((ln[l].x * v[0].x + ln[l].y * v[0].y + ln[l].z * v[0].z) + MCPT_EPS);
-            P.eps[h] = feps[l];
             for (int k = 0; k < 3; k++) {
                 pp[2 * (3 * k) + h] = v[k].x;
                 pp[2 * (3 * k + 1) + h] = v[k].y;
@@ -4868,19 +4187,6 @@ constexpr int kPk2F32Waves = MCPT_PK2_F32_WAVES;
 #define MCPT_PK2_WAVES 6
 #endif
 constexpr int kPk2Waves = MCPT_PK2_WAVES;
-// the boundary-edge prep (k_prep_fan) for the full preps of scenes with eligible light groups; 0: k_prep_pk2
-#ifndef MCPT_FAN
-#define MCPT_FAN 1
-#endif
-#ifndef MCPT_FAN_WAVES
-#define MCPT_FAN_WAVES 4
-#endif
-constexpr int kFanWaves = MCPT_FAN_WAVES;
-// fan preps need this many bytes of sliver-suspect words per node (0: not used)
-// (the kernel's LDS: up to 10 KB per wave at 4 waves / SIMD, up to 16 KB at 2)
-inline size_t fan_smask_bytes(const DScene& d, int nchunks) {
-    return (MCPT_FAN && d.fan_on && fan_wave_bytes(nchunks) <= 16 * 1024) ? 8ull * mask_stride(nchunks) : 0;
-}
 // whether launch_prep(-1, ...) with these masks takes the split form (variant 17), which writes every
 // node's candidate words (k_prep_exact reads them instead of redoing the cheap stages)
 inline bool prep_writes_masks(const DScene& d, const uint64_t* masks) {
@@ -4912,7 +4218,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
                        const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr, bool count_c1 = true,
-                       bool fp32 = false, uint64_t* smasks = nullptr) {
+                       bool fp32 = false) {
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
@@ -4931,18 +4237,6 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
         hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(256), prep_lds_bytes(nchunks), st, d, seed, n, qp, qn, qs, qpixel,
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, work, cache.slack, cache.exact_off,
                            cache.exact_counts, cache.maybe);
-    } else if (variant == 17 && smasks && fan_smask_bytes(d, nchunks) && !fp32 && !cache.build) {
-        // the boundary-edge form (k_prep_fan): the cull also writes the sliver-suspect words
-        if (count_c1 || !stats)
-            hipLaunchKernelGGL((k_prep_cull_lanes<true, true>), dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
-                               n, qp, qn, qs, masks, nchunks, stats, smasks);
-        else
-            hipLaunchKernelGGL((k_prep_cull_lanes<false, true>), dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st,
-                               d, n, qp, qn, qs, masks, nchunks, stats, smasks);
-        const int fb = fan_wave_bytes(nchunks);
-        auto kf = fb <= 10 * 1024 ? k_prep_fan<kFanWaves> : k_prep_fan<2>;
-        hipLaunchKernelGGL(kf, dim3(blocks), dim3(256), kFanSlotBytes + 4 * fb, st, d, seed, n, qp, qs, qpixel, qsample, qnode, u, wsum, pick,
-                           count, stats, nchunks, fb, work, cache, (const uint64_t*)masks, (const uint64_t*)smasks);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
         if (count_c1 || !stats)
             hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
@@ -5061,13 +4355,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     // launch's tail -- measured +6% Veach, +21% Cornell-1M over 4 Mi), but no more than the call's
     // camera samples (a small render holds all its roots at once) and no more than half the free
     // HBM (the other half is left to the root-point cache and the caller)
-    size_t ws_held = D.masks.bytes + D.smasks.bytes, ws_free = 0, ws_total = 0;
+    size_t ws_held = D.masks.bytes, ws_free = 0, ws_total = 0;
     for (int k = 0; k < 14; k++) ws_held += D.qa[k].bytes + D.qb[k].bytes;
     for (int k = 0; k < 9; k++) ws_held += D.aux[k].bytes;
     for (int k = 0; k < 13; k++) ws_held += D.sl[k].bytes;
     HIP_OK(hipMemGetInfo(&ws_free, &ws_total));
-    const size_t ws_node_bytes = 2 * 132 + 152 + 8 * (size_t)mask_stride(prep_chunks(D.d.NL)) + 280 +
-                                 fan_smask_bytes(D.d, prep_chunks(D.d.NL));  // queues aux words (suspect words) slots
+    const size_t ws_node_bytes = 2 * 132 + 152 + 8 * (size_t)mask_stride(prep_chunks(D.d.NL)) + 280;  // queues aux words slots
     const long long ws_mem = (long long)((ws_free + ws_held) / 2 / ((size_t)qf * ws_node_bytes));
     const long long target_ll =
         o->samples_per_launch > 0
@@ -5081,7 +4374,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int cap = (int)std::min<long long>((long long)qf * target + 1024, (1ll << 30));
     int rc;
     if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) ||
-        (MCPT_ROOT_TABLE && ((rc = ensure(D.root_pnw, 72ull * npx)) || (rc = ensure(D.root_kind, 4ull * npx)))) || (rc = ensure(D.stats, 256)) ||
+        (MCPT_ROOT_TABLE && ((rc = ensure(D.root_pnw, 72ull * npx)) || (rc = ensure(D.root_kind, 4ull * npx)))) || (rc = ensure(D.stats, 128)) ||
         (rc = ensure(D.work, 256)))
         return rc;
     Queue qa, qb;
@@ -5125,14 +4418,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0, trace_launches = 0;
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
-    uint64_t* smasks = nullptr;  // the boundary-edge prep's sliver-suspect words (k_prep_fan)
     if (needs_prep && D.d.NL > kSmallNL) {
         if ((rc = ensure(D.masks, (size_t)std::max(cap, npx) * mask_stride(nchunks) * 8))) return rc;
         masks = (uint64_t*)D.masks.p;
-        if (!fp32 && fan_smask_bytes(D.d, nchunks)) {
-            if ((rc = ensure(D.smasks, (size_t)cap * mask_stride(nchunks) * 8))) return rc;
-            smasks = (uint64_t*)D.smasks.p;
-        }
     }
     // exact pick: nodes inside the ambiguity band go to k_prep_exact; the opt-in fp32
     // precision makes no exactness claim, and the small-table prep (k_prep_lane) is exact by construction
@@ -5200,7 +4488,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     }
     // every buffer is allocated above (first-call hipMalloc of the cache is not device work); the
     // timed region (seconds, HIP events) starts at the primary-hit kernel
-    HIP_OK(hipMemsetAsync(D.stats.p, 0, 256, st));
+    HIP_OK(hipMemsetAsync(D.stats.p, 0, 128, st));
     HIP_OK(hipEventRecord(D.ev0, st));
     hipLaunchKernelGGL(grid ? k_primary<true> : k_primary<false>, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock),
                        0, st, D.d, cf, (int*)D.hit_f.p, (double*)D.hit_tbg.p);
@@ -5380,7 +4668,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                        cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
-                                       count_c1, fp32, smasks));
+                                       count_c1, fp32));
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
@@ -5412,7 +4700,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                    cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
-                                   count_c1, fp32, smasks));
+                                   count_c1, fp32));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 timed = true;
             }
@@ -5516,8 +4804,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, D.ev0, D.ev1));
     if (stats) {
-        unsigned long long hs[32] = {0};
-        HIP_OK(hipMemcpy(hs, D.stats.p, 256, hipMemcpyDeviceToHost));
+        unsigned long long hs[16] = {0};
+        HIP_OK(hipMemcpy(hs, D.stats.p, 128, hipMemcpyDeviceToHost));
         stats->seconds = ms * 1e-3;
         stats->camera_samples = (uint64_t)(s1 - s0) * npx;
         stats->light_evals_survived = hs[1];
@@ -5547,9 +4835,6 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->prep_launches = prep_launches;
         stats->prep_exact_nodes = hs[10];
         stats->prep_band_nodes = hs[11];
-        stats->light_evals_weighed = hs[16];
-        stats->prep_fan_edges = hs[17];
-        stats->prep_fan_nodes = hs[18];
 #if MCPT_BAND_DIAG
         fprintf(stderr, "exact diag (10 ns ticks summed over nodes): lists %llu literal %llu lists+literal+sum %llu pick %llu\n",
                 hs[12], hs[13], hs[14], hs[15]);
@@ -5649,9 +4934,6 @@ void add_stats(mcpt_stats& t, const mcpt_stats& x) {
     t.prep_exact_nodes += x.prep_exact_nodes;
     t.prep_band_nodes += x.prep_band_nodes;
     t.cache_build_seconds += x.cache_build_seconds;
-    t.light_evals_weighed += x.light_evals_weighed;
-    t.prep_fan_edges += x.prep_fan_edges;
-    t.prep_fan_nodes += x.prep_fan_nodes;
 }
 
 // progress of a multi-device call: the shards' dispatched counts are summed and the caller's callback
@@ -5971,8 +5253,6 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
     }
     void *dp, *dn, *du, *dw, *dc, *dk, *dm, *dl = nullptr, *ds = nullptr, *dsl = nullptr;
     HIP_OK(hipMalloc(&dm, 8ull * n * mask_stride(prep_chunks(D->d.NL))));  // candidate words of the split prep (variant 17)
-    void* dsm = nullptr;  // and the boundary-edge prep's suspect words
-    if (fan_smask_bytes(D->d, prep_chunks(D->d.NL))) HIP_OK(hipMalloc(&dsm, 8ull * n * mask_stride(prep_chunks(D->d.NL))));
     HIP_OK(hipMalloc(&dp, 24ull * n));
     HIP_OK(hipMalloc(&dn, 24ull * n));
     HIP_OK(hipMalloc(&du, 8ull * n));
@@ -6005,7 +5285,7 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
         cx.maybe = exact ? (int*)dl + n + kExactHead : nullptr;
         HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream,
-                           cx, (uint64_t*)dm, true, false, (uint64_t*)dsm));
+                           cx, (uint64_t*)dm));
         if (exact)
             hipLaunchKernelGGL(k_prep_band, dim3(kBandBlocks), dim3(256), 0, D->stream, D->d, (const int*)cx.maybe,
                                (const double*)dsl, (const double*)dp, n, (const uint64_t*)dm,
@@ -6023,7 +5303,7 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
     HIP_OK(hipMemcpy(count, dc, 4ull * n, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(pick, dk, 4ull * n, hipMemcpyDeviceToHost));
     for (int k = 0; k < n; k++) pick[k] = pick[k] >= 0 ? sc->host.light_facet[pick[k]] : -1;
-    void* bufs[] = {dp, dn, du, dw, dc, dk, dm, dl, ds, dsl, dsm};
+    void* bufs[] = {dp, dn, du, dw, dc, dk, dm, dl, ds, dsl};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     return MCPT_OK;
@@ -6134,7 +5414,7 @@ void mcpt_scene_destroy(mcpt_scene* sc) {
         std::vector<DevBuf*> bufs = {&D->hit_f, &D->hit_tbg, &D->fb, &D->rank_fb, &D->stats, &D->work, &D->cache_bt, &D->cache_lst,
                                      &D->cache_info, &D->cache_w, &D->masks, &D->g_start, &D->g_tri, &D->root_pnw,
                                      &D->root_kind, &D->exact, &D->exact_scr, &D->slack, &D->lit_slot, &D->lit_pool,
-                                     &D->sc_cum, &D->sc_wsum, &D->sc_last, &D->smasks};
+                                     &D->sc_cum, &D->sc_wsum, &D->sc_last};
         for (int k = 0; k < 14; k++) bufs.insert(bufs.end(), {&D->qa[k], &D->qb[k], &D->qs[k]});
         for (int k = 0; k < 9; k++) bufs.push_back(&D->aux[k]);
         for (int k = 0; k < 13; k++) bufs.push_back(&D->sl[k]);
@@ -6365,37 +5645,6 @@ int mcpt_debug_light_literal(mcpt_scene* sc, const double* x1, const double* nrm
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(out, dout, 160ull * NL, hipMemcpyDeviceToHost));
     (void)hipFree(dout);
-    return MCPT_OK;
-}
-
-int mcpt_debug_fan_tables(mcpt_scene* sc, int32_t* ngroups, int32_t* nbr, double* grp, int32_t* gok, float* eps) {
-    if (!sc || !ngroups) {
-        set_error("invalid argument");
-        return MCPT_E_INVALID;
-    }
-    const HostScene& s = sc->host;
-    *ngroups = (int32_t)s.group_start.size();
-    if (!nbr) return MCPT_OK;
-    if (!grp || !gok || !eps) {
-        set_error("invalid argument");
-        return MCPT_E_INVALID;
-    }
-    std::vector<float4> lv;
-    std::vector<double4> ln;
-    light_vertex_tables(s, lv, ln);
-    std::vector<FanGrp> g;
-    std::vector<int4> nb;
-    std::vector<float> e;
-    build_fan_tables(s, lv, ln, g, nb, e);
-    for (int l = 0; l < s.NL; l++) {
-        nbr[4 * l] = nb[l].x, nbr[4 * l + 1] = nb[l].y, nbr[4 * l + 2] = nb[l].z, nbr[4 * l + 3] = nb[l].w;
-        eps[l] = e[l];
-    }
-    for (int k = 0; k < *ngroups; k++) {
-        const double v[8] = {g[k].c[0], g[k].c[1], g[k].c[2], g[k].R, g[k].lmin, g[k].lsum2, (double)g[k].first, (double)g[k].count};
-        for (int q = 0; q < 8; q++) grp[8 * k + q] = v[q];
-        gok[k] = g[k].ok;
-    }
     return MCPT_OK;
 }
 
