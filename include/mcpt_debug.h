@@ -41,7 +41,10 @@ int mcpt_debug_set_collective_lib(const char* path);
  * LDS candidate queue, any N_L); 8 k_prep_pk2 (packed-fp32 cheap stages, stored LDS candidate list,
  * branch-free fp64 batches, lane-parallel batch search in one kernel); 9 k_prep_lane (lane per
  * node, small light sets); 17 k_prep_cull_lanes (lane per node, light table in scalar registers)
- * + k_prep_pk2's fp64 phase (the renderer's form).  Other values: MCPT_E_DEVICE (invalid value). */
+ * + k_prep_pk2's fp64 phase (the renderer's form: the cull's lanes take the nodes bucketed by their
+ * tangent-plane chunk classes and skip the work a class decides, k_cull_classify); 18 variant 17 without
+ * that order and without the chunk classes (its candidate words must be identical).  Other values:
+ * MCPT_E_DEVICE (invalid value). */
 int mcpt_debug_prep_bench(mcpt_scene* scene, int32_t n, const double* x1, const double* normal, const double* u,
                           int32_t variant, int32_t iters, double* ms_per_launch, double* weights_sum, int32_t* pick);
 

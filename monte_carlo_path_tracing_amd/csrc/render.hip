@@ -1782,6 +1782,10 @@ static_assert(kCullBurst % 2 == 0 && kMaskLine % kCullBurst == 0, "cull burst");
 #define MCPT_CULL_SPLITS 6
 #endif
 inline int cull_splits(int nchunks) { return std::max(1, std::min(MCPT_CULL_SPLITS, nchunks / 4)); }
+// chunk classes in the cull (chunk_class) with the nodes ordered by their class pattern (k_cull_classify)
+#ifndef MCPT_CULL_CLASSES
+#define MCPT_CULL_CLASSES 1
+#endif
 // Phase A with a lane per shading node and the light table in scalar registers: each light pair
 // (LightPair, two s_load_dwordx16) is read once per 64 nodes from the scalar cache, and the two
 // cheap stages of both lights run as 13 v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 with one
@@ -1819,10 +1823,28 @@ __device__ inline unsigned shift_in(unsigned w, uint64_t carry) {
     return r;
 }
 
+// Chunk classes of the tangent-plane test (Mylight.cpp:347-357) from the chunk's vertex sphere
+// (chunk_sph: centre c, radius r rounded up): h = n . c - (n . x1 + 1e-8) in the same fp32 form as the
+// cull's t (|c| <= light_bound, so its rounding error is within err too).  ABOVE: h - r > 4 err, so every
+// vertex has t > err in fp32 and t > 0 exactly -- the plane test passes every light of the chunk without
+// ambiguity and the candidate bit is the light-side test alone.  BELOW: h + r < -4 err -- every light is
+// plane-culled exactly and in fp32, so the chunk's word is 0.  (4 err covers err for h, err for t and the
+// rounding of h -+ r.)  Else STRADDLE: the full two-stage cull.
+enum { kChunkStraddle = 0, kChunkAbove = 1, kChunkBelow = 2 };
+__device__ inline unsigned chunk_class(float nx, float ny, float nz, float ncn, float err, float4 sp) {
+    const float h = fmaf(nx, sp.x, fmaf(ny, sp.y, fmaf(nz, sp.z, ncn)));
+    const float m = 4.0f * err;
+    return h - sp.w > m ? kChunkAbove : h + sp.w < -m ? kChunkBelow : kChunkStraddle;
+}
+
 // the two cheap stages of light pair T (lights A, B) for this lane's node, threshold folded in:
 // s = nl . x1 - (nl . p0 + 1e-8), t[k] = n . p_k - (n . x1 + 1e-8)
 struct CullLane {
     v2f xx, yy, zz, nxx, nyy, nzz, ncn;
+    __device__ inline v2f eval_s(const LightPair& L) const {  // the light-side value alone
+        const v2f nlx{L.nl[0].x, L.nl[0].y}, nly{L.nl[1].x, L.nl[1].y}, nlz{L.nl[2].x, L.nl[2].y};
+        return __builtin_elementwise_fma(xx, nlx, __builtin_elementwise_fma(yy, nly, zz * nlz)) - v2f{L.d.x, L.d.y};
+    }
     __device__ inline void eval(const LightPair& L, v2f* s, v2f* t) const {
         const v2f nlx{L.nl[0].x, L.nl[0].y}, nly{L.nl[1].x, L.nl[1].y}, nlz{L.nl[2].x, L.nl[2].y};
         // (the subtraction stays separate: a packed FMA reads at most one scalar operand)
@@ -1840,7 +1862,17 @@ struct CullLane {
 // (bit j = light 64 c + j)
 template <bool kCountC1>
 __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const LightPair* __restrict__ T, int c,
-                                      float err, uint64_t actm, bool act, d3 x1, d3 nn, unsigned long long& c1) {
+                                      float err, uint64_t actm, bool act, d3 x1, d3 nn, unsigned long long& c1,
+                                      bool classes) {
+    // wave-uniform chunk classes (chunk_class; the nodes arrive sorted by their classes, k_cull_order):
+    // every lane BELOW -- the word is 0 (not in the counting instance, which counts the light-side culls);
+    // every lane ABOVE -- the light-side test alone.  Inactive lanes agree with anything.
+    bool above = false;
+    if (MCPT_CULL_CLASSES && classes) {
+        const unsigned cls = chunk_class(cl.nxx[0], cl.nyy[0], cl.nzz[0], cl.ncn[0], err, S.chunk_sph[c]);
+        if (!kCountC1 && (__ballot(cls != kChunkBelow) & actm) == 0) return 0ull;
+        above = (__ballot(cls != kChunkAbove) & actm) == 0;
+    }
     unsigned word[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -1849,6 +1881,20 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
         float amin = __builtin_inff();  // min over the 32 lights of min(|s|, |min(s, max t)|)
         // pairs holding real lights (the table's last chunk is partial: N_L = 3012 leaves 4 of 64)
         const int qend = kCountC1 ? 16 : min(16, max(0, (S.NL - (64 * c + 32 * h) + 1) >> 1));
+        // ABOVE: every fp32 t > err, so min(s, max t) > err iff s > err and |min(s, max t)| <= err iff
+        // |s| <= err -- the same bits and the same fallback trigger as pair() without the t terms.  A NaN
+        // s (a degenerate light's normal) passes the light-side test as in the reference (Mylight.cpp:342
+        // culls only tmp < eps) and as in pair(), whose v_min_f32 returns max t for it: !(s <= err).
+        auto pair_s = [&](int q) {
+            const v2f s1 = cl.eval_s(Th[q]);
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const float sv = s1[e];
+                amin = min_abs_raw(amin, sv);
+                if (kCountC1) c1w += __popcll(__ballot(sv < -err) & actm);  // statistic only
+                w = shift_in(w, __ballot(!(sv <= err)));
+            }
+        };
         auto pair = [&](int q) {
             v2f s1, t[3];
             cl.eval(Th[q], &s1, t);
@@ -1863,8 +1909,13 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
             }
         };
         if (qend == 16) {
+            if (above) {
 #pragma unroll 2
-            for (int q = 0; q < 16; q++) pair(q);
+                for (int q = 0; q < 16; q++) pair_s(q);
+            } else {
+#pragma unroll 2
+                for (int q = 0; q < 16; q++) pair(q);
+            }
         } else {  // the padding lights' bits stay clear; light j's bit back at 31 - j
             for (int q = 0; q < qend; q++) pair(q);
             w = qend == 0 ? 0u : w << (32 - 2 * qend);
@@ -1899,10 +1950,11 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
 template <bool kCountC1>
 __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S, int n, const double* __restrict__ qp,
                                                          const double* __restrict__ qn, int qs, uint64_t* __restrict__ masks,
-                                                         int nchunks, unsigned long long* stats) {
-    const int node = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool act = node < n;
-    const int nd = act ? node : n - 1;
+                                                         int nchunks, unsigned long long* stats,
+                                                         const int* __restrict__ order) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = idx < n;
+    const int nd = order ? order[act ? idx : n - 1] : (act ? idx : n - 1);  // the node this lane culls
     const d3 x1 = ld3(qp, qs, nd);
     const d3 nn = ld3(qn, qs, nd);
     const NodeF f = node_f(x1, nn, S.light_bound);
@@ -1931,7 +1983,7 @@ __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S,
 #pragma unroll
         for (int i = 0; i < kCullBurst; i++) {
             const int c = kCullBurst * p + i;
-            w[i] = c < nchunks ? cull_chunk<kCountC1>(S, cl, T, c, err, actm, act, x1, nn, c1) : 0ull;
+            w[i] = c < nchunks ? cull_chunk<kCountC1>(S, cl, T, c, err, actm, act, x1, nn, c1, order != nullptr) : 0ull;
         }
         if (act)
 #pragma unroll
@@ -1946,6 +1998,95 @@ __global__ __launch_bounds__(256, MCPT_LB_CULL) void k_prep_cull_lanes(DScene S,
     if (kCountC1 && pe == bursts) c1 -= (unsigned long long)(64 * nchunks - S.NL) * (unsigned long long)__popcll(actm);
     if ((threadIdx.x & 63) == 0 && stats && c1) atomicAdd(stats + 6, c1);
 }
+
+// ---- the cull's node order (k_cull_classify + k_cull_scatter) ----
+// A chunk's class skips work in k_prep_cull_lanes only when every lane of the wave agrees, and a
+// generation's nodes come in no spatial order.  The class pattern over the chunks depends on the node's
+// tangent plane alone (every node of a flat surface has the same one), so the nodes are bucketed by a
+// hash of it: k_cull_classify hashes each node's pattern into one of kCullBuckets buckets and counts
+// them, k_cull_scatter writes the order (bucket by bucket) that the cull's lanes read their nodes in.
+// The candidate words do not depend on the order (each lane writes its node's row), only the work does.
+constexpr int kCullBuckets = 64;
+constexpr int kCullPer = 8;  // nodes per thread of the two order kernels
+__device__ inline unsigned cull_pattern_bucket(const DScene& S, d3 x1, d3 nn, int nchunks) {
+    const NodeF f = node_f(x1, nn, S.light_bound);
+    const float ncn = -(float)(dot(nn, x1) + MCPT_EPS);  // as in k_prep_cull_lanes
+    unsigned h = 2166136261u;
+    for (int c = 0; c < nchunks; c++) h = (h ^ chunk_class(f.nx, f.ny, f.nz, ncn, f.err, S.chunk_sph[c])) * 16777619u;
+    h ^= h >> 15;
+    h *= 0x2c1b3c6du;
+    h ^= h >> 12;
+    return h & (kCullBuckets - 1);
+}
+// LDS histogram add of bucket b for the active lanes, one atomic per distinct bucket of the wave in the
+// common case (a wave of one surface); returns this lane's rank among the block's nodes of its bucket
+__device__ inline unsigned hist_add(unsigned* hist, unsigned b) {
+    const unsigned b0 = __builtin_amdgcn_readfirstlane(b);
+    const uint64_t m = __ballot(b == b0);
+    const int lead = __ffsll((unsigned long long)m) - 1;
+    unsigned base = 0;
+    if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(&hist[b0], (unsigned)__popcll(m));
+    base = __builtin_amdgcn_readlane(base, lead);
+    return b == b0 ? base + (unsigned)lane_rank(m) : atomicAdd(&hist[b], 1u);
+}
+__global__ __launch_bounds__(256) void k_cull_classify(DScene S, int n, const double* __restrict__ qp,
+                                                       const double* __restrict__ qn, int qs, int nchunks,
+                                                       unsigned char* __restrict__ keys, unsigned* __restrict__ count) {
+    __shared__ unsigned hist[kCullBuckets];
+    if (threadIdx.x < kCullBuckets) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int k = 0; k < kCullPer; k++) {
+        const int node = (blockIdx.x * kCullPer + k) * 256 + threadIdx.x;
+        if (node < n) {
+            const unsigned b = cull_pattern_bucket(S, ld3(qp, qs, node), ld3(qn, qs, node), nchunks);
+            keys[node] = (unsigned char)b;
+            (void)hist_add(hist, b);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kCullBuckets && hist[threadIdx.x]) atomicAdd(&count[threadIdx.x], hist[threadIdx.x]);
+}
+// count[0, kCullBuckets): nodes per bucket (k_cull_classify); count[kCullBuckets, 2 kCullBuckets): the
+// buckets' fill cursors (zero before the launch); order[bucket start + cursor] = node
+__global__ __launch_bounds__(256) void k_cull_scatter(int n, const unsigned char* __restrict__ keys,
+                                                      unsigned* __restrict__ count, int* __restrict__ order) {
+    __shared__ unsigned hist[kCullBuckets], start[kCullBuckets];
+    if (threadIdx.x < kCullBuckets) {
+        hist[threadIdx.x] = 0;
+        start[threadIdx.x] = count[threadIdx.x];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan of the bucket sizes
+        unsigned s = 0;
+        for (int b = 0; b < kCullBuckets; b++) {
+            const unsigned v = start[b];
+            start[b] = s;
+            s += v;
+        }
+    }
+    unsigned rank[kCullPer], key[kCullPer];
+    for (int k = 0; k < kCullPer; k++) {
+        const int node = (blockIdx.x * kCullPer + k) * 256 + threadIdx.x;
+        if (node < n) {
+            key[k] = keys[node];
+            rank[k] = hist_add(hist, key[k]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kCullBuckets && hist[threadIdx.x])
+        start[threadIdx.x] += atomicAdd(&count[kCullBuckets + threadIdx.x], hist[threadIdx.x]);
+    __syncthreads();
+    for (int k = 0; k < kCullPer; k++) {
+        const int node = (blockIdx.x * kCullPer + k) * 256 + threadIdx.x;
+        if (node < n) order[start[key[k]] + rank[k]] = node;
+    }
+}
+// device scratch of the cull's node order: keys u8[n], order int[n], count u32[2 kCullBuckets]
+struct CullOrder {
+    unsigned char* keys = nullptr;
+    int* order = nullptr;
+    unsigned* count = nullptr;
+};
 
 // skip the list append of an all-zero candidate word by a scalar branch (same-box A/B:
 // 410.6 / 425.0 / 425.1 vs 423.8 / 415.8 / 421.9 Msamples/s, profiles/round2b_ab_zero_words.txt)
@@ -3723,6 +3864,7 @@ struct DeviceState {
     hipStream_t stream = nullptr;
     // reusable work buffers
     DevBuf hit_f, hit_tbg, root_pnw, root_kind, fb, rank_fb, stats, work, qa[14], qb[14], qs[14], aux[9], sl[13], cache_bt, cache_lst, cache_info, cache_w, masks;
+    DevBuf cull_keys, cull_order, cull_count;  // the cull's node order (CullOrder)
     DevBuf exact, exact_scr, slack;  // exact pick: list, k_prep_exact's scratch, per-node slack
     DevBuf lit_slot, lit_pool;        // exact pick: roots' literal sums per pixel (RootLit)
     DevBuf sc_cum, sc_wsum, sc_last;  // small-table root-point cache (SmallCache)
@@ -3763,6 +3905,14 @@ int ensure(DevBuf& b, size_t bytes) {
     b.p = nullptr;
     HIP_OK(hipMalloc(&b.p, std::max<size_t>(bytes, 256)));
     b.bytes = std::max<size_t>(bytes, 256);
+    return MCPT_OK;
+}
+// the cull's node-order scratch for up to n nodes
+int cull_order_bufs(DeviceState& D, size_t n, CullOrder* co) {
+    int rc;
+    if ((rc = ensure(D.cull_keys, n)) || (rc = ensure(D.cull_order, 4 * n)) || (rc = ensure(D.cull_count, 8 * kCullBuckets)))
+        return rc;
+    *co = CullOrder{(unsigned char*)D.cull_keys.p, (int*)D.cull_order.p, (unsigned*)D.cull_count.p};
     return MCPT_OK;
 }
 
@@ -4218,12 +4368,14 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
                        const int* qpixel, const int* qsample, const uint64_t* qnode, const double* u, double* wsum,
                        int* pick, int* count, unsigned long long* stats, unsigned* work, hipStream_t st,
                        const PrepCache& cache = PrepCache{}, uint64_t* masks = nullptr, bool count_c1 = true,
-                       bool fp32 = false) {
+                       bool fp32 = false, const CullOrder& co = CullOrder{}) {
     const int nchunks = prep_chunks(d.NL);
     const int wb = prep_list_wave_bytes(nchunks);
     const bool list_ok = d.NL <= 65535 && 4 * wb <= kPrepListMaxLds;
     if (variant < 0) variant = d.NL <= kSmallNL ? 9 : list_ok ? (masks ? 17 : 8) : 0;  // A/B: tools/prep_variants.py
-    if (variant != 0 && variant != 8 && variant != 9 && variant != 17) return hipErrorInvalidValue;
+    if (variant != 0 && variant != 8 && variant != 9 && variant != 17 && variant != 18) return hipErrorInvalidValue;
+    const bool ordered = variant == 17;  // 18: variant 17 without the node order and the chunk classes (A/B, tests)
+    if (variant == 18) variant = 17;
     if (variant == 9) return launch_prep_lane(d, seed, n, qp, qn, qs, qpixel, qsample, qnode, u, wsum, pick, count, stats, st,
                                               SmallCache{}, false);
     if (variant > 0 && !list_ok) variant = 0;
@@ -4238,12 +4390,21 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
                            qsample, qnode, u, wsum, pick, count, stats, nchunks, work, cache.slack, cache.exact_off,
                            cache.exact_counts, cache.maybe);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
+        const int* order = nullptr;
+        if (MCPT_CULL_CLASSES && co.order && ordered) {  // the nodes bucketed by their chunk-class pattern
+            e = hipMemsetAsync(co.count, 0, 8 * kCullBuckets, st);
+            if (e != hipSuccess) return e;
+            const dim3 go((n + 256 * kCullPer - 1) / (256 * kCullPer));
+            hipLaunchKernelGGL(k_cull_classify, go, dim3(256), 0, st, d, n, qp, qn, qs, nchunks, co.keys, co.count);
+            hipLaunchKernelGGL(k_cull_scatter, go, dim3(256), 0, st, n, (const unsigned char*)co.keys, co.count, co.order);
+            order = co.order;
+        }
         if (count_c1 || !stats)
             hipLaunchKernelGGL(k_prep_cull_lanes<true>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
-                               n, qp, qn, qs, masks, nchunks, stats);
+                               n, qp, qn, qs, masks, nchunks, stats, order);
         else
             hipLaunchKernelGGL(k_prep_cull_lanes<false>, dim3((n + 255) / 256, cull_splits(nchunks)), dim3(256), 0, st, d,
-                               n, qp, qn, qs, masks, nchunks, stats);
+                               n, qp, qn, qs, masks, nchunks, stats, order);
         // fp32: MCPT_RENDER_PRECISION_FP32's packed-fp32 full stage (light_weight_f32x2)
         auto kern = cache.build ? (fp32 ? k_prep_pk2<kPk2F32Waves, true, true, true> : k_prep_pk2<kPk2Waves, true, true, false>)
                                 : (fp32 ? k_prep_pk2<kPk2F32Waves, false, true, true> : k_prep_pk2<kPk2Waves, false, true, false>);
@@ -4418,9 +4579,11 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0, trace_launches = 0;
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
+    CullOrder corder{};
     if (needs_prep && D.d.NL > kSmallNL) {
         if ((rc = ensure(D.masks, (size_t)std::max(cap, npx) * mask_stride(nchunks) * 8))) return rc;
         masks = (uint64_t*)D.masks.p;
+        if ((rc = cull_order_bufs(D, (size_t)std::max(cap, npx), &corder))) return rc;
     }
     // exact pick: nodes inside the ambiguity band go to k_prep_exact; the opt-in fp32
     // precision makes no exactness claim, and the small-table prep (k_prep_lane) is exact by construction
@@ -4526,7 +4689,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             pc.build = 1;
             HIP_OK(hipEventRecord(D.evp0, st));
             HIP_OK(launch_prep(masks ? 17 : 8, D.d, o->seed, nr, qb.p, qb.n, qb.cap, qb.pixel, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks, count_c1, fp32));
+                               nullptr, nullptr, P.stats, (unsigned*)D.work.p, st, pc, masks, count_c1, fp32, corder));
             HIP_OK(hipEventRecord(D.evp1, st));
             HIP_OK(hipEventSynchronize(D.evp1));
             float ms = 0;
@@ -4668,7 +4831,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                        cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
-                                       count_c1, fp32));
+                                       count_c1, fp32, corder));
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
@@ -4700,7 +4863,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                 HIP_OK(hipEventRecord(D.evp0, st));
                 HIP_OK(launch_prep(-1, D.d, o->seed, ni, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
                                    cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
-                                   count_c1, fp32));
+                                   count_c1, fp32, corder));
                 HIP_OK(hipEventRecord(D.evp1, st));
                 timed = true;
             }
@@ -5273,6 +5436,8 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
     }
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
     if ((rc = ensure(D->work, 256))) return rc;
+    CullOrder co{};
+    if ((rc = cull_order_bufs(*D, (size_t)n, &co))) return rc;
     if (all_exact) {
         std::vector<int> all(n + kExactHead, 0);
         all[0] = n;
@@ -5285,7 +5450,7 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
         cx.maybe = exact ? (int*)dl + n + kExactHead : nullptr;
         HIP_OK(launch_prep(-1, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (unsigned*)D->work.p, D->stream,
-                           cx, (uint64_t*)dm));
+                           cx, (uint64_t*)dm, true, false, co));
         if (exact)
             hipLaunchKernelGGL(k_prep_band, dim3(kBandBlocks), dim3(256), 0, D->stream, D->d, (const int*)cx.maybe,
                                (const double*)dsl, (const double*)dp, n, (const uint64_t*)dm,
@@ -5414,7 +5579,7 @@ void mcpt_scene_destroy(mcpt_scene* sc) {
         std::vector<DevBuf*> bufs = {&D->hit_f, &D->hit_tbg, &D->fb, &D->rank_fb, &D->stats, &D->work, &D->cache_bt, &D->cache_lst,
                                      &D->cache_info, &D->cache_w, &D->masks, &D->g_start, &D->g_tri, &D->root_pnw,
                                      &D->root_kind, &D->exact, &D->exact_scr, &D->slack, &D->lit_slot, &D->lit_pool,
-                                     &D->sc_cum, &D->sc_wsum, &D->sc_last};
+                                     &D->sc_cum, &D->sc_wsum, &D->sc_last, &D->cull_keys, &D->cull_order, &D->cull_count};
         for (int k = 0; k < 14; k++) bufs.insert(bufs.end(), {&D->qa[k], &D->qb[k], &D->qs[k]});
         for (int k = 0; k < 9; k++) bufs.push_back(&D->aux[k]);
         for (int k = 0; k < 13; k++) bufs.push_back(&D->sl[k]);
@@ -5686,14 +5851,16 @@ int mcpt_debug_prep_bench(mcpt_scene* sc, int32_t n, const double* x1, const dou
     }
     HIP_OK(hipMemcpy(du, u, 8ull * n, hipMemcpyHostToDevice));
     if ((rc = ensure(D->work, 256))) return rc;
+    CullOrder co{};
+    if ((rc = cull_order_bufs(*D, (size_t)n, &co))) return rc;
     HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                        (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream,
-                       PrepCache{}, (uint64_t*)dm));
+                       PrepCache{}, (uint64_t*)dm, true, false, co));
     HIP_OK(hipEventRecord(D->ev0, D->stream));
     for (int it = 0; it < iters; it++)
         HIP_OK(launch_prep(variant, D->d, 0, n, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, nullptr, nullptr, (unsigned*)D->work.p, D->stream,
-                       PrepCache{}, (uint64_t*)dm));
+                       PrepCache{}, (uint64_t*)dm, true, false, co));
     HIP_OK(hipEventRecord(D->ev1, D->stream));
     HIP_OK(hipEventSynchronize(D->ev1));
     float t = 0;

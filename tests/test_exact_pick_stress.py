@@ -114,3 +114,25 @@ def test_mis_frame_vs_oracle(scenes, name):
         name, l2, mx, st.shading_nodes, st.prep_band_nodes, st.prep_exact_nodes))
     assert np.isfinite(img).all() and ref.sum() > 0
     assert l2 <= TOL and mx <= TOL
+
+
+@pytest.mark.parametrize("name", ["veach"] + sorted(scenegen.STRESS))
+def test_cull_chunk_classes_change_no_candidate(scenes, name):
+    """The cull's chunk classes (a 64-light chunk wholly above / below a node's tangent
+    plane skips the plane test / the whole chunk) and the node order that makes them wave-uniform change
+    work only: 20 000 points area-sampled on both sides of every non-light facet (above, below and
+    straddling chunks all occur), prep variant 17 (ordered, classes on) vs 18 (the plain cull) --
+    weights_sum and picks bit-identical."""
+    if name == "veach":
+        from conftest import SCENE_OBJ as obj, SCENE_XML as xml
+    else:
+        obj, xml, _ = scenes[name]
+    s = mcpt.Scene.load(obj, xml)
+    if s.nlights <= 64 or s.nlights > 7680:  # k_prep_lane / k_prep: no candidate words, no classes
+        pytest.skip("prep without the split cull")
+    X, N, u = surface_points(po.Scene(obj, xml), 20000, seed=11)
+    _, ws17, p17 = mcpt.debug_prep_bench(s, X, N, u, variant=17, iters=1)
+    _, ws18, p18 = mcpt.debug_prep_bench(s, X, N, u, variant=18, iters=1)
+    assert (ws17 > 0).sum() >= 2000
+    assert np.array_equal(ws17.view(np.int64), ws18.view(np.int64))
+    assert np.array_equal(p17, p18)
