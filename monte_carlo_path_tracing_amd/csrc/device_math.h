@@ -458,6 +458,24 @@ __device__ inline double sliver_term(double num, double den) {
     const double x2 = fmax(2.0 * (4.0 - den), 1e-300);
     return x2 * __builtin_amdgcn_rsq(x2) * __builtin_amdgcn_rcp(num) * 1.01;
 }
+// Survival of one light triangle under the reference's literal chain (light_tri_stage == 0) decided
+// without it where that is safe: 0 = culled (the exact cheap stages), 1 = survives, -1 = undecided (run
+// the literal chain).  From the rsqrt unit vectors (~1e-13 from the literal's sqrt / division ones):
+//  * every edge 1 - cos > 1e-9, so the literal's clamped cosines are < 1 (no edge-length cull);
+//  * 4 - den <= 1000 num (not a sliver): the spherical law of sines gives 1 / sin(alpha) = sin b sin c / num
+//    <= (1 - cos b) + (1 - cos c) <= 4 - den (sin^2 <= 2 (1 - cos)), so every vertex angle has
+//    sin >= 1e-3 -- far from the 1e-8 angle culls, and acos is well conditioned (the literal angles are
+//    within ~1e-12 of the true ones);
+//  * num > 1e-9 max(den, 0), i.e. tan(sA / 2) > 1e-9: the literal sA = alpha + beta + gamma - pi is far
+//    above its rounding, so sA >= 0 and w = sA sum L >= 0 is finite.
+__device__ inline int literal_survival_quick(d3 p0, d3 p1, d3 p2, d3 nl, d3 x1, d3 n) {
+    if (light_cheap_stage(p0, p1, p2, nl, x1, n) != 0) return 0;
+    const d3 A = funit(sub(p0, x1)), B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
+    const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
+    const double num = fabs(fdot(A, fcross(B, C))), den = 1.0 + ab + bc + ca;
+    const bool clear = fmax(ab, fmax(bc, ca)) < 1.0 - 1e-9 && 4.0 - den <= 1000.0 * num && num > 1e-9 * fmax(den, 0.0);
+    return clear ? 1 : -1;
+}
 __device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, double* w_out) {
     bool ok;
     *w_out = light_weight_bf(p0, p1, p2, lsum2, x1, &ok);

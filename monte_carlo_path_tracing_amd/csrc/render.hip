@@ -2671,16 +2671,18 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
                 }
             }
             const int node = n0 + 4 * s + g;
+            bool amb = false;
             if (gl == 0 && node < n) {
                 wsum_out[node] = wsum[s];
                 pick_out[node] = pick;
                 if (C.exact) {  // exact pick: the band stored by the cache build + this sum's rounding
                     const double band = (double)__int_as_float(inf[s].w) + band_round(inf[s].y, wsum[s]);
-                    if (!(pick_slack(margin, wsum[s]) > band)) {
-                        const int q = atomicAdd(C.exact, 1);
-                        C.exact[kExactHead + q] = C.exact_off + node;
-                    }
+                    amb = !(pick_slack(margin, wsum[s]) > band);
                 }
+            }
+            if (C.exact) {  // one list atomic per wave (C.exact is launch-uniform)
+                const int q = wave_append(reinterpret_cast<unsigned*>(C.exact), amb);
+                if (amb) C.exact[kExactHead + q] = C.exact_off + node;
             }
         }
         cached += (unsigned long long)min(kR, n - n0);
@@ -3019,7 +3021,10 @@ __device__ inline double state_light_pdf(const DScene& S, int li, const double* 
     if (li < 0 || fabs(st[6]) < MCPT_EPS) return 0.0;
     const d3 x = mk3(st[0], st[1], st[2]), N = mk3(st[3], st[4], st[5]);
     const PrepLight L = load_light(S, li);
-    if (light_tri_eval(L.p0, L.p1, L.p2, L.nl, S.light_sum[li], x, N, nullptr)) return S.light_sum[li] / st[6];
+    // the literal chain only where the quick test cannot decide (slivers, near-degenerate triangles)
+    const int q = literal_survival_quick(L.p0, L.p1, L.p2, L.nl, x, N);
+    if (q > 0 || (q < 0 && light_tri_eval(L.p0, L.p1, L.p2, L.nl, S.light_sum[li], x, N, nullptr)))
+        return S.light_sum[li] / st[6];
     return 0.0;
 }
 
@@ -3460,11 +3465,14 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
     const int pixel = cur.pixel[ii], sample = cur.sample[ii];
     const uint64_t node = cur.node[ii];
     const size_t o1 = ii, o2 = (size_t)A.cap + ii, ol = 2 * (size_t)A.cap + ii;
-    const bool c1 = active && (fl & 1) && A.hf[o1] >= 0;
-    const bool c2 = active && (fl & 2) && A.hf[o2] >= 0;
+    // the three hit slots are loaded with the flags, not after them (a slot of a set the node did not
+    // trace holds a stale value, which the flag tests below mask): one dependent hop less
+    const int h1 = A.hf[o1], h2 = A.hf[o2], hl = A.hf[ol];
+    const bool c1 = active && (fl & 1) && h1 >= 0;
+    const bool c2 = active && (fl & 2) && h2 >= 0;
     const d3 p = ld3(cur.p, cur.cap, ii);
     const d3 N = ld3(cur.n, cur.cap, ii);
-    const int li = (c2 && (fl & 4) && A.hf[ol] >= 0) ? S.tri_light[A.hf[ol]] : -1;
+    const int li = (c2 && (fl & 4) && hl >= 0) ? S.tri_light[hl] : -1;
     const double own[7] = {p.x, p.y, p.z, N.x, N.y, N.z, cur.wsum[ii]};
     const d3 d1 = ld3(A.d1, A.cap, ii);
     const d3 d2 = ld3(A.d2, A.cap, ii);
@@ -3474,11 +3482,11 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
     if (!kStale) {  // fresh light pdf (this node's own prep) and forward throughputs
         d3 tp2 = mk3(0, 0, 0);
         if (c2) tp2 = mul(w2, cosb / (pdf + state_light_pdf(S, li, own)) / MCPT_P_RR);
-        node_entry(P, c1, c1 ? A.hf[o1] : -1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), w1, pixel, sample, 2 * node, nxt);
-        node_entry(P, c2, c2 ? A.hf[o2] : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), tp2, pixel, sample,
+        node_entry(P, c1, c1 ? h1 : -1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), w1, pixel, sample, 2 * node, nxt);
+        node_entry(P, c2, c2 ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), tp2, pixel, sample,
                    2 * node + 1, nxt);
     } else {
-        const int f1 = c1 ? A.hf[o1] : -1, f2 = c2 ? A.hf[o2] : -1;
+        const int f1 = c1 ? h1 : -1, f2 = c2 ? h2 : -1;
         const Entry e1 = entry_eval(P, c1, f1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), pixel, sample, 2 * node);
         const Entry e2 = entry_eval(P, c2, f2, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), pixel, sample, 2 * node + 1);
         const bool lsh = e1.kind == 2, bsh = e2.kind == 2;
