@@ -140,7 +140,19 @@ def main():
         json.dump(summary, f, indent=1, sort_keys=True)
     latest = pmc_latest(a.tag, summary)
     if latest["kernels"]:
-        with open(os.path.join(out, "pmc_latest.json"), "w") as f:
+        # merged into the existing file (one entry per kernel, the newest pass wins), so the summaries of
+        # several configurations (C3, C2's k_extend_brdf, ...) can all be present; sources are listed
+        path = os.path.join(out, "pmc_latest.json")
+        try:
+            with open(path) as f:
+                old = json.load(f)
+        except (OSError, ValueError):
+            old = {}
+        kernels = dict(old.get("kernels", {}))
+        kernels.update(latest["kernels"])
+        srcs = [x for x in old.get("sources", [old["source"]] if "source" in old else []) if x != latest["source"]]
+        latest = {"source": latest["source"], "sources": srcs + [latest["source"]], "kernels": kernels}
+        with open(path, "w") as f:
             json.dump(latest, f, indent=1, sort_keys=True)
     print(json.dumps({k: summary[k] for k in summary if k != "sq"}, indent=1)[:3000])
 
