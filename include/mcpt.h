@@ -179,7 +179,10 @@ typedef struct {
     uint64_t tri_tests;     /* the render sets MCPT_DEBUG_COUNT_TRAVERSAL (mcpt_debug.h), else 0 */
     uint64_t prep_exact_nodes; /* light preps whose pick lay within the rounding band of a cumulative-weight
                                 * boundary and were redone with the reference's literal formulas and
-                                * summation order (Mylight.cpp:335-438), so the pick is the reference's */
+                                * summation order (Mylight.cpp:335-438), so the pick is the reference's.
+                                * The band's constants are calibrated, not a proven bound (DESIGN.md
+                                * §4.3.3: tools/prep_error_study.py on the stand-in, margins x2.7-x38 on
+                                * the stress scenes of tests/test_exact_pick_stress.py) */
     double cache_build_seconds; /* device time building the per-pixel root-point cache (in prep_seconds) */
     uint64_t prep_band_nodes;   /* light preps whose slack the whole-table band bound could not clear and
                                  * that took the per-chunk band test (prep_exact_nodes of them failed it) */
