@@ -136,3 +136,17 @@ def test_cull_chunk_classes_change_no_candidate(scenes, name):
     assert (ws17 > 0).sum() >= 2000
     assert np.array_equal(ws17.view(np.int64), ws18.view(np.int64))
     assert np.array_equal(p17, p18)
+
+
+def test_cull_order_at_scale_changes_no_candidate():
+    """The cull's node order at the size of a real generation's share (10^6 nodes: ~500 blocks of the
+    order kernels, bucket counters under contention): prep variant 17 vs 18 bit-identical on the
+    stand-in (both sides of every facet, so every chunk class occurs)."""
+    from conftest import SCENE_OBJ, SCENE_XML
+    s = mcpt.Scene.load(SCENE_OBJ, SCENE_XML)
+    X, N, u = surface_points(po.Scene(SCENE_OBJ, SCENE_XML), 1 << 20, seed=17)
+    _, ws17, p17 = mcpt.debug_prep_bench(s, X, N, u, variant=17, iters=1)
+    _, ws18, p18 = mcpt.debug_prep_bench(s, X, N, u, variant=18, iters=1)
+    assert (ws17 > 0).sum() >= 100000
+    assert np.array_equal(ws17.view(np.int64), ws18.view(np.int64))
+    assert np.array_equal(p17, p18)
