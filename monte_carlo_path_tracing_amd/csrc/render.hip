@@ -607,9 +607,6 @@ struct Queue {
 #ifndef MCPT_EXACT_PICK
 #define MCPT_EXACT_PICK 1
 #endif
-#ifndef MCPT_PERSIST_QUANT
-#define MCPT_PERSIST_QUANT 1
-#endif
 #ifndef MCPT_WORKING_SET
 #define MCPT_WORKING_SET (48 << 20)  // default wavefront working set (nodes per generation)
 #endif
@@ -2088,11 +2085,8 @@ struct CullOrder {
     unsigned* count = nullptr;
 };
 
-// skip the list append of an all-zero candidate word by a scalar branch (same-box A/B:
-// 410.6 / 425.0 / 425.1 vs 423.8 / 415.8 / 421.9 Msamples/s, profiles/round2b_ab_zero_words.txt)
-#ifndef MCPT_SKIP_ZERO_WORDS
-#define MCPT_SKIP_ZERO_WORDS 1
-#endif
+// an all-zero candidate word skips its list append by a scalar branch (same-box A/B: 410.6 / 425.0 /
+// 425.1 vs 423.8 / 415.8 / 421.9 Msamples/s, profiles/round2b_ab_zero_words.txt)
 constexpr int kMaskBatch = kMaskLine;  // candidate words per batch of scalar loads (k_prep_pk2): one line
 template <int kMinWavesPerSimd, bool kBuild, bool kMaskIn = false, bool kF32 = false>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, uint64_t seed, int n, const double* __restrict__ qp,
@@ -2140,7 +2134,6 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             // kMaskBatch words each, the row zero-padded to whole lines) put them straight into SGPRs,
             // so a word costs 3 VALU (2 v_mbcnt + 1 v_lshl_add) + 1 v_add for the index.
             const unsigned lds_lst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lst);  // LDS offset (low half of the flat address)
-            unsigned idx = (unsigned)lane;
             for (int c0 = 0; c0 < nchunks; c0 += kMaskBatch) {
                 uint64_t mw[kMaskBatch];
 #pragma unroll
@@ -2148,18 +2141,11 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
 #pragma unroll
                 for (int q = 0; q < kMaskBatch; q++) {
                     const uint64_t m = mw[q];
-                    (void)idx;
-#if MCPT_SKIP_ZERO_WORDS
                     if (m != 0) {  // wave-uniform (SGPR word): an empty chunk costs no VALU
                         append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_lst + 2u * (unsigned)ncand,
                                       (unsigned)lane + 64u * (unsigned)(c0 + q));
                         ncand += __popcll(m);
                     }
-#else
-                    append_masked(m, (unsigned)m, (unsigned)(m >> 32), lds_lst + 2u * (unsigned)ncand, idx);
-                    ncand += __popcll(m);
-                    idx += 64;
-#endif
                 }
             }
         } else {
@@ -2484,9 +2470,6 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
 #ifndef MCPT_PICK_SLOTS
 #define MCPT_PICK_SLOTS 4  // roots per wave = 4 x slots (A/B: 2 slots at 7 waves 476.8-478.2, 4 slots at 4 waves 480.2-480.5)
 #endif
-#ifndef MCPT_PICK_PREFETCH
-#define MCPT_PICK_PREFETCH 1
-#endif
 #ifndef MCPT_PICK_GROUPS
 #define MCPT_PICK_GROUPS 1  // 0: k_prep_pick (wave per root) for every table size (A/B)
 #endif
@@ -2510,30 +2493,8 @@ __device__ inline T sel4v(T v0, T v1, T v2, T v3, int k) {
 }
 template <class T>
 __device__ inline T sel4(const T (&v)[4], int k) { return sel4v(v[0], v[1], v[2], v[3], k); }
-// first set bit of the group's 64 entries (entry 16 k + l is bit l of field g of m[k]); -1 if none
-__device__ inline int group_first(const uint64_t (&m)[4], int g) {
-    int r = -1;
-#pragma unroll
-    for (int k = 3; k >= 0; k--) {
-        const unsigned f = (unsigned)(m[k] >> (16 * g)) & 0xffffu;
-        r = f ? 16 * k + __ffs(f) - 1 : r;
-    }
-    return r;
-}
-__device__ inline int group_last(const uint64_t (&m)[4], int g) {
-    int r = -1;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const unsigned f = (unsigned)(m[k] >> (16 * g)) & 0xffffu;
-        r = f ? 16 * k + 31 - __clz(f) : r;
-    }
-    return r;
-}
-// the same first / last searches by a 16-lane row reduction (DPP row_ror butterflies: four VALU each)
-// on per-lane candidate indices instead of decoding the ballot masks lane by lane
-#ifndef MCPT_PICK_DPP
-#define MCPT_PICK_DPP 1
-#endif
+// first / last searches within a 16-lane group by a row reduction (DPP row_ror butterflies: four VALU
+// each) on per-lane candidate indices, instead of decoding ballot masks lane by lane (round 3, +1.1%)
 __device__ inline unsigned row_min_u32(unsigned v) {
     v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
     v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false));  // row_ror:4
@@ -2558,7 +2519,7 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
     const int nq = (nchunks + 15) >> 4;  // row entries per lane (<= 4)
     unsigned long long cached = 0;
     // lane r < kR: root n0 + r (coalesced queue loads), fetched one iteration ahead so that the queue
-    // hop overlaps the previous roots' cache hops (MCPT_PICK_PREFETCH)
+    // hop overlaps the previous roots' cache hops (round 3: +0.6%)
     int f_px = 0, f_smp = 0;
     uint64_t f_nid = 0;
     auto fetch = [&](int m0) {
@@ -2567,12 +2528,11 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
         f_smp = qsample[node];
         f_nid = qnode[node];
     };
-    if (MCPT_PICK_PREFETCH && gw * kR < n) fetch(gw * kR);
+    if (gw * kR < n) fetch(gw * kR);
     for (int n0 = gw * kR; n0 < n; n0 += waves * kR) {
-        if (!MCPT_PICK_PREFETCH) fetch(n0);
         const int pxl = f_px;
         const double ul = counter_u(counter_key(seed, (uint64_t)pxl, (uint64_t)f_smp, f_nid), 1);  // dim 1
-        if (MCPT_PICK_PREFETCH && n0 + waves * kR < n) fetch(n0 + waves * kR);
+        if (n0 + waves * kR < n) fetch(n0 + waves * kR);
         // slot s: group g takes root 4 s + g; its row of batch totals (inclusive scan) and info
         int px[kPickSlots];
         int4 inf[kPickSlots];
@@ -2595,19 +2555,13 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
             wsum[s] = nb > 0 ? W : 0.0;
             const bool valid = !(fabs(wsum[s]) < MCPT_EPS);
             target[s] = bperm_f64(ul, 4 * s + g) * wsum[s];
-            if (MCPT_PICK_DPP) {
+            {
                 unsigned c = 64;
 #pragma unroll
                 for (int k = 3; k >= 0; k--)
                     c = valid && 16 * k + gl < nb && bv[s][k] >= target[s] && bv[s][k] > 0.0 ? 16 * k + gl : c;
                 c = row_min_u32(c);
                 kb[s] = c < 64 ? (int)c : -1;
-            } else {
-                uint64_t m[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    m[k] = __ballot(valid && 16 * k + gl < nb && bv[s][k] >= target[s] && bv[s][k] > 0.0);
-                kb[s] = group_first(m, g);
             }
             const int lb = max(kb[s] - 1, 0);
             const double b = bperm_f64(sel4(bv[s], lb >> 4), g0 + (lb & 15));
@@ -2629,7 +2583,7 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
 #pragma unroll
         for (int s = 0; s < kPickSlots; s++) {
             int pl;
-            if (MCPT_PICK_DPP) {
+            {
                 unsigned cf = 64;
                 int cl = -1;
 #pragma unroll
@@ -2641,16 +2595,6 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
                 cf = row_min_u32(cf);
                 const int lastv = row_max_i32(cl);  // every lane of the row takes part in the DPP steps
                 pl = cf < 64 ? (int)cf : lastv;
-            } else {
-                uint64_t cm[4], om[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const bool ok = !signbit(wc[s][k]);
-                    cm[k] = __ballot(ok && (base[s] + fabs(wc[s][k]) >= target[s]));
-                    om[k] = __ballot(ok);
-                }
-                pl = group_first(cm, g);
-                if (pl < 0) pl = group_last(om, g);
             }
             double margin = INFINITY;
             int pick = -1;
@@ -3032,9 +2976,6 @@ __device__ inline double state_light_pdf(const DScene& S, int li, const double* 
 // state st -- to its parent slot; the parent goes to ready list rp once both children have (one
 // append per wave: a single counter word saturates at ~88 atomics/us, MI355X_MICROARCH.md); a root
 // adds L / spp to its pixel.  Every lane of the wave that reaches the call must make it.
-#ifndef MCPT_SPLAT_ZERO_SKIP
-#define MCPT_SPLAT_ZERO_SKIP 1
-#endif
 __device__ inline void mis_report(const Params& P, const Slots& T, bool act, int par, int pixel, d3 L, const double* st,
                                   int rp) {
     bool ready = false;
@@ -3043,9 +2984,9 @@ __device__ inline void mis_report(const Params& P, const Slots& T, bool act, int
         // a zero component adds nothing (the framebuffer is never -0), so its device-scope fp64 atomic
         // is skipped -- the same image bit for bit
         double* px = P.fb + 3 * (size_t)pixel;
-        if (!MCPT_SPLAT_ZERO_SKIP || L.x != 0.0) unsafeAtomicAdd(px + 0, L.x * P.inv_spp);
-        if (!MCPT_SPLAT_ZERO_SKIP || L.y != 0.0) unsafeAtomicAdd(px + 1, L.y * P.inv_spp);
-        if (!MCPT_SPLAT_ZERO_SKIP || L.z != 0.0) unsafeAtomicAdd(px + 2, L.z * P.inv_spp);
+        if (L.x != 0.0) unsafeAtomicAdd(px + 0, L.x * P.inv_spp);
+        if (L.y != 0.0) unsafeAtomicAdd(px + 1, L.y * P.inv_spp);
+        if (L.z != 0.0) unsafeAtomicAdd(px + 2, L.z * P.inv_spp);
     } else if (act) {
         ps = par >> 2;
         const int role = (par >> 1) & 1;
@@ -3367,11 +3308,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
         if (__ballot(busy) == 0) break;  // pool exhausted and no ray in flight
         // one round of trace4_ww's outer loop on every lane in flight
         if (busy) {
-#if MCPT_PERSIST_QUANT
             const BvhNode4Q* __restrict__ nodes = set == 2 ? S.lbvh4q : S.bvh4q;
-#else
-            const BvhNode4* __restrict__ nodes = set == 2 ? S.lbvh4 : S.bvh4;
-#endif
             const float4* __restrict__ leafv = set == 2 ? S.lleaf_v : S.leaf_v;
             const float inv3[3] = {ix, iy, iz}, oi3[3] = {oix, oiy, oiz};
             const bool neg3[3] = {ix < 0, iy < 0, iz < 0};
@@ -3379,19 +3316,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
                 if (kCount) ++visits;
                 float tn[3][4], tf[3][4];  // near / far slab distances per axis and child
                 int chs[4];
-#if MCPT_PERSIST_QUANT
                 node_tplanes(nodes + node, inv3, oi3, neg3, tn, tf, chs);
-#else
-                float lo[3][4], hi[3][4];
-                load_node(nodes + node, lo, hi, chs);
-#pragma unroll
-                for (int a = 0; a < 3; a++)
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const float t0 = fmaf(lo[a][k], inv3[a], -oi3[a]), t1 = fmaf(hi[a][k], inv3[a], -oi3[a]);
-                        tn[a][k] = neg3[a] ? t1 : t0, tf[a][k] = neg3[a] ? t0 : t1;
-                    }
-#endif
                 float t[4];
                 int code[4];
 #pragma unroll
