@@ -4,8 +4,9 @@
 // The recursion is flattened into generations of a persistent SoA node queue in HBM:
 //
 //   k_primary          lane per pixel : camera ray (main.cpp:547-564) + closest hit, once per call
-//   k_roots            lane per root  : node-entry checks of a camera sample's root (back-face,
-//                                       emitter, RR) -> queue (path regeneration)
+//   k_root_table       lane per pixel : a root's point, normal, wo and kind, once per call
+//   k_roots_t          8 roots per lane : a camera sample's root from that table (RR) -> queue
+//                                       (path regeneration)
 //   k_root_points      lane per pixel : root shading points for the per-pixel root-point cache
 //   k_prep_cull_lanes  lane per node  : light prep phase A -- the light-side and tangent-plane culls
 //                                       of Mylight.cpp:340-357 against every light (light table
@@ -795,14 +796,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_primary(DScene S, CamFrame cam,
 // hit) is the same for every sample of its pixel except the Russian roulette draw, so the point, normal
 // and wo (9 doubles) and the kind (-2 nothing: miss or back face, -1 shading, >= 0 emitter li) are
 // computed once per pixel with the same functions, and k_roots_t only draws RR and appends.
-// MCPT_ROOT_TABLE: roots from the per-pixel table by k_roots_t (kRootsPT roots per thread, one queue
-// atomic per 2 048 roots).  The table alone in k_roots (one atomic per 256 roots) changed nothing
-// (k_roots 111-112 ms per profile run, profiles/round3_ab_acos_dpp_roottab.txt): k_roots was bound by
-// the queue counter's atomic rate; with k_roots_t 112 -> 55 ms, MIS +1.7% same-box
-// (profiles/round3_ab_roots_batched.txt).  0: k_roots (node_entry per root).
-#ifndef MCPT_ROOT_TABLE
-#define MCPT_ROOT_TABLE 1
-#endif
+// Roots from the per-pixel table by k_roots_t (kRootsPT roots per thread, one queue atomic per 2 048
+// roots).  The table alone in round 3's k_roots (node_entry per root, one atomic per 256 roots) changed
+// nothing (111-112 ms per profile run, profiles/round3_ab_acos_dpp_roottab.txt): it was bound by the
+// queue counter's atomic rate; with k_roots_t 112 -> 55 ms, MIS +1.7% same-box
+// (profiles/round3_ab_roots_batched.txt).
 struct RootTab {
     double* pnw;  // [npx][9]: p, N, wo
     int* kind;    // [npx]
@@ -923,27 +921,6 @@ __global__ __launch_bounds__(256) void k_roots_t(Params P, const int* __restrict
         q.node[slot] = 1;
         q.par[slot] = -1;
     }
-}
-
-__global__ __launch_bounds__(256) void k_roots(Params P, CamFrame cam, const int* hit_f, const double* hit_tbg,
-                                               int s0, long long rbase, int nroots, Queue q, int group, int nsamp) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    const int npx = cam.W * cam.H;
-    bool active = r < nroots;
-    int pixel = 0, sample = 0, f = -1;
-    double beta = 0, gamma = 0;
-    d3 wo = mk3(0, 0, 0);
-    if (active) {
-        root_of(rbase + r, npx, s0, group, nsamp, &pixel, &sample);
-        f = hit_f[pixel];
-        active = f >= 0;
-        if (active) {
-            beta = hit_tbg[3 * pixel + 1];
-            gamma = hit_tbg[3 * pixel + 2];
-            wo = mul(cam_dir(cam, pixel / cam.W, pixel % cam.W), -1);
-        }
-    }
-    node_entry(P, active, f, beta, gamma, wo, mk3(1, 1, 1), pixel, sample, 1, q);
 }
 
 // moves nodes [sb, sb + m) of src to [db, db + m) of dst (every field a generation carries into the
@@ -1779,10 +1756,6 @@ static_assert(kCullBurst % 2 == 0 && kMaskLine % kCullBurst == 0, "cull burst");
 #define MCPT_CULL_SPLITS 6
 #endif
 inline int cull_splits(int nchunks) { return std::max(1, std::min(MCPT_CULL_SPLITS, nchunks / 4)); }
-// chunk classes in the cull (chunk_class) with the nodes ordered by their class pattern (k_cull_classify)
-#ifndef MCPT_CULL_CLASSES
-#define MCPT_CULL_CLASSES 1
-#endif
 // Phase A with a lane per shading node and the light table in scalar registers: each light pair
 // (LightPair, two s_load_dwordx16) is read once per 64 nodes from the scalar cache, and the two
 // cheap stages of both lights run as 13 v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 with one
@@ -1865,7 +1838,7 @@ __device__ inline uint64_t cull_chunk(const DScene& S, const CullLane& cl, const
     // every lane BELOW -- the word is 0 (not in the counting instance, which counts the light-side culls);
     // every lane ABOVE -- the light-side test alone.  Inactive lanes agree with anything.
     bool above = false;
-    if (MCPT_CULL_CLASSES && classes) {
+    if (classes) {
         const unsigned cls = chunk_class(cl.nxx[0], cl.nyy[0], cl.nzz[0], cl.ncn[0], err, S.chunk_sph[c]);
         if (!kCountC1 && (__ballot(cls != kChunkBelow) & actm) == 0) return 0ull;
         above = (__ballot(cls != kChunkAbove) & actm) == 0;
@@ -4324,7 +4297,7 @@ hipError_t launch_prep(int variant, const DScene& d, uint64_t seed, int n, const
                            cache.exact_counts, cache.maybe);
     } else if (variant == 17) {  // phase A lane per node (light table in scalar registers), then phase B
         const int* order = nullptr;
-        if (MCPT_CULL_CLASSES && co.order && ordered) {  // the nodes bucketed by their chunk-class pattern
+        if (co.order && ordered) {  // the nodes bucketed by their chunk-class pattern
             e = hipMemsetAsync(co.count, 0, 8 * kCullBuckets, st);
             if (e != hipSuccess) return e;
             const dim3 go((n + 256 * kCullPer - 1) / (256 * kCullPer));
@@ -4468,7 +4441,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int cap = (int)std::min<long long>((long long)qf * target + 1024, (1ll << 30));
     int rc;
     if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) ||
-        (MCPT_ROOT_TABLE && ((rc = ensure(D.root_pnw, 72ull * npx)) || (rc = ensure(D.root_kind, 4ull * npx)))) || (rc = ensure(D.stats, 128)) ||
+        (rc = ensure(D.root_pnw, 72ull * npx)) || (rc = ensure(D.root_kind, 4ull * npx)) || (rc = ensure(D.stats, 128)) ||
         (rc = ensure(D.work, 256)))
         return rc;
     Queue qa, qb;
@@ -4589,15 +4562,11 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     hipLaunchKernelGGL(grid ? k_primary<true> : k_primary<false>, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock),
                        0, st, D.d, cf, (int*)D.hit_f.p, (double*)D.hit_tbg.p);
     HIP_OK(hipGetLastError());
-    RootTab rtab{};
-    if (MCPT_ROOT_TABLE) {
-        rtab.pnw = (double*)D.root_pnw.p;
-        rtab.kind = (int*)D.root_kind.p;
-        hipLaunchKernelGGL(k_root_table, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
-                           (const double*)D.hit_tbg.p, rtab);
-        HIP_OK(hipGetLastError());
-        if (fused) P.root_pnw = rtab.pnw;  // BRDF-only: lite root entries (Params::root_pnw)
-    }
+    RootTab rtab{(double*)D.root_pnw.p, (int*)D.root_kind.p};
+    hipLaunchKernelGGL(k_root_table, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
+                       (const double*)D.hit_tbg.p, rtab);
+    HIP_OK(hipGetLastError());
+    if (fused) P.root_pnw = rtab.pnw;  // BRDF-only: lite root entries (Params::root_pnw)
     if (pc.use || small_use) {
         HIP_OK(hipMemsetAsync(qb.count, 0, 4, st));
         hipLaunchKernelGGL(k_root_points, dim3((npx + 255) / 256), dim3(256), 0, st, D.d, cf, (const int*)D.hit_f.p,
@@ -4714,13 +4683,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const unsigned n_children = n;  // [0, n_children) children, [n_children, n) fresh roots
         if (rnext < R && n < (unsigned)fill) {  // refill with roots (appended through node_entry)
             const int m = (int)std::min<long long>((long long)fill - n, R - rnext);
-            if (rtab.pnw)
-                hipLaunchKernelGGL(k_roots_t, dim3((m + 256 * kRootsPT - 1) / (256 * kRootsPT)), dim3(256), 0, st, P,
-                                   (const int*)D.hit_f.p, npx, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab,
-                                   P.root_pnw ? 1 : 0);
-            else
-                hipLaunchKernelGGL(k_roots, dim3((m + 255) / 256), dim3(256), 0, st, P, cf, (const int*)D.hit_f.p,
-                                   (const double*)D.hit_tbg.p, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0);
+            hipLaunchKernelGGL(k_roots_t, dim3((m + 256 * kRootsPT - 1) / (256 * kRootsPT)), dim3(256), 0, st, P,
+                               (const int*)D.hit_f.p, npx, s0, rnext, m, *cur, std::max(1, nminor), s1 - s0, rtab,
+                               P.root_pnw ? 1 : 0);
             HIP_OK(hipGetLastError());
             rnext += m;
             if ((rc = read_count(&n))) return rc;
