@@ -251,6 +251,20 @@ def test_render_parity_full_size_pixel_subset(scene, oscene, mode, spp):
     assert g.mean() > 0
 
 
+def test_c3_full_frame_vs_oracle(scene, oscene):
+    """C3's frame (800x600, MIS with the reference's stale light pdf) in full, every pixel against the
+    oracle at the same seed: 2 spp (960 000 camera samples, the same counter-RNG samples on both sides;
+    the oracle on 16 host threads) -- relative L2 and every pixel <= 1e-3 (north star)."""
+    cam = mcpt.Camera.reference(800, 600)
+    g, st = mcpt.render(scene, cam, 2, mode="mis", seed=SEED)
+    c, _ = oscene.render(po.reference_camera(800, 600), po.MODE_MIS, SEED, 2, nthreads=16)
+    err, mx = rel_l2(g, c), max_px_rel(g, c)
+    print("mis 800x600x2 full frame: rel L2 %.3e, max per-pixel %.3e; %d shading nodes, %d exact preps" % (
+        err, mx, st.shading_nodes, st.prep_exact_nodes))
+    assert np.isfinite(g).all() and (g >= 0).all() and c.sum() > 0
+    assert err <= L2_TOL and mx <= L2_TOL
+
+
 @pytest.mark.parametrize("W,H,spp", [(80, 60, 8), (800, 600, 16)])
 def test_mis_fresh_pdf_flag_vs_oracle(scene, oscene, W, H, spp):
     """MCPT_RENDER_FRESH_PDF (the node's own light pdf, not the reference's stale sampler state,
