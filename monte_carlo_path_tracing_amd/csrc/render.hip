@@ -3059,12 +3059,42 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
 // kCount: counts node visits / triangle tests into cnt[0] / cnt[1] (statistics replay only)
 template <bool kGrid, bool kCount = false>
 __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, Queue cur, int n, Aux A, int first_set,
-                                                          unsigned long long* cnt = nullptr, int seeded = 0) {
+                                                          unsigned long long* cnt = nullptr, int seeded = 0,
+                                                          int compact = 0) {
     constexpr int kTop = kGrid ? 0 : kRayTop;
     __shared__ int stack[kRayTopLds * kRayBlock];
     __shared__ BvhNode4 top[kTop > 0 ? kTop : 1];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int set = blockIdx.y + first_set;
+    // compact (shade() modes): the block's nodes regrouped stably -- the nodes that trace this set
+    // first, in their order, the others in the block's last waves, which then exit at once.  shade-area
+    // +6% (its light rays are traced by a minority of nodes); MIS, whose three sets are traced densely or
+    // by half of the nodes, ran 3.5% slower traversal with it (profiles/round4_ab_cull_classes.txt)
+    __shared__ int s_wc[kRayBlock / 64][2], s_off[kRayBlock / 64][2], s_ord[kRayBlock];
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (compact) {  // uniform
+        const int i0 = i;
+        const int key = i0 < n && (A.flags[i0] & (1 << set)) ? 0 : 1;
+        const int w = threadIdx.x >> 6;
+        const uint64_t m0 = __ballot(key == 0);
+        const int rank = key == 0 ? lane_rank(m0) : lane_rank(~m0);
+        if (lane_id() == 0) {
+            s_wc[w][0] = __popcll(m0);
+            s_wc[w][1] = 64 - __popcll(m0);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // offsets: traced nodes first, waves in order within a key
+            int t = 0;
+            for (int b = 0; b < 2; b++)
+                for (int ww = 0; ww < kRayBlock / 64; ww++) {
+                    s_off[ww][b] = t;
+                    t += s_wc[ww][b];
+                }
+        }
+        __syncthreads();
+        s_ord[s_off[w][key] + rank] = i0;
+        __syncthreads();
+        i = s_ord[threadIdx.x];
+    }
     if (kTop > 0) {  // the tree's top levels into LDS (uniform per block: blockIdx.y picks the tree)
         const BvhNode4* src = set == 2 ? S.lbvh4 : S.bvh4;
         const int cnt4 = min(kTop, set == 2 ? S.nlbvh4 : S.nbvh4) * (int)(sizeof(BvhNode4) / sizeof(float4));
@@ -4795,7 +4825,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                                    first_set, nsets, pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
         } else {
             hipLaunchKernelGGL(K_MIS_RAYS, dim3((ni + kRayBlock - 1) / kRayBlock, nsets), dim3(kRayBlock), 0, st, D.d,
-                               *cur, ni, aux, first_set, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
+                               *cur, ni, aux, first_set, tcnt, MCPT_SEED_LIGHT ? seeded : 0,
+                               o->mode == MCPT_MODE_MIS ? 0 : 1);
         }
     };
         // trace_seconds: HIP events around the traversal kernel (k_mis_rays; BRDF-only: k_extend_brdf)
