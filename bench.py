@@ -332,6 +332,9 @@ def main():
                 if (k == n or (tail and k.startswith(head) and k.endswith(tail))) and v.get("valu_issue_frac") is not None:
                     out[k] = v["valu_issue_frac"]
         return out
+    def pmc_src(*names):  # the summaries the matched kernels' PMC figures came from
+        srcs = sorted({pk[k].get("source") or pmc.get("source") for n in names for k in busy(n)})
+        return "; ".join(s for s in srcs if s) or None
     dev_s = max(totals.get("seconds", 0.0), 1e-12)
     # ---- roofline of the light prep (rank 0's launches; HIP events on its stream) ----
     roof_prep = None
@@ -341,6 +344,7 @@ def main():
                                                        "light_evals_candidates"))
         launches = max(totals.get("prep_launches", 0), 1)
         c2 = ev_tot - c1 - cand
+        prep_k = ("k_prep_cull_lanes<false>", "k_prep_pk2<*, false, true, %s>" % ("true" if args.precision == "fp32" else "false"))
         flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
         t_launch = prep_s / launches
         achieved = flops / launches / t_launch / 1e12
@@ -360,9 +364,8 @@ def main():
             "bound": "valu_fp32" if fp32 else "valu_fp64", "kernel": "k_prep_cull_lanes+k_prep_pk2",
             "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "traffic_source": tsrc,
-            "valu_issue_frac": busy("k_prep_cull_lanes<false>",
-                              "k_prep_pk2<*, false, true, %s>" % ("true" if args.precision == "fp32" else "false")),
-            "valu_issue_frac_source": pmc.get("source"),
+            "valu_issue_frac": busy(*prep_k),
+            "valu_issue_frac_source": pmc_src(*prep_k),
             "hbm_frac_algorithmic": round(alg_gbs / HBM_PEAK_GBS, 5),
             "hbm_frac_measured": round(traffic / t_launch / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
             "avg_launch_ms": round(t_launch * 1e3, 3), "launches": launches, "flop_per_launch": flops / launches,
@@ -400,8 +403,8 @@ def main():
             "frac": round(max(v_frac, h_frac), 4), "valu_frac": round(v_frac, 4), "mem_model_frac": round(h_frac, 4),
             "accel_bytes": accel, "bytes_per_node_visit": BYTES_NODE_VISIT[kname], "structure_level": level,
             "hbm_model_frac": hbm_model,
-            "traffic": hbm_meas, "traffic_source": ("PMC profile, not this run: %s" % pmc.get("source")) if hbm_meas else None,
-            "valu_issue_frac": busy(pk_name), "valu_issue_frac_source": pmc.get("source"),
+            "traffic": hbm_meas, "traffic_source": ("PMC profile, not this run: %s" % (pk.get(pk_name, {}).get("source") or pmc.get("source"))) if hbm_meas else None,
+            "valu_issue_frac": busy(pk_name), "valu_issue_frac_source": pmc_src(pk_name),
             "avg_launch_ms": round(t_launch * 1e3, 3), "launches": tr_n,
             "node_visits_per_ray": round(visits / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),
             "tri_tests_per_ray": round(tests / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),

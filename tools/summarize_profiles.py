@@ -148,10 +148,11 @@ def main():
                 old = json.load(f)
         except (OSError, ValueError):
             old = {}
-        kernels = dict(old.get("kernels", {}))
-        kernels.update(latest["kernels"])
-        srcs = [x for x in old.get("sources", [old["source"]] if "source" in old else []) if x != latest["source"]]
-        latest = {"source": latest["source"], "sources": srcs + [latest["source"]], "kernels": kernels}
+        # each kernel entry names the summary it came from (bench.py cites it per roofline)
+        kernels = {k: dict(v, source=v.get("source", old.get("source"))) for k, v in old.get("kernels", {}).items()}
+        kernels.update({k: dict(v, source=latest["source"]) for k, v in latest["kernels"].items()})
+        srcs = sorted({v["source"] for v in kernels.values() if v.get("source")})
+        latest = {"source": latest["source"], "sources": srcs, "kernels": kernels}
         with open(path, "w") as f:
             json.dump(latest, f, indent=1, sort_keys=True)
     print(json.dumps({k: summary[k] for k in summary if k != "sq"}, indent=1)[:3000])
