@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/sec (whole node) + per-pixel L2 vs CPU, Veach-MIS 800×600@1024spp"
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (spec); see DESIGN.md §roofline
 HBM_PEAK_GBS = 8000.0
+SMALL_NL = 64  # render.hip kSmallNL: light tables this small take the lane-per-node prep (k_prep_lane)
 # algorithmic fp64 operations of one light-triangle evaluation of Mylight.cpp:335-413 by the
 # stage at which it ends (+,-,*,/,sqrt,acos,fmin/fmax each 1)
 FLOPS_CULL_BACKFACE = 8
@@ -321,7 +322,10 @@ def main():
         dist.destroy_process_group()
         return
     pmc = load_json(os.path.join(ROOT, "profiles", "pmc_latest.json")) or {"kernels": {}}
-    pk = pmc["kernels"]
+    # the PMC figures of this workload when they were profiled (tools/summarize_profiles.py), else the
+    # headline's
+    wl = "brdf" if args.mode == "brdf" else ("cornell" if args.scene != "veach" else "c3")
+    pk = pmc.get("configs", {}).get(wl, {}).get("kernels") or pmc["kernels"]
     # bounded VALU figure from the SQ pass (tools/summarize_profiles.py): 4 x SQ_INSTS_VALU / (SIMDs x
     # cycles) -- the issue slots the kernel's VALU instructions hold (>= 4 cycles each for wave64)
     def busy(*names):  # a name ending in "*>" matches any launch bound: "k_prep_pk2<*, false, true, false>"
@@ -344,14 +348,22 @@ def main():
                                                        "light_evals_candidates"))
         launches = max(totals.get("prep_launches", 0), 1)
         c2 = ev_tot - c1 - cand
-        prep_k = ("k_prep_cull_lanes<false>", "k_prep_pk2<*, false, true, %s>" % ("true" if args.precision == "fp32" else "false"))
+        # the children's prep kernels: lane per node for small light tables (render.hip kSmallNL), else
+        # the cull + wave-per-node pk2
+        small = scene.nlights <= SMALL_NL
+        prep_k = (("k_prep_lane<*, false>",) if small else
+                  ("k_prep_cull_lanes<false>", "k_prep_pk2<*, false, true, %s>" % ("true" if args.precision == "fp32" else "false")))
         flops = c1 * FLOPS_CULL_BACKFACE + c2 * FLOPS_CULL_PLANE + cand * FLOPS_FULL
         t_launch = prep_s / launches
         achieved = flops / launches / t_launch / 1e12
         nodes = totals.get("prep_full_nodes", 0)
         traffic, tsrc = None, None
-        hb = load_json(os.path.join(ROOT, "profiles", "k_prep_hbm_bytes_per_node.json"))
-        if hb and hb.get("hbm_bytes_per_node") is not None:
+        hb = None if small else load_json(os.path.join(ROOT, "profiles", "k_prep_hbm_bytes_per_node.json"))
+        lane_k = [k for k in busy(*prep_k) if pk[k].get("hbm_bytes_per_dispatch")] if small else []
+        if lane_k:
+            traffic = pk[lane_k[0]]["hbm_bytes_per_dispatch"]
+            tsrc = "PMC profile, not this run: %s HBM bytes per dispatch (%s)" % (lane_k[0], pk[lane_k[0]].get("source"))
+        elif hb and hb.get("hbm_bytes_per_node") is not None:
             traffic = hb["hbm_bytes_per_node"] * nodes / launches
             tsrc = ("PMC profile, not this run: %.1f HBM B/node (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                     "profiles/k_prep_hbm_bytes_per_node.json) x this run's %.0f full-prep nodes per launch"
@@ -361,7 +373,7 @@ def main():
         fp32 = args.precision == "fp32"
         peak = FP32_VECTOR_PEAK_TFLOPS if fp32 else FP64_VECTOR_PEAK_TFLOPS
         roof_prep = {
-            "bound": "valu_fp32" if fp32 else "valu_fp64", "kernel": "k_prep_cull_lanes+k_prep_pk2",
+            "bound": "valu_fp32" if fp32 else "valu_fp64", "kernel": "k_prep_lane" if small else "k_prep_cull_lanes+k_prep_pk2",
             "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "traffic_source": tsrc,
             "valu_issue_frac": busy(*prep_k),

@@ -148,11 +148,20 @@ def main():
                 old = json.load(f)
         except (OSError, ValueError):
             old = {}
-        # each kernel entry names the summary it came from (bench.py cites it per roofline)
-        kernels = {k: dict(v, source=v.get("source", old.get("source"))) for k, v in old.get("kernels", {}).items()}
-        kernels.update({k: dict(v, source=latest["source"]) for k, v in latest["kernels"].items()})
-        srcs = sorted({v["source"] for v in kernels.values() if v.get("source")})
-        latest = {"source": latest["source"], "sources": srcs, "kernels": kernels}
+        # one entry per workload (the tag's suffix after the round name: "" = the headline C3, "brdf",
+        # "cornell", ...), each kernel naming the summary it came from; bench.py reads its workload's
+        # entries.  "kernels" is the headline's, with kernels only other workloads run added
+        wl = a.tag.split("_", 1)[1] if "_" in a.tag else "c3"
+        configs = dict(old.get("configs", {}))
+        configs[wl] = {"source": latest["source"],
+                       "kernels": {k: dict(v, source=latest["source"]) for k, v in latest["kernels"].items()}}
+        kernels = {}
+        for name in sorted(configs, key=lambda c: c != "c3"):
+            for k, v in configs[name]["kernels"].items():
+                kernels.setdefault(k, v)
+        srcs = sorted({c["source"] for c in configs.values()})
+        latest = {"source": configs.get("c3", configs[wl])["source"], "sources": srcs, "kernels": kernels,
+                  "configs": configs}
         with open(path, "w") as f:
             json.dump(latest, f, indent=1, sort_keys=True)
     print(json.dumps({k: summary[k] for k in summary if k != "sq"}, indent=1)[:3000])
