@@ -1093,14 +1093,18 @@ __global__ __launch_bounds__(256) void k_prep_lane(DScene S, uint64_t seed, int 
             if (count_out) count_out[i] = (int)surv;
         }
     }
-    if (stats) {
+    if (stats) {  // launch-uniform: one atomic per counter per workgroup (per-wave atomics on one word
+                  // serialise at ~88 per us)
+        __shared__ unsigned long long s_st[4][4];  // [counter][wave], 256 threads
+        const int wid = threadIdx.x >> 6;
         const unsigned long long ss = wave_sum_u64(surv), cs = wave_sum_u64(cand), c1s = wave_sum_u64(c1);
         const unsigned long long full = __popcll(__ballot(active));
-        if (lane_id() == 0) {
-            if (ss) atomicAdd(stats + 1, ss);
-            if (cs) atomicAdd(stats + 5, cs);
-            if (c1s) atomicAdd(stats + 6, c1s);
-            if (full) atomicAdd(stats + 7, full);
+        if (lane_id() == 0) s_st[0][wid] = ss, s_st[1][wid] = cs, s_st[2][wid] = c1s, s_st[3][wid] = full;
+        __syncthreads();
+        if (threadIdx.x < 4) {
+            const unsigned long long t = s_st[threadIdx.x][0] + s_st[threadIdx.x][1] + s_st[threadIdx.x][2] + s_st[threadIdx.x][3];
+            constexpr int kIdx[4] = {1, 5, 6, 7};
+            if (t) atomicAdd(stats + kIdx[threadIdx.x], t);
         }
     }
 }
@@ -4512,7 +4516,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const bool count_c1 = !(o->flags & MCPT_RENDER_NO_BACKFACE_STATS);
     const bool fp32 = (o->flags & MCPT_RENDER_PRECISION_FP32) != 0;
     double prep_ms = 0, trace_ms = 0, cache_ms = 0;
-    uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0, trace_launches = 0;
+    uint64_t gens = 0, prep_launches = 0, nodes_total = 0, cache_points = 0, trace_launches = 0, cached_roots = 0;
     // candidate words of the split light prep (k_prep_cull -> k_prep_pk2<mask-in>): per node and chunk
     uint64_t* masks = nullptr;
     CullOrder corder{};
@@ -4763,10 +4767,13 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
                 }
+                // the cached roots are counted here (nr is known): the pick kernels' per-wave atomics on
+                // one statistics word serialised at ~88 per us -- 2.3 of k_prep_lane_pick's 2.5 ms per C5 launch
+                if (nr > 0) cached_roots += (uint64_t)nr;
                 if (nr > 0 && small_use) {
                     hipLaunchKernelGGL(k_prep_lane_pick, dim3((nr + 255) / 256), dim3(256), 0, st, D.d, o->seed, nr,
                                        cur->pixel + nc, cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc,
-                                       P.stats, scache);
+                                       nullptr, scache);
                     HIP_OK(hipGetLastError());
                 } else if (nr > 0) {
                     root_off = nc;
@@ -4776,12 +4783,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                     if (MCPT_PICK_GROUPS && nchunks <= 64) {  // 16 lanes per root
                         const int blocks = std::max(1, std::min((nr + 16 * kPickSlots - 1) / (16 * kPickSlots), 8192));
                         hipLaunchKernelGGL(k_prep_pick_g, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
-                                           cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats,
+                                           cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, nullptr,
                                            nchunks, pr);
                     } else {
                         const int blocks = std::max(1, std::min((nr + 4 * kPickNodes - 1) / (4 * kPickNodes), 8192));
                         hipLaunchKernelGGL(k_prep_pick, dim3(blocks), dim3(256), 0, st, D.d, o->seed, nr, cur->pixel + nc,
-                                           cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, P.stats,
+                                           cur->sample + nc, cur->node + nc, cur->wsum + nc, cur->pick + nc, nullptr,
                                            nchunks, pr);
                     }
                     HIP_OK(hipGetLastError());
@@ -4910,7 +4917,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         // k_prep / k_prep_lane (huge / tiny light sets) run every node in full
         const uint64_t full = hs[7] ? hs[7] : (needs_prep ? nodes_total : 0);
         stats->prep_full_nodes = full;
-        stats->prep_cached_nodes = hs[0];
+        stats->prep_cached_nodes = hs[0] + cached_roots;
         stats->prep_cache_points = cache_points;
         stats->light_evals_total = full * (uint64_t)D.d.NL;
         stats->light_evals_culled_backface = count_c1 ? hs[6] : 0;
