@@ -693,6 +693,16 @@ __device__ inline void block_count(unsigned long long* ca, unsigned a, unsigned 
     __syncthreads();  // s_sum is reused by the next call
 }
 
+// the statistics block: words 0..15 (the render's counters), then kStatShards 128-B lines for the
+// ray counts (rays, light_rays), which every wavefront workgroup adds to -- one line per 8 workgroups
+// round robin instead of one word for all (the host sums the shards)
+constexpr int kStatShards = 8;
+constexpr int kStatBytes = 128 * (1 + kStatShards);
+template <class P_>
+__device__ inline unsigned long long* ray_stats(const P_& P) {
+    return P.stats + 16 * (1 + (blockIdx.x & (kStatShards - 1)));
+}
+
 // shading point and normal of a hit (main.cpp:406-407: interpolated position, normalised
 // interpolation of the vertex normals)
 __device__ inline void node_point(const DScene& S, int f, double beta, double gamma, d3* p, d3* N) {
@@ -3457,7 +3467,7 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt);
         queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt);
     }
-    block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, P.stats + 3,
+    block_count(ray_stats(P), active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, ray_stats(P) + 1,
                 (active && c2) ? 1u : 0u);
 }
 
@@ -3655,7 +3665,7 @@ __global__ __launch_bounds__(256) void k_shade_combine(Params P, Queue cur, int 
     const d3 w2 = ld3(A.w2, A.cap, ii);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
-    block_count(P.stats + 2, active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u);
+    block_count(ray_stats(P), active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u);
 }
 
 // shade_with_brdf (main.cpp:385-396): gen samples the bounce, combine spawns the child on any hit
@@ -3695,7 +3705,7 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
     const d3 w2 = ld3(A.w2, A.cap, ii);
     node_entry(P, c, c ? h2 : -1, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), w2, cur.pixel[ii], cur.sample[ii],
                cur.node[ii] + 1, nxt);
-    block_count(P.stats + 2, (active && (fl & 2)) ? 1u : 0u);
+    block_count(ray_stats(P), (active && (fl & 2)) ? 1u : 0u);
 }
 
 // one BRDF-only path vertex (main.cpp:385-396)
@@ -3756,7 +3766,7 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
         }
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
-    block_count(P.stats + 2, traced);
+    block_count(ray_stats(P), traced);
     if (kCount) wave_count2(P.stats + 8, visits, P.stats + 9, tests);
 }
 
@@ -4475,7 +4485,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     const int cap = (int)std::min<long long>((long long)qf * target + 1024, (1ll << 30));
     int rc;
     if ((rc = ensure(D.hit_f, 4ull * npx)) || (rc = ensure(D.hit_tbg, 24ull * npx)) ||
-        (rc = ensure(D.root_pnw, 72ull * npx)) || (rc = ensure(D.root_kind, 4ull * npx)) || (rc = ensure(D.stats, 128)) ||
+        (rc = ensure(D.root_pnw, 72ull * npx)) || (rc = ensure(D.root_kind, 4ull * npx)) || (rc = ensure(D.stats, kStatBytes)) ||
         (rc = ensure(D.work, 256)))
         return rc;
     Queue qa, qb;
@@ -4591,7 +4601,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     }
     // every buffer is allocated above (first-call hipMalloc of the cache is not device work); the
     // timed region (seconds, HIP events) starts at the primary-hit kernel
-    HIP_OK(hipMemsetAsync(D.stats.p, 0, 128, st));
+    HIP_OK(hipMemsetAsync(D.stats.p, 0, kStatBytes, st));
     HIP_OK(hipEventRecord(D.ev0, st));
     hipLaunchKernelGGL(grid ? k_primary<true> : k_primary<false>, dim3((npx + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock),
                        0, st, D.d, cf, (int*)D.hit_f.p, (double*)D.hit_tbg.p);
@@ -4903,8 +4913,9 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, D.ev0, D.ev1));
     if (stats) {
-        unsigned long long hs[16] = {0};
-        HIP_OK(hipMemcpy(hs, D.stats.p, 128, hipMemcpyDeviceToHost));
+        unsigned long long hs[kStatBytes / 8] = {0};
+        HIP_OK(hipMemcpy(hs, D.stats.p, kStatBytes, hipMemcpyDeviceToHost));
+        for (int k = 1; k <= kStatShards; k++) hs[2] += hs[16 * k], hs[3] += hs[16 * k + 1];  // ray_stats shards
         stats->seconds = ms * 1e-3;
         stats->camera_samples = (uint64_t)(s1 - s0) * npx;
         stats->light_evals_survived = hs[1];
