@@ -9,14 +9,18 @@ steps x gpus x spp_per_step samples per pixel.
 Each call computes everything it uses, including its root-point light-prep cache (DESIGN.md §4.4);
 nothing is carried from one step to the next except the framebuffer.
 
-Multi-GPU (torchrun, one process per GPU): sample-range sharding -- weak scaling for --config c3 (each
-rank S samples per step), strong scaling for --config c4 (1600x1200, one 4096-spp frame per step split
-over the ranks, BASELINE.json configs[3]).  Every rank joins
-the library's own RCCL communicator (mcpt_comm: rank 0's ncclUniqueId is broadcast over
-torch.distributed, then mcpt_comm_init_rank); step k is the job [k*G*S, (k+1)*G*S) of global sample
-indices, which the library splits into one S-sample shard per rank and ends with ONE ncclReduce(sum)
-of the fp64 framebuffers into rank 0 (include/mcpt.h, mcpt_render_opts.comm).  torch.distributed
-only provides the barrier and the max-over-ranks timing.
+Multi-GPU: sample-range sharding -- weak scaling for --config c3 (each rank S samples per step), strong
+scaling for --config c4 (1600x1200, one 4096-spp frame per step split over the ranks, BASELINE.json
+configs[3]).  Step k is the job [k*G*S, (k+1)*G*S) of global sample indices, which the library splits
+into one S-sample shard per GPU and ends with ONE ncclReduce(sum) of the fp64 framebuffers into GPU 0.
+Two launch forms:
+  * `python3 bench.py --gpus N` (no WORLD_SIZE in the environment): one process drives all N GPUs
+    through the library's device list (mcpt_render_opts.devices = 0..N-1: a host thread and stream
+    per GPU, ncclCommInitAll, one grouped reduce per step);
+  * `torchrun --nproc-per-node N bench.py --gpus N`: one process per GPU, each joining the library's own
+    RCCL communicator (mcpt_comm: rank 0's ncclUniqueId is broadcast over torch.distributed, then
+    mcpt_comm_init_rank); torch.distributed only provides the barrier and the max-over-ranks timing.
+    WORLD_SIZE must equal --gpus.
 
 Also reported: the roofline of the dominant kernel (k_prep: fp64 VALU-bound light prep), the
 CPU baseline (the C oracle on a bounded stratified pixel subset, rank 0, N=1 only) and the
@@ -127,12 +131,19 @@ def cpu_threads():
     return max(1, min(n, 16, os.cpu_count() or 1))
 
 
-def cpu_baseline(scene_name, W, H, mode, seed, full_spp, max_s):
+def cpu_baseline(scene_name, W, H, mode, seed, full_spp, max_s, single_s):
     """The C oracle (oracle/liboracle.so: the reference's algorithm incl. its uniform grid and O(N_L) light
-    prep per node, fp64) on the stratified pixel subset of BASELINE.md §3 -- every 20th pixel in x and y --
-    at the workload's FULL spp, with the host's CPU share (cpu_threads(): the oracle parallelises over
-    pixels; `cores` says how many).  If that would exceed max_s the spp is reduced and the full-spp time is
-    extrapolated (stated in the record).  Returns (dict, subset image, spp)."""
+    prep per node, fp64) on the stratified pixel subset of BASELINE.md §3 -- every 20th pixel in x and y.
+
+    Two legs, both measured on this host:
+      * single thread (the baseline BASELINE.md §3 / north_star name: the reference's loop main.cpp:557-588
+        is single-threaded, README.md:418): the subset at as many spp as fit in single_s seconds (the oracle's
+        time per camera sample does not depend on spp: it caches nothing across samples), so `value` is a
+        measured 1-core rate, `cores` 1;
+      * all of the host's CPU share (cpu_threads(): the oracle parallelises over pixels) at the workload's
+        FULL spp if that fits in max_s (else fewer spp, extrapolated; stated), whose image is the L2
+        reference of the bench line.
+    Returns (dict, subset image of the multi-thread leg, its spp)."""
     from oracle import pyoracle as po
 
     obj, xml, xml_cam = scene_files(scene_name)
@@ -145,7 +156,9 @@ def cpu_baseline(scene_name, W, H, mode, seed, full_spp, max_s):
     e, _ = po.camera_ray(ocam, 0, 0)
     osc.build_grid(e)
     m = {"mis": po.MODE_MIS, "brdf": po.MODE_BRDF, "shade": po.MODE_SHADE, "shade_area": po.MODE_SHADE_AREA}[mode]
+    npx = len(range(7, H, 20)) * len(range(7, W, 20))
     nt = cpu_threads()
+    # ---- multi-thread leg: full spp (the L2 reference image) ----
     t = time.perf_counter()
     osc.render(ocam, m, seed, 4, s1=4, stride=20, offset=7, nthreads=nt)  # calibration: 4 spp
     t4 = time.perf_counter() - t
@@ -154,30 +167,38 @@ def cpu_baseline(scene_name, W, H, mode, seed, full_spp, max_s):
     t = time.perf_counter()
     img, _ = osc.render(ocam, m, seed, spp, stride=20, offset=7, nthreads=nt)
     dt = time.perf_counter() - t
-    npx = len(range(7, H, 20)) * len(range(7, W, 20))
-    value = npx * spp / dt / 1e6
-    out = {"value": value, "unit": "Msamples/s", "cores": nt, "kind": "port",
+    mt_value = npx * spp / dt / 1e6
+    # ---- single-thread leg: the same subset, samples [0, spp1) at the same seed ----
+    per_sample_1t = dt * nt / (npx * spp)  # first guess from the multi-thread leg
+    spp1 = int(max(1, min(full_spp, single_s / max(per_sample_1t * npx, 1e-9))))
+    t = time.perf_counter()
+    osc.render(ocam, m, seed, spp1, stride=20, offset=7, nthreads=1)
+    dt1 = time.perf_counter() - t
+    value = npx * spp1 / dt1 / 1e6
+    out = {"value": value, "unit": "Msamples/s", "cores": 1, "kind": "port",
            "host_cpu": host_cpu_model(), "host_cpus_visible": os.cpu_count(),
-           "per_core_value": value / nt, "spp": spp, "full_spp": spp == full_spp,
-           "subset_pixels": npx, "subset_seconds": round(dt, 2),
-           "sample": "oracle/mcpt_oracle.c (fp64 C restatement incl. the reference's uniform grid), %d threads over "
-                     "pixels, every 20th pixel in x and y of %dx%d (%d px = 1/400 of the frame) x %d spp %s = %d camera "
-                     "samples in %.1f s%s" % (nt, W, H, npx, spp, mode.upper(), npx * spp, dt,
-                                              "" if spp == full_spp else
-                                              " (full %d spp extrapolated: %.0f s)" % (full_spp, dt * full_spp / spp))}
-    out["full_frame_seconds_extrapolated"] = dt * (full_spp / spp) * (W * H / npx)
+           "single_thread_value": value, "single_thread_spp": spp1, "single_thread_seconds": round(dt1, 2),
+           "multi_thread_value": mt_value, "multi_thread_cores": nt, "multi_thread_spp": spp,
+           "multi_thread_full_spp": spp == full_spp, "multi_thread_seconds": round(dt, 2),
+           "subset_pixels": npx,
+           "sample": "oracle/mcpt_oracle.c (fp64 C restatement incl. the reference's uniform grid) on 1 core: every 20th "
+                     "pixel in x and y of %dx%d (%d px = 1/400 of the frame) x %d spp %s = %d camera samples in %.1f s "
+                     "(time per sample is independent of spp; full %d spp extrapolated: %.0f s); also %d threads at %d spp "
+                     "in %.1f s (%.4f Msamples/s), whose image is the L2 reference" % (
+                         W, H, npx, spp1, mode.upper(), npx * spp1, dt1, full_spp, dt1 * full_spp / spp1, nt, spp, dt,
+                         mt_value)}
+    out["full_frame_seconds_extrapolated_1core"] = dt1 * (full_spp / spp1) * (W * H / npx)
     # The reference itself cannot travel to the GPU box.  Its single-thread speed relative to this
-    # restatement was measured on identical frames in the build container (tools/time_reference_cpu.py):
-    # the restatement is faster (no std::map facet lookups), so the reference-equivalent baseline is
-    # value / ratio (per thread: the reference is single-threaded, README.md:418).
+    # restatement was measured on identical frames in the build container (tools/time_reference_cpu.py) --
+    # a cross-host factor (another CPU), applied to the single-thread value measured here.
     ref = load_json(os.path.join(ROOT, "profiles", "cpu_reference_vs_oracle.json"))
     r = (ref or {}).get("modes", {}).get(mode) if scene_name == "veach" else None
     if r:
-        out["oracle_over_reference"] = r["oracle_over_reference"]
-        out["reference_equivalent_value"] = value / nt / r["oracle_over_reference"]
-        out["reference_equivalent_source"] = ("single thread: per-core value / oracle_over_reference; "
-                                              "profiles/cpu_reference_vs_oracle.json: compiled reference %.0f vs oracle "
-                                              "%.0f samples/s, 1 core of '%s', %s" % (
+        out["oracle_over_reference_cross_host"] = r["oracle_over_reference"]
+        out["reference_equivalent_value"] = value / r["oracle_over_reference"]
+        out["reference_equivalent_source"] = ("single_thread_value (measured on this host) / oracle_over_reference_cross_host "
+                                              "(profiles/cpu_reference_vs_oracle.json: compiled reference %.0f vs oracle "
+                                              "%.0f samples/s, 1 core of '%s', not this host; %s)" % (
                                                   r["reference_samples_per_s"], r["oracle_samples_per_s"],
                                                   ref.get("host", "?"), r["frame"]))
     return out, img, spp
@@ -204,6 +225,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20240430)
     ap.add_argument("--cpu-seconds", type=float, default=90.0,
                     help="CPU baseline budget: the full-spp subset runs if it fits, else fewer spp, extrapolated")
+    ap.add_argument("--cpu-single-seconds", type=float, default=20.0,
+                    help="budget of the single-thread CPU baseline leg (spp reduced to fit; rate per sample)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and L2 check")
     ap.add_argument("--fresh-pdf", action="store_true",
                     help="MIS with the node's own light pdf (MCPT_RENDER_FRESH_PDF) instead of the reference's stale one")
@@ -222,9 +245,20 @@ def main():
                          "share GPUs round-robin and torch.distributed uses gloo")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    # Two launch forms, one per-GPU shard each:
+    #  * torchrun (WORLD_SIZE set): one process per GPU, the library's per-process communicator
+    #    (mcpt_comm, ncclCommInitRank); WORLD_SIZE must equal --gpus;
+    #  * plain `python3 bench.py --gpus N` (no WORLD_SIZE): ONE process drives N GPUs through the
+    #    library's device list (mcpt_render_opts.devices = 0..N-1: one host thread + stream per GPU,
+    #    ncclCommInitAll, ONE grouped ncclReduce per step into device 0).
+    launched = "WORLD_SIZE" in os.environ
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if launched and world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks (WORLD_SIZE)" % (args.gpus, world))
     import torch
     import torch.distributed as dist
 
@@ -233,21 +267,35 @@ def main():
     rehearsal = bool(args.collective_lib)
     if rehearsal:
         mcpt.set_collective_lib(args.collective_lib)
-        local = local % max(torch.cuda.device_count(), 1)
+    ndev = torch.cuda.device_count()  # counts without initialising the GPU (no HIP call yet)
+    devices = None  # the in-process device list (plain launch with --gpus > 1)
+    if not launched and args.gpus > 1:
+        if ndev < args.gpus and not rehearsal:
+            raise SystemExit("bench.py --gpus %d: only %d GPUs visible" % (args.gpus, ndev))
+        # rehearsal on fewer GPUs (test infrastructure): the list repeats devices and every entry is its own
+        # rank of the (shim) communicator, MCPT_DEBUG_SHARD_RANKS
+        devices = [k % max(ndev, 1) for k in range(args.gpus)]
+        world = args.gpus
+    if rehearsal:
+        local = local % max(ndev, 1)
     torch.cuda.set_device(local)
-    if world > 1:
+    if launched and world > 1:
         if rehearsal:  # RCCL refuses two ranks on one GPU: barrier and timing over gloo
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    # the library's RCCL communicator (one rank per process); a 1-rank communicator at N=1
-    uid = [mcpt.Comm.unique_id() if rank == 0 else None]
-    if world > 1:
-        dist.broadcast_object_list(uid, src=0)
-    comm = mcpt.Comm(world, rank, uid[0], device=local)
+    comm = None
+    if devices is None:
+        # the library's RCCL communicator (one rank per process); a 1-rank communicator at N=1
+        uid = [mcpt.Comm.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = mcpt.Comm(world, rank, uid[0], device=local)
+    multi = dict(comm=comm) if devices is None else dict(devices=devices)
+    list_flags = mcpt.DEBUG_SHARD_RANKS if devices is not None and rehearsal else 0
 
     def barrier():
-        if world > 1:
+        if launched and world > 1:
             dist.barrier()
 
     cfg = CONFIGS[args.config]
@@ -272,11 +320,11 @@ def main():
 
     mode_flags = (mcpt.RENDER_FRESH_PDF if args.fresh_pdf else 0) | (
         mcpt.RENDER_PRECISION_FP32 if args.precision == "fp32" else 0) | (
-        mcpt.DEBUG_NO_ROOT_CACHE if args.no_root_cache else 0) | args.debug_flags
+        mcpt.DEBUG_NO_ROOT_CACHE if args.no_root_cache else 0) | args.debug_flags | list_flags
     flags = mcpt.RENDER_NO_BACKFACE_STATS | mode_flags
     for k in range(args.warmup):  # warmup renders (same kernels and flags as the timed steps) go to scratch
         mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
-                           sample_range=(0, world * S), comm=comm, flags=flags)
+                           sample_range=(0, world * S), flags=flags, **multi)
     totals = {}
     barrier()
     torch.cuda.synchronize()
@@ -284,7 +332,7 @@ def main():
     tlog = t0
     for k in range(args.steps):  # the job of step k: [k*G*S, (k+1)*G*S), S samples per rank, 1 reduce
         st = mcpt.render_device(scene, cam, frame_spp, fb.data_ptr(), mode=args.mode, seed=args.seed,
-                                sample_range=(k * world * S, (k + 1) * world * S), comm=comm, flags=flags)
+                                sample_range=(k * world * S, (k + 1) * world * S), flags=flags, **multi)
         for key, v in st.as_dict().items():
             totals[key] = totals.get(key, 0) + v
         if rank == 0 and time.perf_counter() - tlog > 30:
@@ -293,7 +341,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if launched and world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -306,8 +354,8 @@ def main():
     rep = {}
     for k in range(args.steps):
         st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
-                                sample_range=(k * world * S, (k + 1) * world * S), comm=comm,
-                                flags=mcpt.DEBUG_COUNT_TRAVERSAL | mode_flags)
+                                sample_range=(k * world * S, (k + 1) * world * S),
+                                flags=mcpt.DEBUG_COUNT_TRAVERSAL | mode_flags, **multi)
         for key, v in st.as_dict().items():
             rep[key] = rep.get(key, 0) + v
     for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays",
@@ -321,6 +369,10 @@ def main():
         comm.close()
         dist.destroy_process_group()
         return
+    if devices is not None:
+        # every distinct device's shard ran concurrently: the device time of the run is its wall time
+        # on each of them (render_multi's stats sum the shards' kernel times)
+        totals["seconds"] = totals.get("seconds", 0.0) * max(totals.get("devices_used", 1) // max(args.steps, 1), 1)
     pmc = load_json(os.path.join(ROOT, "profiles", "pmc_latest.json")) or {"kernels": {}}
     # the PMC figures of this workload when they were profiled (tools/summarize_profiles.py), else the
     # headline's
@@ -428,30 +480,37 @@ def main():
     cpu = None
     l2 = l2max = None
     if world == 1 and not args.no_cpu:
-        log("cpu baseline (<= ~%.0f s) ..." % args.cpu_seconds)
-        cpu, cimg, cspp = cpu_baseline(args.scene, W, H, args.mode, args.seed, S, args.cpu_seconds)
+        log("cpu baseline (<= ~%.0f + %.0f s) ..." % (args.cpu_seconds, args.cpu_single_seconds))
+        cpu, cimg, cspp = cpu_baseline(args.scene, W, H, args.mode, args.seed, S, args.cpu_seconds,
+                                       args.cpu_single_seconds)
         g, _ = mcpt.render(scene, cam, cspp, mode=args.mode, seed=args.seed, device=local, flags=mode_flags)
         sub = (slice(7, None, 20), slice(7, None, 20))
         l2 = rel_l2(g[sub], cimg[sub])
         l2max = max_px_rel(g[sub], cimg[sub])
+        cpu["gpu_over_single_thread"] = round(value / cpu["value"], 1)
+        cpu["gpu_over_host_threads"] = round(value / cpu["multi_thread_value"], 1)
     if args.out:
         mcpt.write_bmp(args.out, mcpt.tone_map(fb.cpu().numpy()))
     line = {
         "metric": SCENES[args.scene][0], "value": round(value, 4), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": cfg["scaling"],
-        # the GPU over the compiled reference's own single thread on the same workload (the CPU
-        # baseline's reference-equivalent rate; BASELINE.md publishes only render times of another frame)
-        "vs_baseline": round(value / cpu["reference_equivalent_value"], 1) if cpu and cpu.get("reference_equivalent_value") else None,
+        # BASELINE.md publishes no number for this metric (only render times of another frame on unstated
+        # hardware), so there is nothing to divide by; the GPU/CPU ratios live in cpu_baseline
+        "vs_baseline": None,
         "dtype": "f64" if args.precision == "fp64" else "f64 (light-prep weights f32, MCPT_RENDER_PRECISION_FP32)",
         "data": SCENES[args.scene][1],
         "config": {"workload": "%s %s %dx%d" % ("veach-mis" if args.scene == "veach" else "cornell-1M", args.mode.upper(), W, H),
                    "config": args.config, "width": W, "height": H,
                    "mode": args.mode, "spp_per_step": S, "frame_spp": frame_spp, "seed": args.seed,
                    "precision": args.precision, "root_cache": not args.no_root_cache,
-                   "parallelism": "sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm)" % world + (
+                   "parallelism": ("sample-shard x%d + 1 RCCL reduce per step (library mcpt_comm, one process per GPU)" % world
+                                   if devices is None else
+                                   "sample-shard x%d + 1 grouped RCCL reduce per step (library device list %s, one process)"
+                                   % (world, devices)) + (
                        " [rehearsal: collective %s, ranks sharing GPUs]" % os.path.basename(args.collective_lib)
                        if rehearsal else ""),
+                   "launch": "torchrun" if launched else "single process",
                    "job_spp_per_step": world * S},
         "roofline": roofline,
         "roofline_prep": roof_prep,
@@ -463,8 +522,9 @@ def main():
         "samples": samples,
     }
     print(json.dumps(line), flush=True)
-    comm.close()
-    if world > 1:
+    if comm is not None:
+        comm.close()
+    if launched and world > 1:
         dist.destroy_process_group()
 
 

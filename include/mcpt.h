@@ -126,7 +126,14 @@ typedef struct {
     /* One process per GPU: this process renders rank's share of [sample_begin, sample_end) on the
      * communicator's device and the call ends with ONE ncclReduce(sum, root rank 0): the whole job's
      * sum is ADDED to rank 0's buffer; other ranks' buffers are left unchanged (their shard goes
-     * through a library buffer).  Every rank must make the same call.  Exclusive with devices. */
+     * through a library buffer).  Every rank must make the same call.  Exclusive with devices.
+     * Failures: a rank whose render fails (out of memory, its own cancel, ...) still joins the reduce with
+     * a failure flag, so rank 0 returns MCPT_E_DEVICE "k of N ranks failed" and nobody blocks.  The one
+     * exception is a rank that cannot take part in the reduce at all -- it cannot allocate its
+     * (W*H*3 + 1)-double reduce buffer (done first, before any other allocation of the call, and kept
+     * for later calls of the same frame size) or its device can no longer enqueue work: it aborts the
+     * communicator and returns, and under RCCL its peers then block in ncclReduce (RCCL has no way to
+     * release them from one rank).  Leave that buffer's room free on every device. */
     mcpt_comm* comm;
 } mcpt_render_opts;
 /* mcpt_render_opts.flags: skip the light-side cull statistic in the hot loop of the split light cull;

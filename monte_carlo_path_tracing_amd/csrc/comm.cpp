@@ -15,7 +15,10 @@
 // mcpt_debug_set_collective_lib (include/mcpt_debug.h) points that dlopen at another library with the
 // same NCCL entry points before the first use -- the test-only host-memory collective of
 // tests/collshim, which lets 2-8 ranks share the one GPU of a test box (RCCL refuses two ranks on one
-// device), so the multi-rank protocol below runs in CI exactly as it does over xGMI.
+// device), so the multi-rank protocol below (the shard split, the buffers, the calls and their order, the
+// failure flag) runs in CI as the 8-GPU run issues it.  The shim differs from RCCL in its transport and in
+// one failure mode: it is synchronous and times out (MCPT_COLLSHIM_TIMEOUT) where an RCCL peer of an
+// aborted rank blocks (include/mcpt.h, mcpt_render_opts.comm).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>

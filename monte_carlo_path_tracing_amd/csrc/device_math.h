@@ -467,13 +467,16 @@ __device__ inline double sliver_term(double num, double den) {
 //    sin >= 1e-3 -- far from the 1e-8 angle culls, and acos is well conditioned (the literal angles are
 //    within ~1e-12 of the true ones);
 //  * num > 1e-9 max(den, 0), i.e. tan(sA / 2) > 1e-9: the literal sA = alpha + beta + gamma - pi is far
-//    above its rounding, so sA >= 0 and w = sA sum L >= 0 is finite.
-__device__ inline int literal_survival_quick(d3 p0, d3 p1, d3 p2, d3 nl, d3 x1, d3 n) {
+//    above its rounding, so sA > 0;
+//  * 0 <= sum L < 1e300 (sA <= 2 pi): w = sA sum L is >= 0 and finite, so the literal chain's w < 0 / inf /
+//    NaN culls (Mylight.cpp:405-411) cannot fire.  A negative, huge or NaN radiance is left to the chain.
+__device__ inline int literal_survival_quick(d3 p0, d3 p1, d3 p2, d3 nl, double lsum, d3 x1, d3 n) {
     if (light_cheap_stage(p0, p1, p2, nl, x1, n) != 0) return 0;
     const d3 A = funit(sub(p0, x1)), B = funit(sub(p1, x1)), C = funit(sub(p2, x1));
     const double ab = fdot(A, B), bc = fdot(B, C), ca = fdot(C, A);
     const double num = fabs(fdot(A, fcross(B, C))), den = 1.0 + ab + bc + ca;
-    const bool clear = fmax(ab, fmax(bc, ca)) < 1.0 - 1e-9 && 4.0 - den <= 1000.0 * num && num > 1e-9 * fmax(den, 0.0);
+    const bool clear = fmax(ab, fmax(bc, ca)) < 1.0 - 1e-9 && 4.0 - den <= 1000.0 * num && num > 1e-9 * fmax(den, 0.0) &&
+                       lsum >= 0.0 && lsum < 1e300;
     return clear ? 1 : -1;
 }
 __device__ inline bool light_weight(d3 p0, d3 p1, d3 p2, double lsum2, d3 x1, double* w_out) {

@@ -2953,9 +2953,10 @@ __device__ inline double state_light_pdf(const DScene& S, int li, const double* 
     const d3 x = mk3(st[0], st[1], st[2]), N = mk3(st[3], st[4], st[5]);
     const PrepLight L = load_light(S, li);
     // the literal chain only where the quick test cannot decide (slivers, near-degenerate triangles)
-    const int q = literal_survival_quick(L.p0, L.p1, L.p2, L.nl, x, N);
-    if (q > 0 || (q < 0 && light_tri_eval(L.p0, L.p1, L.p2, L.nl, S.light_sum[li], x, N, nullptr)))
-        return S.light_sum[li] / st[6];
+    const double lsum = S.light_sum[li];
+    const int q = literal_survival_quick(L.p0, L.p1, L.p2, L.nl, lsum, x, N);
+    if (q > 0 || (q < 0 && light_tri_eval(L.p0, L.p1, L.p2, L.nl, lsum, x, N, nullptr)))
+        return lsum / st[6];
     return 0.0;
 }
 
@@ -4618,7 +4619,16 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         HIP_OK(hipGetLastError());
         HIP_OK(hipMemcpyAsync(D.pinned_count, qb.count, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
-        const int nr = (int)std::min<unsigned>(D.pinned_count[0], (unsigned)cap);
+        int nr = (int)std::min<unsigned>(D.pinned_count[0], (unsigned)cap);
+        if (D.pinned_count[0] > (unsigned)cap) {
+            // more root points than the queue holds (a frame of more pixels than the working set under memory
+            // pressure): k_root_points dropped some, and their pixels' cache rows would be stale -- no root cache
+            // in this call, every root runs the full prep (same image, slower)
+            pc.use = 0;
+            small_use = false;
+            rl = RootLit{};
+            nr = 0;
+        }
         if (nr > 0 && small_use) {
             HIP_OK(hipEventRecord(D.evp0, st));
             HIP_OK(launch_prep_lane(D.d, o->seed, nr, qb.p, qb.n, qb.cap, qb.pixel, nullptr, nullptr, nullptr, nullptr, nullptr,

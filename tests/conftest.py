@@ -15,6 +15,18 @@ SCENE_DIR = ROOT / "scenes" / "veach-mis"
 SCENE_OBJ = str(SCENE_DIR / "veach-mis.obj")
 SCENE_XML = str(SCENE_DIR / "veach-mis.xml")
 
+# Parity gates.  The north star's statement is <= 1e-3 relative (frame L2 and per pixel); every frame test
+# asserts it.  The build reproduces the oracle far more closely than that (fp64 throughout, picks exact), so
+# the frame tests also assert what it achieves, with 10-100x margin over the round-4 measurements
+# (profiles/round4m_gputests.log): frame relative L2 <= 1e-8 (measured <= 3.1e-10), max per-pixel <= 1e-6 on
+# the stride-20 subsets and small frames (measured <= 3.2e-8), <= 2e-5 on whole 400x300 / 800x600 frames,
+# whose worst pixels carry glibc-vs-correctly-rounded acos differences (measured 8.2e-7 / 2.4e-6).  A pick or
+# ordering regression that moves any pixel by ~1e-5 fails these.
+NORTH_STAR_TOL = 1e-3
+TIGHT_L2 = 1e-8
+TIGHT_PX = 1e-6
+TIGHT_PX_FRAME = 2e-5
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")

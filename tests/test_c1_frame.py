@@ -16,7 +16,7 @@ own acos rounding.)"""
 import numpy as np
 import pytest
 
-from conftest import SCENE_OBJ, SCENE_XML
+from conftest import SCENE_OBJ, SCENE_XML, TIGHT_L2, TIGHT_PX_FRAME
 import monte_carlo_path_tracing_amd as mcpt
 from oracle import pyoracle as po
 
@@ -62,4 +62,5 @@ def test_c1_gpu_equals_cpu_path(mode):
     print("C1 %s 400x300x4: rel L2 %.3e, max per-pixel %.3e, pixels above 1e-6: %d; exact-fallback preps %d of %d" % (
         mode, err, mx, (pr > 1e-6).sum(), st.prep_exact_nodes, st.prep_full_nodes + st.prep_cached_nodes))
     assert err <= 1e-3 and mx <= 1e-3
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX_FRAME, (err, mx)  # what the build achieves (tests/conftest.py)
     assert np.array_equal(mcpt.tone_map(img), mcpt.tone_map(ref)) or np.mean(mcpt.tone_map(img) != mcpt.tone_map(ref)) < 1e-4

@@ -8,7 +8,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import cornell_scene
+from conftest import TIGHT_L2, TIGHT_PX, cornell_scene
 import monte_carlo_path_tracing_amd as mcpt
 from oracle import pyoracle as po
 
@@ -108,6 +108,7 @@ def test_cornell_1m_render_parity(big, mode, omode, spp):
         mode, spp, err, mx, st.camera_samples / st.seconds / 1e6))
     assert np.isfinite(img).all() and (img >= 0).all() and ref.sum() > 0
     assert err <= L2_TOL and mx <= L2_TOL
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX, (err, mx)
 
 
 @pytest.mark.gpu
@@ -121,3 +122,4 @@ def test_cornell_1m_full_size_pixel_subset(big):
     print("cornell-1M mis 800x600x8 subset rel L2 %.3e, max per-pixel %.3e; %.2f Msamples/s" % (
         err, mx, st.camera_samples / st.seconds / 1e6))
     assert err <= L2_TOL and mx <= L2_TOL
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX, (err, mx)

@@ -23,7 +23,7 @@ from oracle import pyoracle as po
 
 pytestmark = pytest.mark.gpu
 SEED = 20240430
-L2_TOL = 1e-3
+from conftest import NORTH_STAR_TOL as L2_TOL, TIGHT_L2, TIGHT_PX, TIGHT_PX_FRAME  # noqa: E402
 
 
 @pytest.fixture(scope="module")
@@ -232,6 +232,7 @@ def test_render_parity_small(scene, oscene, mode, spp):
     print("%s 80x60x%d rel L2 %.3e, max per-pixel %.3e, device %.4fs" % (mode, spp, err, mx, st.seconds))
     assert np.isfinite(g).all() and (g >= 0).all()
     assert err <= L2_TOL and mx <= L2_TOL
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX, (err, mx)
 
 
 @pytest.mark.parametrize("mode,spp", [("mis", 16), ("brdf", 64), ("shade", 16), ("shade_area", 32)])
@@ -248,6 +249,7 @@ def test_render_parity_full_size_pixel_subset(scene, oscene, mode, spp):
         mode, spp, err, mx, st.camera_samples / st.seconds / 1e6))
     assert np.isfinite(g).all() and (g >= 0).all()
     assert err <= L2_TOL and mx <= L2_TOL
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX, (err, mx)
     assert g.mean() > 0
 
 
@@ -263,6 +265,7 @@ def test_c3_full_frame_vs_oracle(scene, oscene):
         err, mx, st.shading_nodes, st.prep_exact_nodes))
     assert np.isfinite(g).all() and (g >= 0).all() and c.sum() > 0
     assert err <= L2_TOL and mx <= L2_TOL
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX_FRAME, (err, mx)
 
 
 @pytest.mark.parametrize("W,H,spp", [(80, 60, 8), (800, 600, 16)])
@@ -280,6 +283,7 @@ def test_mis_fresh_pdf_flag_vs_oracle(scene, oscene, W, H, spp):
     err, mx = rel_l2(g[sub], c[sub]), max_px_rel(g[sub], c[sub])
     print("fresh-pdf MIS %dx%dx%d rel L2 %.3e, max per-pixel %.3e" % (W, H, spp, err, mx))
     assert err <= L2_TOL and mx <= L2_TOL
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX, (err, mx)
     d, _ = mcpt.render(scene, cam, spp, mode="mis", seed=SEED)
     assert rel_l2(d[sub], g[sub]) > 1e-9
 

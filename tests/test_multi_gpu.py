@@ -25,7 +25,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import ROOT, SCENE_OBJ, SCENE_XML
+from conftest import ROOT, SCENE_OBJ, SCENE_XML, TIGHT_L2, TIGHT_PX_FRAME
 import monte_carlo_path_tracing_amd as mcpt
 from oracle import pyoracle as po
 
@@ -172,6 +172,7 @@ def test_c4_frame_1600x1200_vs_oracle_subset(scene):
     l2, mx = rel_l2(g, c), max_px_rel(g, c)
     print("C4 1600x1200x%d MIS subset: rel L2 %.3e, max per-pixel %.3e" % (spp, l2, mx))
     assert l2 <= 1e-3 and mx <= 1e-3
+    assert l2 <= TIGHT_L2 and mx <= TIGHT_PX_FRAME, (l2, mx)  # what the build achieves (tests/conftest.py)
 
 
 def test_comm_failures_join_the_reduce_and_leave_the_comm_usable(scene, single):

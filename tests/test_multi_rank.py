@@ -23,7 +23,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import ROOT, SCENE_OBJ, SCENE_XML
+from conftest import ROOT, SCENE_OBJ, SCENE_XML, TIGHT_L2, TIGHT_PX_FRAME
 import monte_carlo_path_tracing_amd as mcpt
 
 pytestmark = pytest.mark.gpu
@@ -245,6 +245,7 @@ def test_c4_split_over_two_ranks_vs_oracle(tmp_path):
     l2, mx = rel_l2(g, c), max_px_rel(g, c)
     print("C4 1600x1200x%d MIS split over 2 ranks, subset vs oracle: rel L2 %.3e, max per-pixel %.3e" % (spp, l2, mx))
     assert l2 <= 1e-3 and mx <= 1e-3
+    assert l2 <= TIGHT_L2 and mx <= TIGHT_PX_FRAME, (l2, mx)  # what the build achieves (tests/conftest.py)
 
 
 def test_bench_two_ranks_under_torchrun(tmp_path):
@@ -264,3 +265,24 @@ def test_bench_two_ranks_under_torchrun(tmp_path):
     line = json.loads([ln for ln in text.splitlines() if ln.startswith("{\"metric\"")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["samples"] == 800 * 600 * 2 * 8
     assert line["config"]["job_spp_per_step"] == 16
+
+
+def test_bench_plain_launch_uses_n_gpus(tmp_path):
+    """`python3 bench.py --gpus 2` exactly as the driver invokes it -- no torchrun, no WORLD_SIZE: ONE
+    process renders the job over the library's device list (one shard per GPU, ncclCommInitAll, one
+    grouped reduce per step).  On this one-GPU box the two list entries share cuda:0 as two ranks of the
+    collective shim (--collective-lib); the line must say n_gpus 2 and count both shards' samples."""
+    out = tmp_path / "bench_plain.log"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--spp-per-step", "8", "--no-cpu", "--collective-lib", SHIM]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MCPT_COLLSHIM_TIMEOUT"] = "90"
+    with open(out, "w") as f:
+        rc = subprocess.run(cmd, stdout=f, stderr=subprocess.STDOUT, timeout=300, env=env).returncode
+    text = out.read_text()
+    assert rc == 0, text[-3000:]
+    line = json.loads([ln for ln in text.splitlines() if ln.startswith("{\"metric\"")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["samples"] == 800 * 600 * 2 * 8
+    assert line["config"]["job_spp_per_step"] == 16 and line["config"]["launch"] == "single process"
+    assert "device list [0, 0]" in line["config"]["parallelism"]
+
