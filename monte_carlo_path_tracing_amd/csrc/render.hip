@@ -316,6 +316,9 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 // source in round 4): node loads as 32-bit byte offsets (neutral); near / far planes picked once per
 // ray by the inverse direction's sign (97 -> 63 VALU per visit, but k_mis_rays 3.81 -> 4.02 ms); the
 // near / far planes selected after the usual loads (MIS 464.3 -> 463.2, BRDF-only 5 831 -> 5 760).
+#ifndef MCPT_MARGIN_FMA
+#define MCPT_MARGIN_FMA 0  // A/B: the slab test's 1e-5 relative margin as one FMA
+#endif
 #ifndef MCPT_FILTER_MIS
 #define MCPT_FILTER_MIS 1
 #endif
@@ -344,10 +347,19 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 // events; only the untimed statistics replay instantiates it)
 // kTop > 0: nodes [0, kTop) are read from `top` (an LDS copy of the tree's top levels) through a
 // generic pointer, the rest from `nodes`
+// MCPT_TRACE_DIAG (diagnostics only, with kCount): *witer / *wleaf count the WAVE's iterations of the
+// node-visit loop and of the triangle loop (added by the wave's first active lane), so that visits /
+// (64 witer) is the traversal's SIMD lane utilisation
+#ifndef MCPT_TRACE_DIAG
+#define MCPT_TRACE_DIAG 0
+#endif
 template <int kLds, bool kCount = false, int kTop = 0, bool kFilter = true>
 __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
                                 int exclude, int* __restrict__ lds, int stride, unsigned* visits = nullptr,
-                                unsigned* tests = nullptr, const BvhNode4* top = nullptr, float tlimit0 = FLT_MAX) {
+                                unsigned* tests = nullptr, const BvhNode4* top = nullptr, float tlimit0 = FLT_MAX,
+                                unsigned* witer = nullptr, unsigned* wleaf = nullptr) {
+    auto first_lane = []() { return (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1; };
+    (void)first_lane;
     constexpr int kDone = 0x7fffffff;
     Hit best{-1, DBL_MAX, 0, 0};
     if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
@@ -402,6 +414,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     while (node != kDone || leaf < 0) {
         while (node >= 0 && node != kDone) {
             if (kCount) ++*visits;
+            if (kCount && MCPT_TRACE_DIAG && witer && first_lane()) ++*witer;
             float t[4];
             int code[4];
             // the tree's top levels from LDS when the whole wave is in them (a wave-uniform branch)
@@ -417,7 +430,11 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                     const float tz0 = fmaf(lo[2][k], iz, -oiz), tz1 = fmaf(hi[2][k], iz, -oiz);
                     const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
                     const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
+#if MCPT_MARGIN_FMA
+                    const bool h = chs[k] != kBvh4Empty && t0 <= fmaf(t1, 1.00001f, 1e-6f);
+#else
                     const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
+#endif
                     t[k] = h ? t0 : FLT_MAX;
                     code[k] = h ? chs[k] : kDone;
                 }
@@ -446,6 +463,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
             for (int q = first; q < first + cnt; q++) {
                 const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
                 const int fac = __float_as_int(a4.w);
+                if (kCount && MCPT_TRACE_DIAG && wleaf && first_lane()) ++*wleaf;
                 if (fac == exclude) continue;
                 if (kCount) ++*tests;
                 if (kFilter) {
@@ -3121,7 +3139,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
     const int fl = i < n ? A.flags[i] : 0;
     int f = -1;
     double beta = 0, gamma = 0;
-    unsigned visits = 0, tests = 0;
+    unsigned visits = 0, tests = 0, witer = 0, wleaf = 0;
     if (fl & (1 << set)) {
         const double* d = set == 0 ? A.d1 : A.d2;
         const d3 ro = ld3(cur.p, cur.cap, i);
@@ -3140,7 +3158,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
                 if (t0 > 0) tl0 = (float)t0 * 1.0001f + 1e-5f;
             }
             h = trace4_ww<kRayTopLds, kCount, kTop, MCPT_FILTER_MIS>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
-                                                    stack + threadIdx.x, kRayBlock, &visits, &tests, top, tl0);
+                                                    stack + threadIdx.x, kRayBlock, &visits, &tests, top, tl0, &witer, &wleaf);
         }
         f = h.f;
         beta = h.beta;
@@ -3148,6 +3166,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
     }
     if (kCount) {
         wave_count2(cnt, visits, cnt + 1, tests);
+        if (MCPT_TRACE_DIAG) wave_count2(cnt + 6, witer, cnt + 7, wleaf);
         if (i >= n) return;
     }
     // only a traced set's slots are written (its consumers test the node's flags first), and (beta,
@@ -3718,6 +3737,9 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
 constexpr int kBrdfTop = MCPT_BRDF_TOP;
 constexpr int kBrdfBlock = kBrdfTop > 0 ? 256 : kTraceBlock;
 constexpr int kBrdfLds = kBrdfTop > 0 ? 8 : kRayLds;
+#ifndef MCPT_BRDF_TIMING
+#define MCPT_BRDF_TIMING 0  // A/B only: 1 = sampling twice, 2 = traversal twice (cost shares, timing builds)
+#endif
 #ifndef MCPT_BRDF_WAVES
 #define MCPT_BRDF_WAVES 5  // 96 VGPRs (10 spilled): 4 -> 5 waves/SIMD, +5% BRDF-only (profiles/round2b_ab_brdf.txt)
 #endif
@@ -3745,7 +3767,7 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
         p = ld3(cur.p, cur.cap, ii), N = ld3(cur.n, cur.cap, ii), wo = ld3(cur.wo, cur.cap, ii), tp = ld3(cur.tp, cur.cap, ii);
     }
     bool c = false;
-    unsigned traced = 0, visits = 0, tests = 0;
+    unsigned traced = 0, visits = 0, tests = 0, witer = 0, wleaf = 0;
     Hit h{-1, 0, 0, 0};
     d3 wi = mk3(0, 0, 0), tpc = mk3(0, 0, 0);
     if (active) {
@@ -3755,6 +3777,14 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
         const double sh = m[6];
         double pdf;
         wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+#if MCPT_BRDF_TIMING == 1  // timing-only build: the sampling and shading run twice (cost share of that region)
+        {
+            double pdf2;
+            const d3 wi2 = sample_phong(N, wo, kd, ks, sh, counter_u(key, 7), counter_u(key, 8), counter_u(key, 9), &pdf2);
+            const d3 b2 = brdf_phong(N, wi2, wo, kd, ks, sh);
+            if (P.mode == 12345) wi = wi2, pdf = pdf2 + b2.x;
+        }
+#endif
         if (!(dot(wi, N) < 0)) {
             traced = 1;
             // the child's throughput does not depend on the hit: computed before the traversal, so
@@ -3762,13 +3792,21 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
             const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
             tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
             h = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
-                                                      &tests, top);
+                                                      &tests, top, FLT_MAX, &witer, &wleaf);
+#if MCPT_BRDF_TIMING == 2  // timing-only build: the traversal runs twice
+            {
+                const Hit h2 = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x,
+                                                                                    kBrdfBlock, &visits, &tests, top);
+                if (P.mode == 12345) h = h2;
+            }
+#endif
             c = h.f >= 0;
         }
     }
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
     block_count(ray_stats(P), traced);
     if (kCount) wave_count2(P.stats + 8, visits, P.stats + 9, tests);
+    if (kCount && MCPT_TRACE_DIAG) wave_count2(P.stats + 14, witer, P.stats + 15, wleaf);
 }
 
 // batch closest hit (test / FFI entry mcpt_closest_hit)
@@ -4955,6 +4993,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         stats->prep_launches = prep_launches;
         stats->prep_exact_nodes = hs[10];
         stats->prep_band_nodes = hs[11];
+#if MCPT_TRACE_DIAG
+        if (hs[8])
+            fprintf(stderr, "trace diag: %llu visits over %llu wave node-iterations (lane use %.3f), %llu tests over %llu wave "
+                            "leaf-iterations (lane use %.3f)\n", hs[8], hs[14], hs[8] / (64.0 * std::max<unsigned long long>(hs[14], 1)),
+                    hs[9], hs[15], hs[9] / (64.0 * std::max<unsigned long long>(hs[15], 1)));
+#endif
 #if MCPT_BAND_DIAG
         fprintf(stderr, "exact diag (10 ns ticks summed over nodes): lists %llu literal %llu lists+literal+sum %llu pick %llu\n",
                 hs[12], hs[13], hs[14], hs[15]);
