@@ -16,8 +16,16 @@ enum {
     MCPT_DEBUG_SPLIT_BRDF = 1 << 16,
     MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17,
     MCPT_DEBUG_COUNT_TRAVERSAL = 1 << 18,
-    MCPT_DEBUG_SHARD_RANKS = 1 << 19
+    MCPT_DEBUG_SHARD_RANKS = 1 << 19,
+    MCPT_DEBUG_RAYS_CW8 = 1 << 20,
+    MCPT_DEBUG_RAYS_BVH4 = 1 << 21
 };
+/* MCPT_DEBUG_RAYS_CW8: the MIS / shade ray sets of every scene go through the persistent 8-wide traversal
+ * (k_rays_cw8), which by default serves only trees beyond an XCD's L2 -- parity tests run it on the small
+ * stand-in.  MCPT_DEBUG_RAYS_BVH4: trees beyond L2 keep the 4-wide persistent kernel (k_rays_persistent),
+ * the A/B baseline of k_rays_cw8.  mcpt_closest_hit flag MCPT_DEBUG_HIT_CW8: trace the batch through the
+ * 8-wide trees (one ray per thread, k_rays_cw8's traversal). */
+enum { MCPT_DEBUG_HIT_CW8 = 1 << 8 };
 /* MCPT_DEBUG_COUNT_TRAVERSAL runs the traversal kernel's counting instance, which fills
  * mcpt_stats.node_visits / tri_tests (the events of the traversal roofline; slower, for untimed
  * replays).
@@ -68,6 +76,12 @@ int mcpt_debug_light_literal(mcpt_scene* scene, const double x1[3], const double
  * tup >= its t; 1 undecided.  Lets a CPU test check the bound's soundness against the fp64 test. */
 int mcpt_debug_tri_filter(int32_t n, const float* tri, const double* ro, const double* rd, const float* tlim,
                           int32_t* verdict, float* tup);
+
+/* diagnostics (host only): checks the 8-wide compressed tree of the scene (light_only: the light-only tree)
+ * against its binary tree.  out[6] = nodes reached, triangles reached, facets of the binary tree,
+ * facets reached more than once, errors (bad indices, or a triangle vertex outside the decoded box of a slot
+ * on its path), depth. */
+int mcpt_debug_bvh8_check(mcpt_scene* scene, int32_t light_only, int64_t out[6]);
 
 #ifdef __cplusplus
 }

@@ -64,6 +64,9 @@ RENDER_FRESH_PDF = 2  # shade_with_mis: the node's own light pdf instead of the 
 RENDER_PRECISION_FP32 = 4  # opt-in FP32_STABLE light prep (packed-fp32 weights, fp64 sums); default FP64_LIGHT
 DEBUG_SPLIT_BRDF, DEBUG_NO_ROOT_CACHE, DEBUG_COUNT_TRAVERSAL = 1 << 16, 1 << 17, 1 << 18  # include/mcpt_debug.h
 DEBUG_SHARD_RANKS = 1 << 19  # device lists: every entry its own communicator rank (tests/collshim)
+DEBUG_RAYS_CW8 = 1 << 20  # MIS / shade ray sets through the persistent 8-wide traversal on every scene
+DEBUG_RAYS_BVH4 = 1 << 21  # trees beyond L2 keep the 4-wide persistent traversal (A/B baseline of k_rays_cw8)
+DEBUG_HIT_CW8 = 1 << 8  # mcpt_closest_hit: trace through the 8-wide trees
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_uint64)
@@ -94,7 +97,7 @@ EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_cre
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
 DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter", "mcpt_debug_light_prep_exact", "mcpt_debug_light_literal",
-                 "mcpt_debug_set_collective_lib"]  # include/mcpt_debug.h
+                 "mcpt_debug_set_collective_lib", "mcpt_debug_bvh8_check"]  # include/mcpt_debug.h
 
 
 def lib():
@@ -143,7 +146,8 @@ def lib():
                "mcpt_debug_tri_filter": [I, fp, dp, dp, fp, ip, fp],
                "mcpt_debug_light_prep_exact": [P, I, dp, dp, dp, dp, ip, ip],
                "mcpt_debug_light_literal": [P, dp, dp, dp],
-               "mcpt_debug_set_collective_lib": [C.c_char_p]}
+               "mcpt_debug_set_collective_lib": [C.c_char_p],
+               "mcpt_debug_bvh8_check": [P, I, np.ctypeslib.ndpointer(np.int64, flags="C")]}
         for name, argt in dbg.items():
             if hasattr(L, name):
                 getattr(L, name).argtypes = argt
@@ -329,14 +333,15 @@ def render_device(scene, camera, spp, dev_ptr, mode="mis", seed=DEFAULT_SEED, sa
     return st
 
 
-def closest_hit(scene, ro, rd, exclude=None, light_only=False, grid=False):
+def closest_hit(scene, ro, rd, exclude=None, light_only=False, grid=False, wide=False):
     """Myobj::closet_ray_intersect (Myobj.cpp:334) / ..._light_triangle (:476) for a batch of rays.
-    grid=True traverses the reference's uniform grid of Scene.meshing (crack included), else the BVH."""
+    grid=True traverses the reference's uniform grid of Scene.meshing (crack included), else the BVH;
+    wide=True (diagnostics) the 8-wide compressed BVH of the persistent traversal (k_rays_cw8)."""
     ro, rd = _d(ro, (-1, 3)), _d(rd, (-1, 3))
     n = ro.shape[0]
     ex = np.full(n, -1, np.int32) if exclude is None else np.ascontiguousarray(exclude, np.int32)
     f, tbg = np.zeros(n, np.int32), np.zeros((n, 3))
-    flags = (HIT_LIGHT_ONLY if light_only else 0) | (HIT_GRID if grid else 0)
+    flags = (HIT_LIGHT_ONLY if light_only else 0) | (HIT_GRID if grid else 0) | (DEBUG_HIT_CW8 if wide else 0)
     _check(lib().mcpt_closest_hit(scene.h, n, ro, rd, ex, flags, f, tbg))
     return f, tbg
 
@@ -365,6 +370,14 @@ def debug_light_literal(scene, x1, normal):
     out = np.zeros((scene.nlights, 20))
     _check(lib().mcpt_debug_light_literal(scene.h, _d(x1, (3,)), _d(normal, (3,)), out.reshape(-1)))
     return out
+
+
+def debug_bvh8_check(scene, light_only=False):
+    """Diagnostics (host only): the 8-wide tree against its binary tree (include/mcpt_debug.h).  Returns dict
+    nodes, tris, facets, duplicates, errors, depth."""
+    out = np.zeros(6, np.int64)
+    _check(lib().mcpt_debug_bvh8_check(scene.h, 1 if light_only else 0, out))
+    return dict(zip(("nodes", "tris", "facets", "duplicates", "errors", "depth"), (int(v) for v in out)))
 
 
 def debug_tri_filter(tri, ro, rd, tlim=None):

@@ -351,4 +351,213 @@ std::vector<BvhNode4Q> quantize_bvh4(const std::vector<BvhNode4>& in) {
     return out;
 }
 
+// ---- 8-wide compressed tree (BvhNode8Q) ----
+namespace {
+struct BN {  // binary node with its own box: inner (l, r >= 0) or leaf (first, count <= 2 after splitting)
+    float lo[3], hi[3];
+    int32_t l = -1, r = -1;
+    int32_t first = 0, count = 0;
+};
+struct Bvh8Builder {
+    const HostScene& s;
+    const Bvh& b;
+    double margin = 0;
+    std::vector<BN> bn;
+    Bvh8 out;
+    Bvh8Builder(const HostScene& s_, const Bvh& b_) : s(s_), b(b_) {}
+
+    // box of leaf slots [first, first + count): the triangles' float vertices, enlarged like Builder::to_float_box
+    void leaf_box(int32_t first, int32_t count, float* lo, float* hi) const {
+        double l[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, h[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int32_t i = first; i < first + count; i++) {
+            const float* v = &s.pos[9 * (size_t)b.leaf_facets[i]];
+            for (int k = 0; k < 3; k++)
+                for (int c = 0; c < 3; c++) l[c] = std::min(l[c], (double)v[3 * k + c]), h[c] = std::max(h[c], (double)v[3 * k + c]);
+        }
+        for (int c = 0; c < 3; c++) {
+            lo[c] = std::nextafter(static_cast<float>(l[c] - margin), -FLT_MAX);
+            hi[c] = std::nextafter(static_cast<float>(h[c] + margin), FLT_MAX);
+        }
+    }
+    // a leaf of the binary tree (box as stored there); more than two triangles: index halves, boxes of their own
+    int32_t leaf(int32_t first, int32_t count, const float* lo, const float* hi) {
+        const int32_t me = (int32_t)bn.size();
+        bn.push_back(BN{});
+        for (int c = 0; c < 3; c++) bn[me].lo[c] = lo[c], bn[me].hi[c] = hi[c];
+        if (count <= 2) {
+            bn[me].first = first, bn[me].count = count;
+            return me;
+        }
+        const int32_t h = count / 2;
+        float l0[3], h0[3], l1[3], h1[3];
+        leaf_box(first, h, l0, h0);
+        leaf_box(first + h, count - h, l1, h1);
+        const int32_t a = leaf(first, h, l0, h0), c = leaf(first + h, count - h, l1, h1);
+        bn[me].l = a, bn[me].r = c;
+        return me;
+    }
+    // child k of binary node ni, or -1 for the single-leaf root's empty slot
+    int32_t conv(int32_t ni, int k) {
+        const BvhNode& nd = b.nodes[ni];
+        if (nd.child[k] < 0 && nd.count[k] == 0) return -1;
+        if (nd.child[k] < 0) return leaf(~nd.child[k], nd.count[k], nd.lo[k], nd.hi[k]);
+        const int32_t me = (int32_t)bn.size();
+        bn.push_back(BN{});
+        for (int c = 0; c < 3; c++) bn[me].lo[c] = nd.lo[k][c], bn[me].hi[c] = nd.hi[k][c];
+        const int32_t a = conv(nd.child[k], 0), c = conv(nd.child[k], 1);
+        bn[me].l = a, bn[me].r = c;
+        return me;
+    }
+    static double area(const BN& x) { return box_area(x.lo, x.hi); }
+
+    // fills node `self` from the children of binary node `root` (collapsed up to eight)
+    void node(int32_t root, int32_t self) {
+        std::vector<int32_t> cand;
+        for (int32_t c : {bn[root].l, bn[root].r})
+            if (c >= 0) cand.push_back(c);
+        while (cand.size() < 8) {  // expand the largest-area inner candidate (as collapse_bvh4)
+            int best = -1;
+            double ba = -1;
+            for (size_t i = 0; i < cand.size(); i++)
+                if (bn[cand[i]].l >= 0 && area(bn[cand[i]]) > ba) ba = area(bn[cand[i]]), best = (int)i;
+            if (best < 0) break;
+            const int32_t in = cand[best];
+            cand.erase(cand.begin() + best);
+            for (int32_t c : {bn[in].l, bn[in].r})
+                if (c >= 0) cand.push_back(c);
+        }
+        // octant slots: greedy over (child, slot) by the child centre's offset from the node centre along
+        // the slot's direction (bit a set: -a)
+        double nlo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, nhi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int32_t c : cand)
+            for (int a = 0; a < 3; a++) nlo[a] = std::min(nlo[a], (double)bn[c].lo[a]), nhi[a] = std::max(nhi[a], (double)bn[c].hi[a]);
+        int32_t slot_of[8];
+        for (int k = 0; k < 8; k++) slot_of[k] = -1;  // child at slot
+        std::vector<bool> placed(cand.size(), false);
+        for (size_t it = 0; it < cand.size(); it++) {
+            double bs = -DBL_MAX;
+            int bc = -1, bsl = -1;
+            for (size_t i = 0; i < cand.size(); i++) {
+                if (placed[i]) continue;
+                for (int sl = 0; sl < 8; sl++) {
+                    if (slot_of[sl] >= 0) continue;
+                    double sc = 0;
+                    for (int a = 0; a < 3; a++) {
+                        const double off = 0.5 * ((double)bn[cand[i]].lo[a] + bn[cand[i]].hi[a]) - 0.5 * (nlo[a] + nhi[a]);
+                        sc += ((sl >> a) & 1) ? -off : off;
+                    }
+                    if (sc > bs) bs = sc, bc = (int)i, bsl = sl;
+                }
+            }
+            placed[bc] = true;
+            slot_of[bsl] = (int32_t)bc;
+        }
+        // inner children contiguous in slot order; leaf triangles at base_tri + 2 slot + j
+        int ninner = 0, kmin = 8, kmax = -1;
+        for (int sl = 0; sl < 8; sl++) {
+            if (slot_of[sl] < 0) continue;
+            const BN& c = bn[cand[slot_of[sl]]];
+            if (c.l >= 0) ninner++;
+            else kmin = std::min(kmin, sl), kmax = std::max(kmax, sl);
+        }
+        // inner children at base_inner + slot (eight node slots reserved per node with inner children, the
+        // unused ones never referenced): a stack entry is then (base, hit bits) in one word
+        const int32_t base_inner = ninner > 0 ? (int32_t)out.nodes.size() : 0;
+        if (ninner > 0) out.nodes.resize(out.nodes.size() + 8);
+        int32_t base_tri = 0;
+        uint32_t tvalid = 0, imask = 0;
+        if (kmax >= 0) {
+            const int32_t at = (int32_t)out.tri_facets.size();
+            out.tri_facets.resize(out.tri_facets.size() + 2 * (kmax - kmin + 1), -1);
+            base_tri = at - 2 * kmin;
+        }
+        std::vector<std::pair<int32_t, int32_t>> todo;  // (binary node, node index)
+        for (int sl = 0; sl < 8; sl++) {
+            if (slot_of[sl] < 0) continue;
+            const BN& c = bn[cand[slot_of[sl]]];
+            if (c.l >= 0) {
+                imask |= 1u << sl;
+                todo.emplace_back(cand[slot_of[sl]], base_inner + sl);
+            } else {
+                for (int j = 0; j < c.count; j++) {
+                    out.tri_facets[base_tri + 2 * sl + j] = b.leaf_facets[c.first + j];
+                    tvalid |= 1u << (2 * sl + j);
+                }
+            }
+        }
+        // quantized planes (as quantize_bvh4): per axis the union minimum and the smallest power-of-two
+        // scale whose 255 steps reach the maximum, each plane rounded outward in the decode arithmetic
+        BvhNode8Q o;
+        std::memset(&o, 0, sizeof(o));
+        for (int a = 0; a < 3; a++) {
+            float lo = FLT_MAX, hi = -FLT_MAX;
+            for (int sl = 0; sl < 8; sl++)
+                if (slot_of[sl] >= 0) lo = std::min(lo, bn[cand[slot_of[sl]]].lo[a]), hi = std::max(hi, bn[cand[slot_of[sl]]].hi[a]);
+            if (lo > hi) lo = hi = 0.0f;
+            o.org[a] = lo;
+            const double ext = (double)hi - (double)lo;
+            int e = ext > 0 ? std::max(1, std::min(254, (int)std::ceil(std::log2(ext / 255.0)) + 127 - 1)) : 1;
+            uint32_t ql[2], qh[2];
+            for (;; e++) {
+                if (e > 254) e = 254;
+                bool ok = decode_plane(255, e, lo) >= hi || e == 254;
+                ql[0] = ql[1] = qh[0] = qh[1] = 0;
+                for (int sl = 0; ok && sl < 8; sl++) {
+                    const int h = sl >> 2, sh = 8 * (sl & 3);
+                    if (slot_of[sl] < 0) {
+                        ql[h] |= 255u << sh;  // empty slot (the traversal masks it out)
+                        continue;
+                    }
+                    const BN& c = bn[cand[slot_of[sl]]];
+                    const double scale = std::ldexp(1.0, e - 127);
+                    int q0 = std::max(0, std::min(255, (int)std::floor(((double)c.lo[a] - lo) / scale)));
+                    while (q0 > 0 && decode_plane(q0, e, lo) > c.lo[a]) q0--;
+                    int q1 = std::max(0, std::min(255, (int)std::ceil(((double)c.hi[a] - lo) / scale)));
+                    while (q1 < 255 && decode_plane(q1, e, lo) < c.hi[a]) q1++;
+                    if (decode_plane(q0, e, lo) > c.lo[a] || decode_plane(q1, e, lo) < c.hi[a]) {
+                        ok = false;
+                        break;
+                    }
+                    ql[h] |= (uint32_t)q0 << sh;
+                    qh[h] |= (uint32_t)q1 << sh;
+                }
+                if (ok || e == 254) break;
+            }
+            o.ex |= (uint32_t)e << (8 * a);
+            o.qlo[a][0] = ql[0], o.qlo[a][1] = ql[1];
+            o.qhi[a][0] = qh[0], o.qhi[a][1] = qh[1];
+        }
+        o.ex |= imask << 24;
+        o.base_inner = base_inner;
+        o.base_tri = base_tri;
+        o.tvalid = tvalid;
+        out.nodes[self] = o;
+        for (auto& t : todo) node(t.first, t.second);
+    }
+};
+}  // namespace
+
+Bvh8 build_bvh8(const HostScene& s, const Bvh& b) {
+    Bvh8Builder B(s, b);
+    double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    for (int32_t f : b.leaf_facets)
+        for (int k = 0; k < 9; k++) lo[k % 3] = std::min(lo[k % 3], (double)s.pos[9 * (size_t)f + k]), hi[k % 3] = std::max(hi[k % 3], (double)s.pos[9 * (size_t)f + k]);
+    double ext = 0;
+    for (int c = 0; c < 3; c++) ext = std::max(ext, hi[c] - lo[c]);
+    B.margin = 1e-5 * ext + 1e-6;  // Builder::margin of the same facets
+    B.out.nodes.resize(1);
+    if (b.nodes.empty() || b.leaf_facets.empty()) {  // no facets: a root without children
+        std::memset(&B.out.nodes[0], 0, sizeof(BvhNode8Q));
+        return B.out;
+    }
+    BN root;
+    root.l = -1, root.r = -1;
+    B.bn.push_back(root);
+    const int32_t a = B.conv(0, 0), c = B.conv(0, 1);
+    B.bn[0].l = a, B.bn[0].r = c;
+    if (B.bn[0].l < 0) std::swap(B.bn[0].l, B.bn[0].r);
+    B.node(0, 0);
+    return B.out;
+}
+
 }  // namespace mcpt

@@ -84,6 +84,34 @@ std::vector<BvhNode4Q> quantize_bvh4(const std::vector<BvhNode4>& in);
 // four children); leaves and leaf slots are shared with the binary tree
 std::vector<BvhNode4> collapse_bvh4(const Bvh& b);
 
+// 8-wide compressed node (128 B, one cache line) for the wide traversal (k_rays_cw8), after Ylitie, Karras &
+// Laine's compressed wide BVH (HPG 2017), adapted: the same conservative byte planes as BvhNode4Q for eight
+// children, children ordered by OCTANT -- slot s holds the child whose centre lies on the negative side of
+// the node centre along axis a iff bit a of s is set (greedy assignment) -- so that a ray visits hit
+// children in (slot XOR its octant code) order, near to far, with no sort; inner child s at node base + s
+// (eight node slots reserved per node with inner children: a stack entry is (base << 8 | hit bits), no
+// child code needs loading) and each leaf child's <= 2 triangles at fixed triangle slots (a triangle
+// group is a base and a 16-bit mask).  Binary leaves with more than two triangles are split (by index
+// halves) before the collapse.
+struct BvhNode8Q {
+    float org[3];
+    uint32_t ex;           // bytes 0-2: biased fp32 exponent of axis a's scale; byte 3: imask (slots of inner children)
+    uint32_t qlo[3][2];    // qlo[a][h]: byte k = lo plane of child 4 h + k on axis a (plane = fma(q, 2^(e - 127), org))
+    uint32_t qhi[3][2];
+    int32_t base_inner;    // inner child of slot s: node base_inner + s
+    int32_t base_tri;      // triangle j (0, 1) of leaf child s: triangle slot base_tri + 2 s + j
+    uint32_t tvalid;       // bit 2 s + j: that triangle slot holds a triangle
+    uint32_t pad[13];
+};
+static_assert(sizeof(BvhNode8Q) == 128, "BvhNode8Q must be 128 B");
+struct Bvh8 {
+    std::vector<BvhNode8Q> nodes;      // node 0 = root
+    std::vector<int32_t> tri_facets;   // facet of each triangle slot (-1: unused)
+};
+// the 8-wide tree of a binary BVH built by build_bvh over the same facets (boxes conservative: every decoded
+// child box contains the fp32 box the binary tree holds for it, or its triangles' for a split leaf)
+Bvh8 build_bvh8(const HostScene& s, const Bvh& b);
+
 // grid.cpp -- the reference's uniform grid (Myobj.cpp:78-162) for the MCPT_ACCEL_GRID mode
 struct Grid {
     bool ok = false;

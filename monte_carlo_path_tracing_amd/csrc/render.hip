@@ -34,6 +34,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -93,6 +94,12 @@ struct DScene {
     const BvhNode4Q* lbvh4q;
     int nbvh4, nlbvh4;        // node counts
     const float4* lleaf_v;
+    // 8-wide compressed trees (BvhNode8Q, k_rays_cw8) and their triangle slots (3 float4 each, w of the
+    // first = facet id bits; unused slots are never read); null when a tree does not fit the 24-bit base
+    const BvhNode8Q* bvh8;
+    const BvhNode8Q* lbvh8;
+    const float4* tri8_v;
+    const float4* ltri8_v;
     // select_a_point_from_lights (MCPT_MODE_SHADE_AREA): the lightsRadiance map in name order --
     // RadianceRGB::sum() per light and its running sum, the light-table run of its triangles -- and
     // the triangles' areas (Mylight.cpp:66-69) with their running sum within their light
@@ -488,6 +495,107 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     if (kFilter && pend1 >= 0) exact(pend1);
     return best;
 }
+
+// ---- 8-wide traversal over BvhNode8Q (the compressed wide BVH, mcpt_internal.h) ----
+// Per lane: a node group (nb << 8 | the hit bits of the node's inner children in near-to-far order: the
+// bit of slot s at position s ^ oct, oct = the octant code of the ray's direction, so that the lowest bit
+// is the nearest child), a triangle group (base triangle slot tb, 16-bit mask tw) and a stack of node
+// groups (one word each).  No sorting and no child codes to load: child = base + slot.  Closest hit by the
+// reference's fp64 test (Myobj.cpp:165-192) with ties to the lower facet id, on conservatively pruned
+// boxes -- the same hits as trace4_ww, visited in another order.
+struct Cw8Frame {  // per-ray constants of the slab tests
+    float inv[3], oi[3];
+    unsigned oct;  // bit a set iff the ray goes +a: near children (negative side) come first
+};
+__device__ inline Cw8Frame cw8_frame(d3 ro, d3 rd) {
+    Cw8Frame F;
+    auto inv = [](double d) {
+        float f = (float)d;
+        if (fabsf(f) < 1e-30f) f = copysignf(1e-30f, f);
+        return 1.0f / f;
+    };
+    F.inv[0] = inv(rd.x), F.inv[1] = inv(rd.y), F.inv[2] = inv(rd.z);
+    F.oi[0] = (float)ro.x * F.inv[0], F.oi[1] = (float)ro.y * F.inv[1], F.oi[2] = (float)ro.z * F.inv[2];
+    F.oct = (F.inv[0] < 0 ? 0u : 1u) | (F.inv[1] < 0 ? 0u : 2u) | (F.inv[2] < 0 ? 0u : 4u);
+    return F;
+}
+// one node visit: the eight children's slab tests on the decoded byte planes (near / far planes picked per
+// axis by the direction's sign, as node_tplanes), then the new node group (inner hits in key order) and
+// triangle group (leaf hits spread over their two triangle slots, masked by the used slots)
+__device__ inline void cw8_visit(const BvhNode8Q* __restrict__ nd, const Cw8Frame& F, float tlimit, unsigned* ng, int* tb,
+                                 unsigned* tw) {
+    const float4 v0 = *reinterpret_cast<const float4*>(nd->org);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(&nd->qlo[0][0]);
+    const uint4 v2 = *reinterpret_cast<const uint4*>(&nd->qlo[2][0]);
+    const uint4 v3 = *reinterpret_cast<const uint4*>(&nd->qhi[1][0]);
+    const int4 v4 = *reinterpret_cast<const int4*>(&nd->base_inner);
+    const unsigned ex = __float_as_uint(v0.w);
+    const float org[3] = {v0.x, v0.y, v0.z};
+    const unsigned ql[3][2] = {{v1.x, v1.y}, {v1.z, v1.w}, {v2.x, v2.y}};
+    const unsigned qh[3][2] = {{v2.z, v2.w}, {v3.x, v3.y}, {v3.z, v3.w}};
+    float m[3], b[3];
+    unsigned qn[3][2], qf[3][2];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        m[a] = __uint_as_float(((ex >> (8 * a)) & 0xffu) << 23) * F.inv[a];
+        b[a] = fmaf(org[a], F.inv[a], -F.oi[a]);
+        const bool neg = F.inv[a] < 0;
+#pragma unroll
+        for (int h = 0; h < 2; h++) qn[a][h] = neg ? qh[a][h] : ql[a][h], qf[a][h] = neg ? ql[a][h] : qh[a][h];
+    }
+    unsigned hit = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int h = k >> 2, sh = 8 * (k & 3);
+        float tn[3], tf[3];
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            tn[a] = fmaf((float)((qn[a][h] >> sh) & 0xffu), m[a], b[a]);
+            tf[a] = fmaf((float)((qf[a][h] >> sh) & 0xffu), m[a], b[a]);
+        }
+        const float t0 = fmaxf(fmaxf(tn[0], tn[1]), fmaxf(tn[2], 0.0f));
+        const float t1 = fminf(fminf(tf[0], tf[1]), fminf(tf[2], tlimit));
+        hit |= (t0 <= fmaf(t1, 1.00001f, 1e-6f)) ? 1u << k : 0u;
+    }
+    const unsigned imask = ex >> 24;
+    unsigned ih = hit & imask;  // slot s -> bit s ^ oct
+    ih = (F.oct & 1) ? ((ih & 0x55u) << 1) | ((ih >> 1) & 0x55u) : ih;
+    ih = (F.oct & 2) ? ((ih & 0x33u) << 2) | ((ih >> 2) & 0x33u) : ih;
+    ih = (F.oct & 4) ? ((ih & 0x0fu) << 4) | ((ih >> 4) & 0x0fu) : ih;
+    *ng = ((unsigned)v4.x << 8) | ih;
+    unsigned lh = hit & ~imask & 0xffu;  // slot s -> triangle slots 2 s, 2 s + 1
+    lh = (lh | (lh << 4)) & 0x0f0fu;
+    lh = (lh | (lh << 2)) & 0x3333u;
+    lh = (lh | (lh << 1)) & 0x5555u;
+    *tb = v4.y;
+    *tw = (lh | (lh << 1)) & (unsigned)v4.z;
+}
+// the next child of a node group (its nearest remaining hit), removed from the group
+__device__ inline int cw8_next(unsigned* ng, unsigned oct) {
+    const unsigned bit = (unsigned)__builtin_ctz(*ng & 0xffu);
+    *ng &= ~(1u << bit);
+    return (int)((*ng >> 8) + (bit ^ oct));
+}
+// the reference's fp64 test of triangle slot q against the best hit so far (origin facet excluded)
+__device__ inline void cw8_tri(const float4* __restrict__ triv, int q, d3 ro, d3 rd, int excl, Hit* best, float* tlimit) {
+    const float4 a4 = triv[3 * q], b4 = triv[3 * q + 1], c4 = triv[3 * q + 2];
+    const int fac = __float_as_int(a4.w);
+    if (fac == excl) return;
+    const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
+    const double detA = det3(ab, ac, rd);
+    if (fabs(detA) < MCPT_EPS) return;
+    const double nb = det3(ar, ac, rd), ng = det3(ab, ar, rd), nt = det3(ab, ac, ar);
+    const bool neg = detA < 0;
+    if ((nb != 0 && ((nb < 0) != neg)) || (ng != 0 && ((ng < 0) != neg)) || (nt != 0 && ((nt < 0) != neg))) return;
+    const double beta = nb / detA, gamma = ng / detA, tt = nt / detA;
+    if (beta < 0 || gamma < 0 || beta + gamma > 1 || tt < 0 || fabs(tt) < MCPT_EPS) return;
+    if (tt < best->t || (tt == best->t && fac < best->f)) {
+        *best = Hit{fac, tt, beta, gamma};
+        *tlimit = fminf(*tlimit, (float)tt * 1.0001f + 1e-5f);
+    }
+}
+// the root's node group: its only "child" is node 0 (slot 0, bit oct)
+__device__ inline unsigned cw8_root(unsigned oct) { return 1u << oct; }
 
 // The picked triangle's spherical triangle for Arvo's sampler (Mylight.cpp:453-461): the reference's
 // literal chain (light_tri_stage -- sqrt / division unit vectors, correctly rounded acos for
@@ -3417,6 +3525,130 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
     if (kCount) wave_count2(cnt, visits, cnt + 1, tests);
 }
 
+// k_rays_persistent over the 8-wide compressed trees (BvhNode8Q): the same refilling persistent waves,
+// pool and hit slots; a round is, for every lane in flight, node visits until the lane holds a triangle
+// group (while-while: the wave descends until every lane does or has run out of nodes), then that group's
+// triangles.  Hits are bit-identical to k_rays_persistent / k_mis_rays (same tests, same total order on
+// (t, facet), conservative boxes); visits and their order differ.
+#ifndef MCPT_RAYS_CW8
+#define MCPT_RAYS_CW8 1  // 0: k_rays_persistent (4-wide) for the scenes beyond L2 (A/B)
+#endif
+#ifndef MCPT_CW8_WAVES
+#define MCPT_CW8_WAVES 6
+#endif
+template <bool kCount = false>
+__global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S, Queue cur, int n, Aux A, int first_set, int nsets,
+                                                                  unsigned* __restrict__ pool, unsigned long long* cnt = nullptr,
+                                                                  int seeded = 0) {
+    __shared__ unsigned stack[kPersistLds * kRayBlock];
+    unsigned* __restrict__ lds = stack + threadIdx.x;
+    constexpr int stride = kRayBlock;
+    const int lane = threadIdx.x & 63;
+    const unsigned total = (unsigned)nsets * (unsigned)n;
+    unsigned spill[kStack - kPersistLds];
+    unsigned visits = 0, tests = 0;
+    bool busy = false, exhausted = false;
+    unsigned wnext = 0, wend = 0;
+    int set = 0, ii = 0, excl = -1;
+    d3 ro = mk3(0, 0, 0), rd = mk3(0, 0, 0);
+    Cw8Frame F{};
+    float tlimit = FLT_MAX;
+    unsigned ng = 0, tw = 0;
+    int tb = 0, sp = 0;
+    Hit best{-1, DBL_MAX, 0, 0};
+    auto push = [&](unsigned v) {
+        if (sp < kPersistLds) lds[sp * stride] = v;
+        else if (sp < kStack) spill[sp - kPersistLds] = v;
+        sp = sp < kStack ? sp + 1 : sp;
+    };
+    auto pop = [&]() -> unsigned {
+        --sp;
+        return sp < kPersistLds ? lds[sp * stride] : spill[sp - kPersistLds];
+    };
+    auto finish = [&]() {
+        const size_t o = (size_t)set * A.cap + ii;
+        A.hf[o] = best.f;
+        if (set < 2 && best.f >= 0) {
+            A.hbg[2 * o] = best.beta;
+            A.hbg[2 * o + 1] = best.gamma;
+        }
+        busy = false;
+    };
+    while (true) {
+        while (!exhausted) {  // refill, as k_rays_persistent
+            const uint64_t idle = __ballot(!busy);
+            if (idle == 0 || (__popcll(idle) < kRefill && __ballot(busy) != 0)) break;
+            if (wnext >= wend) {
+                unsigned base = 0;
+                if (lane == 0) base = atomicAdd(pool, (unsigned)kRayChunk);
+                base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+                if (base >= total) {
+                    exhausted = true;
+                    break;
+                }
+                wnext = base;
+                wend = min(base + (unsigned)kRayChunk, total);
+            }
+            const unsigned take = min((unsigned)__popcll(idle), wend - wnext);
+            const unsigned rk = (unsigned)lane_rank(idle);
+            const unsigned base = wnext;
+            wnext += take;
+            if (!busy && rk < take) {
+                const unsigned it = base + rk;
+                set = first_set + (int)(it / (unsigned)n);
+                ii = (int)(it % (unsigned)n);
+                best = Hit{-1, DBL_MAX, 0, 0};
+                if (A.flags[ii] & (1 << set)) {
+                    const double* d = set == 0 ? A.d1 : A.d2;
+                    ro = ld3(cur.p, cur.cap, ii);
+                    rd = ld3(d, A.cap, ii);
+                    excl = cur.f[ii];
+                    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) {  // reference: UB (Myobj.cpp:463-468)
+                        finish();
+                    } else {
+                        F = cw8_frame(ro, rd);
+                        tlimit = FLT_MAX;
+                        if (set == 0 && (seeded & 1)) {  // set 0: the light triangle's exact t (seed_light_t)
+                            const double t0 = A.hbg[2 * ((size_t)set * A.cap + ii)];
+                            if (t0 > 0) tlimit = (float)t0 * 1.0001f + 1e-5f;
+                        }
+                        ng = cw8_root(F.oct);
+                        tw = 0;
+                        sp = 0;
+                        busy = true;
+                    }
+                } else {
+                    busy = false;
+                }
+            }
+        }
+        if (__ballot(busy) == 0) break;  // pool exhausted and no ray in flight
+        if (busy) {
+            const BvhNode8Q* __restrict__ nodes = set == 2 ? S.lbvh8 : S.bvh8;
+            const float4* __restrict__ triv = set == 2 ? S.ltri8_v : S.tri8_v;
+            while (true) {  // descend until every lane holds a triangle group or is out of nodes
+                const bool want = tw == 0 && ((ng & 0xffu) != 0 || sp > 0);
+                if (!__any(want)) break;
+                if (want) {
+                    if ((ng & 0xffu) == 0) ng = pop();
+                    const int child = cw8_next(&ng, F.oct);
+                    if (ng & 0xffu) push(ng);
+                    if (kCount) ++visits;
+                    cw8_visit(nodes + child, F, tlimit, &ng, &tb, &tw);
+                }
+            }
+            while (tw != 0) {
+                const int bit = __builtin_ctz(tw);
+                tw &= tw - 1;
+                if (kCount) ++tests;
+                cw8_tri(triv, tb + bit, ro, rd, excl, &best, &tlimit);
+            }
+            if ((ng & 0xffu) == 0 && sp == 0) finish();
+        }
+    }
+    if (kCount) wave_count2(cnt, visits, cnt + 1, tests);
+}
+
 template <bool kStale>
 __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
@@ -3827,6 +4059,57 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_batch(DScene S, int n, co
     tbg[3 * i + 2] = h.f >= 0 ? h.gamma : 0.0;
 }
 
+// batch closest hit through the 8-wide trees, one ray per thread (mcpt_closest_hit with MCPT_HIT_CW8,
+// include/mcpt_debug.h): the traversal of k_rays_cw8 for tests against the reference goldens
+__global__ __launch_bounds__(kTraceBlock) void k_trace_batch_cw8(DScene S, int n, const double* ro_, const double* rd_,
+                                                                const int* ex, int light_only, int* f_out, double* tbg) {
+    __shared__ unsigned stack[kRayLds * kTraceBlock];
+    unsigned* lds = stack + threadIdx.x;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const d3 ro = mk3(ro_[3 * i], ro_[3 * i + 1], ro_[3 * i + 2]), rd = mk3(rd_[3 * i], rd_[3 * i + 1], rd_[3 * i + 2]);
+    const BvhNode8Q* nodes = light_only ? S.lbvh8 : S.bvh8;
+    const float4* triv = light_only ? S.ltri8_v : S.tri8_v;
+    Hit best{-1, DBL_MAX, 0, 0};
+    if (!(isnan(rd.x) || isnan(rd.y) || isnan(rd.z))) {
+        unsigned spill[kStack - kRayLds];
+        int sp = 0;
+        const Cw8Frame F = cw8_frame(ro, rd);
+        float tlimit = FLT_MAX;
+        unsigned ng = cw8_root(F.oct), tw = 0;
+        int tb = 0;
+        while (true) {
+            while (true) {
+                const bool want = tw == 0 && ((ng & 0xffu) != 0 || sp > 0);
+                if (!__any(want)) break;
+                if (want) {
+                    if ((ng & 0xffu) == 0) {
+                        --sp;
+                        ng = sp < kRayLds ? lds[sp * kTraceBlock] : spill[sp - kRayLds];
+                    }
+                    const int child = cw8_next(&ng, F.oct);
+                    if (ng & 0xffu) {
+                        if (sp < kRayLds) lds[sp * kTraceBlock] = ng;
+                        else if (sp < kStack) spill[sp - kRayLds] = ng;
+                        sp = sp < kStack ? sp + 1 : sp;
+                    }
+                    cw8_visit(nodes + child, F, tlimit, &ng, &tb, &tw);
+                }
+            }
+            if (tw == 0) break;
+            while (tw != 0) {
+                const int bit = __builtin_ctz(tw);
+                tw &= tw - 1;
+                cw8_tri(triv, tb + bit, ro, rd, ex[i], &best, &tlimit);
+            }
+        }
+    }
+    f_out[i] = best.f;
+    tbg[3 * i] = best.f >= 0 ? best.t : 0.0;
+    tbg[3 * i + 1] = best.f >= 0 ? best.beta : 0.0;
+    tbg[3 * i + 2] = best.f >= 0 ? best.gamma : 0.0;
+}
+
 // ============================================================================================
 // host side
 // ============================================================================================
@@ -3869,6 +4152,7 @@ struct DeviceState {
 struct mcpt_scene {
     HostScene host;
     Bvh bvh, lbvh;
+    Bvh8 bvh8, lbvh8;  // 8-wide compressed trees of bvh / lbvh (k_rays_cw8)
     Grid grid;             // Myobj::cal_scene_boundingbox(eye) + meshing(n0) (mcpt_scene_meshing)
     int grid_version = 0;  // bumped by every rebuild; devices re-upload on mismatch
     std::vector<std::unique_ptr<DeviceState>> devs;
@@ -4167,6 +4451,23 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, quantize_bvh4(b4), &d.bvh4q))) return rc;
     if ((rc = upload(*D, quantize_bvh4(lb4), &d.lbvh4q))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
+    // the 8-wide trees (k_rays_cw8); a tree whose reserved node slots exceed the 24-bit stack base stays null
+    for (int t = 0; t < 2; t++) {
+        const Bvh8& b8 = t == 0 ? sc->bvh8 : sc->lbvh8;
+        if (b8.nodes.empty() || b8.nodes.size() >= (1u << 24)) continue;
+        std::vector<float4> tv8(3 * std::max<size_t>(b8.tri_facets.size(), 1), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t q = 0; q < b8.tri_facets.size(); q++) {
+            const int f = b8.tri_facets[q];
+            if (f < 0) continue;
+            for (int k = 0; k < 3; k++) {
+                float w;
+                std::memcpy(&w, &f, 4);
+                tv8[3 * q + k] = make_float4(s.pos[9 * f + 3 * k], s.pos[9 * f + 3 * k + 1], s.pos[9 * f + 3 * k + 2], k == 0 ? w : 0.0f);
+            }
+        }
+        if ((rc = upload(*D, b8.nodes, t == 0 ? &d.bvh8 : &d.lbvh8))) return rc;
+        if ((rc = upload(*D, tv8, t == 0 ? &d.tri8_v : &d.ltri8_v))) return rc;
+    }
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc(&D->pinned_count, 64 + kCtrlBytes));
     HIP_OK(hipEventCreate(&D->ev0));
@@ -4462,7 +4763,7 @@ int validate_render(const mcpt_render_opts* o) {
     }
     if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
                      MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL |
-                     MCPT_DEBUG_SHARD_RANKS)) {
+                     MCPT_DEBUG_SHARD_RANKS | MCPT_DEBUG_RAYS_CW8 | MCPT_DEBUG_RAYS_BVH4)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
@@ -4876,13 +5177,21 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const dim3 g256((ni + 255) / 256), b256(256);
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
     auto launch_rays = [&](int first_set, int nsets, int seeded) {
-        const bool pers = MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
+        const bool force_cw8 = (o->flags & MCPT_DEBUG_RAYS_CW8) != 0;
+        const bool pers = force_cw8 || MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
         if (pers && !grid) {
             unsigned* pool = (unsigned*)D.work.p + 8;
             (void)hipMemsetAsync(pool, 0, sizeof(unsigned), st);
             const long long items = (long long)nsets * ni;
             const int blocks = (int)std::max<long long>(1, std::min<long long>((items + kRayBlock - 1) / kRayBlock, 2048));
-            if (count_trav)
+            if ((force_cw8 || (MCPT_RAYS_CW8 && !(o->flags & MCPT_DEBUG_RAYS_BVH4))) && D.d.bvh8 && D.d.lbvh8) {
+                if (count_trav)
+                    hipLaunchKernelGGL(k_rays_cw8<true>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux, first_set, nsets,
+                                       pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
+                else
+                    hipLaunchKernelGGL(k_rays_cw8<false>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux, first_set, nsets,
+                                       pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
+            } else if (count_trav)
                 hipLaunchKernelGGL(k_rays_persistent<true>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux,
                                    first_set, nsets, pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);
             else
@@ -5496,6 +5805,8 @@ static int finish_scene(HostScene&& hs, mcpt_scene** out) {
     constexpr int kMaxLeaf = 2;
     sc->bvh = build_bvh(sc->host, all, kMaxLeaf);
     sc->lbvh = build_bvh(sc->host, lights, kMaxLeaf);
+    sc->bvh8 = build_bvh8(sc->host, sc->bvh);
+    sc->lbvh8 = build_bvh8(sc->host, sc->lbvh);
     *out = sc;
     return MCPT_OK;
 }
@@ -5741,7 +6052,9 @@ int mcpt_scene_grid_info(const mcpt_scene* sc, double* box_and_cell, int32_t* ce
 
 int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* rd, const int32_t* ex,
                      int32_t flags, int32_t* facet, double* tbg) {
-    if (!sc || n < 0 || (n && (!ro || !rd || !ex || !facet || !tbg)) || (flags & ~(MCPT_HIT_LIGHT_ONLY | MCPT_HIT_GRID))) {
+    if (!sc || n < 0 || (n && (!ro || !rd || !ex || !facet || !tbg)) ||
+        (flags & ~(MCPT_HIT_LIGHT_ONLY | MCPT_HIT_GRID | MCPT_DEBUG_HIT_CW8)) ||
+        ((flags & MCPT_HIT_GRID) && (flags & MCPT_DEBUG_HIT_CW8))) {
         set_error("invalid argument");
         return MCPT_E_INVALID;
     }
@@ -5768,8 +6081,17 @@ int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* 
     HIP_OK(hipMemcpy(dro, ro, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(drd, rd, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(dex, ex, 4ull * n, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(grid ? k_trace_batch<true> : k_trace_batch<false>, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d, n,
-                       (const double*)dro, (const double*)drd, (const int*)dex, light_only, (int*)df, (double*)dt);
+    if (flags & MCPT_DEBUG_HIT_CW8) {
+        if (!D->d.bvh8 || !D->d.lbvh8) {
+            set_error("MCPT_DEBUG_HIT_CW8: no 8-wide tree for this scene");
+            return MCPT_E_INVALID;
+        }
+        hipLaunchKernelGGL(k_trace_batch_cw8, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0, D->stream, D->d, n,
+                           (const double*)dro, (const double*)drd, (const int*)dex, light_only, (int*)df, (double*)dt);
+    } else {
+        hipLaunchKernelGGL(grid ? k_trace_batch<true> : k_trace_batch<false>, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), 0,
+                           D->stream, D->d, n, (const double*)dro, (const double*)drd, (const int*)dex, light_only, (int*)df, (double*)dt);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(facet, df, 4ull * n, hipMemcpyDeviceToHost));
@@ -5811,6 +6133,77 @@ int mcpt_debug_light_literal(mcpt_scene* sc, const double* x1, const double* nrm
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(out, dout, 160ull * NL, hipMemcpyDeviceToHost));
     (void)hipFree(dout);
+    return MCPT_OK;
+}
+
+// host-only check of an 8-wide tree (include/mcpt_debug.h): every facet of the binary tree is reached exactly
+// once, and every reached triangle's vertices lie inside the decoded box of every slot on its path (the
+// traversal prunes with those boxes, so this is what keeps its hits the binary tree's)
+int mcpt_debug_bvh8_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
+    if (!sc || !out) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    const Bvh8& b = light_only ? sc->lbvh8 : sc->bvh8;
+    const Bvh& bb = light_only ? sc->lbvh : sc->bvh;
+    const HostScene& hs = sc->host;
+    int64_t nodes = 0, tris = 0, dup = 0, bad = 0, maxd = 0;
+    std::vector<int> seen(hs.F, 0);
+    struct Box {
+        float lo[3], hi[3];
+    };
+    std::vector<Box> path;
+    auto decode = [](const BvhNode8Q& n, int a, int k, bool hi) {
+        const uint32_t w = hi ? n.qhi[a][k >> 2] : n.qlo[a][k >> 2];
+        const uint32_t bits = ((n.ex >> (8 * a)) & 0xffu) << 23;
+        float sc_;
+        std::memcpy(&sc_, &bits, 4);
+        return std::fmaf((float)((w >> (8 * (k & 3))) & 0xffu), sc_, n.org[a]);
+    };
+    std::function<void(int32_t, int)> walk = [&](int32_t ni, int depth) {
+        if (ni < 0 || (size_t)ni >= b.nodes.size()) {
+            bad++;
+            return;
+        }
+        nodes++;
+        maxd = std::max<int64_t>(maxd, depth);
+        const BvhNode8Q& n = b.nodes[ni];
+        const uint32_t imask = n.ex >> 24;
+        for (int k = 0; k < 8; k++) {
+            Box bx;
+            for (int a = 0; a < 3; a++) bx.lo[a] = decode(n, a, k, false), bx.hi[a] = decode(n, a, k, true);
+            path.push_back(bx);
+            if (imask & (1u << k)) {
+                walk(n.base_inner + k, depth + 1);
+            } else {
+                for (int j = 0; j < 2; j++) {
+                    if (!(n.tvalid & (1u << (2 * k + j)))) continue;
+                    const int64_t q = (int64_t)n.base_tri + 2 * k + j;
+                    if (q < 0 || (size_t)q >= b.tri_facets.size() || b.tri_facets[q] < 0 || b.tri_facets[q] >= hs.F) {
+                        bad++;
+                        continue;
+                    }
+                    const int f = b.tri_facets[q];
+                    tris++;
+                    if (seen[f]++) dup++;
+                    for (const Box& p : path)
+                        for (int v = 0; v < 3; v++)
+                            for (int a = 0; a < 3; a++) {
+                                const float x = hs.pos[9 * (size_t)f + 3 * v + a];
+                                if (!(x >= p.lo[a] && x <= p.hi[a])) bad++;
+                            }
+                }
+            }
+            path.pop_back();
+        }
+    };
+    if (!b.nodes.empty()) walk(0, 1);
+    out[0] = nodes;
+    out[1] = tris;
+    out[2] = (int64_t)bb.leaf_facets.size();
+    out[3] = dup;
+    out[4] = bad;
+    out[5] = maxd;
     return MCPT_OK;
 }
 
