@@ -17,13 +17,13 @@ enum {
     MCPT_DEBUG_NO_ROOT_CACHE = 1 << 17,
     MCPT_DEBUG_COUNT_TRAVERSAL = 1 << 18,
     MCPT_DEBUG_SHARD_RANKS = 1 << 19,
-    MCPT_DEBUG_RAYS_CW8 = 1 << 20,
-    MCPT_DEBUG_RAYS_BVH4 = 1 << 21
+    MCPT_DEBUG_RAYS_PERSIST = 1 << 20,
+    MCPT_DEBUG_RAYS_CW8 = 1 << 21
 };
-/* MCPT_DEBUG_RAYS_CW8: the MIS / shade ray sets of every scene go through the persistent 8-wide traversal
- * (k_rays_cw8), which by default serves only trees beyond an XCD's L2 -- parity tests run it on the small
- * stand-in.  MCPT_DEBUG_RAYS_BVH4: trees beyond L2 keep the 4-wide persistent kernel (k_rays_persistent),
- * the A/B baseline of k_rays_cw8.  mcpt_closest_hit flag MCPT_DEBUG_HIT_CW8: trace the batch through the
+/* MCPT_DEBUG_RAYS_PERSIST: the MIS / shade ray sets of every scene go through the persistent refilling
+ * traversal (by default only trees beyond an XCD's L2 do; smaller ones take k_mis_rays, one ray per thread).
+ * MCPT_DEBUG_RAYS_CW8: the persistent traversal walks the 8-wide compressed trees (k_rays_cw8) instead of the
+ * 4-wide ones (k_rays_persistent).  mcpt_closest_hit flag MCPT_DEBUG_HIT_CW8: trace the batch through the
  * 8-wide trees (one ray per thread, k_rays_cw8's traversal). */
 enum { MCPT_DEBUG_HIT_CW8 = 1 << 8 };
 /* MCPT_DEBUG_COUNT_TRAVERSAL runs the traversal kernel's counting instance, which fills

@@ -64,8 +64,8 @@ RENDER_FRESH_PDF = 2  # shade_with_mis: the node's own light pdf instead of the 
 RENDER_PRECISION_FP32 = 4  # opt-in FP32_STABLE light prep (packed-fp32 weights, fp64 sums); default FP64_LIGHT
 DEBUG_SPLIT_BRDF, DEBUG_NO_ROOT_CACHE, DEBUG_COUNT_TRAVERSAL = 1 << 16, 1 << 17, 1 << 18  # include/mcpt_debug.h
 DEBUG_SHARD_RANKS = 1 << 19  # device lists: every entry its own communicator rank (tests/collshim)
-DEBUG_RAYS_CW8 = 1 << 20  # MIS / shade ray sets through the persistent 8-wide traversal on every scene
-DEBUG_RAYS_BVH4 = 1 << 21  # trees beyond L2 keep the 4-wide persistent traversal (A/B baseline of k_rays_cw8)
+DEBUG_RAYS_PERSIST = 1 << 20  # MIS / shade ray sets through the persistent refilling traversal on every scene
+DEBUG_RAYS_CW8 = 1 << 21  # the persistent traversal walks the 8-wide compressed trees (k_rays_cw8)
 DEBUG_HIT_CW8 = 1 << 8  # mcpt_closest_hit: trace through the 8-wide trees
 
 

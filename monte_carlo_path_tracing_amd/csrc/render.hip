@@ -596,6 +596,49 @@ __device__ inline void cw8_tri(const float4* __restrict__ triv, int q, d3 ro, d3
 }
 // the root's node group: its only "child" is node 0 (slot 0, bit oct)
 __device__ inline unsigned cw8_root(unsigned oct) { return 1u << oct; }
+// closest hit of one ray per lane through an 8-wide tree (while-while: the wave descends until every lane
+// holds a triangle group or is done, then tests the groups); stack of node groups: kLds entries in LDS
+// ([entry][lane], stride) and a private overflow up to kStack
+template <int kLds, bool kCount = false>
+__device__ inline Hit trace_cw8(const BvhNode8Q* __restrict__ nodes, const float4* __restrict__ triv, d3 ro, d3 rd, int excl,
+                                unsigned* __restrict__ lds, int stride, float tlimit = FLT_MAX, unsigned* visits = nullptr,
+                                unsigned* tests = nullptr) {
+    Hit best{-1, DBL_MAX, 0, 0};
+    if (isnan(rd.x) || isnan(rd.y) || isnan(rd.z)) return best;  // reference: UB (Myobj.cpp:463-468)
+    unsigned spill[kStack - kLds];
+    int sp = 0;
+    const Cw8Frame F = cw8_frame(ro, rd);
+    unsigned ng = cw8_root(F.oct), tw = 0;
+    int tb = 0;
+    while (true) {
+        while (true) {
+            const bool want = tw == 0 && ((ng & 0xffu) != 0 || sp > 0);
+            if (!__any(want)) break;
+            if (want) {
+                if ((ng & 0xffu) == 0) {
+                    --sp;
+                    ng = sp < kLds ? lds[sp * stride] : spill[sp - kLds];
+                }
+                const int child = cw8_next(&ng, F.oct);
+                if (ng & 0xffu) {
+                    if (sp < kLds) lds[sp * stride] = ng;
+                    else if (sp < kStack) spill[sp - kLds] = ng;
+                    sp = sp < kStack ? sp + 1 : sp;
+                }
+                if (kCount) ++*visits;
+                cw8_visit(nodes + child, F, tlimit, &ng, &tb, &tw);
+            }
+        }
+        if (tw == 0) break;
+        while (tw != 0) {
+            const int bit = __builtin_ctz(tw);
+            tw &= tw - 1;
+            if (kCount) ++*tests;
+            cw8_tri(triv, tb + bit, ro, rd, excl, &best, &tlimit);
+        }
+    }
+    return best;
+}
 
 // The picked triangle's spherical triangle for Arvo's sampler (Mylight.cpp:453-461): the reference's
 // literal chain (light_tri_stage -- sqrt / division unit vectors, correctly rounded acos for
@@ -3363,7 +3406,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)nsets * (unsigned)n;
     int spill[kStack - kPersistLds];
-    unsigned visits = 0, tests = 0;
+    unsigned visits = 0, tests = 0, witer = 0, wleaf = 0;
     bool busy = false, exhausted = false;
     unsigned wnext = 0, wend = 0;  // the wave's private range of pool items (wave-uniform)
     int set = 0, ii = 0, excl = -1;
@@ -3459,6 +3502,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
             const bool neg3[3] = {ix < 0, iy < 0, iz < 0};
             while (node >= 0 && node != kDone) {
                 if (kCount) ++visits;
+                if (kCount && MCPT_TRACE_DIAG && (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++witer;
                 float tn[3][4], tf[3][4];  // near / far slab distances per axis and child
                 int chs[4];
                 node_tplanes(nodes + node, inv3, oi3, neg3, tn, tf, chs);
@@ -3495,6 +3539,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
             while (leaf < 0) {
                 const int packed = ~leaf, first = packed >> kLeafBits, cnt4 = packed & ((1 << kLeafBits) - 1);
                 for (int q = first; q < first + cnt4; q++) {
+                    if (kCount && MCPT_TRACE_DIAG && (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++wleaf;
                     const float4 a4 = leafv[3 * q], b4 = leafv[3 * q + 1], c4 = leafv[3 * q + 2];
                     const int fac = __float_as_int(a4.w);
                     if (fac == excl) continue;
@@ -3523,6 +3568,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
         }
     }
     if (kCount) wave_count2(cnt, visits, cnt + 1, tests);
+    if (kCount && MCPT_TRACE_DIAG) wave_count2(cnt + 6, witer, cnt + 7, wleaf);
 }
 
 // k_rays_persistent over the 8-wide compressed trees (BvhNode8Q): the same refilling persistent waves,
@@ -3531,7 +3577,11 @@ __global__ __launch_bounds__(kRayBlock, MCPT_RAYS_WAVES) void k_rays_persistent(
 // triangles.  Hits are bit-identical to k_rays_persistent / k_mis_rays (same tests, same total order on
 // (t, facet), conservative boxes); visits and their order differ.
 #ifndef MCPT_RAYS_CW8
-#define MCPT_RAYS_CW8 1  // 0: k_rays_persistent (4-wide) for the scenes beyond L2 (A/B)
+// 1: the persistent traversal uses the 8-wide trees by default.  Off: measured slower on C5 (round 5, same
+// binary, profiles/round5_ab_cornell_cw8.txt): 22.1 node visits per ray instead of 30.8, but 8.0 triangle
+// tests instead of 6.7 (octant order instead of sorted hits) and twice the box tests per visit --
+// k_rays_cw8 5.18 vs k_rays_persistent 3.91 ms per launch, C5 1 651 vs 2 044 Msamples/s
+#define MCPT_RAYS_CW8 0
 #endif
 #ifndef MCPT_CW8_WAVES
 #define MCPT_CW8_WAVES 6
@@ -3546,7 +3596,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)nsets * (unsigned)n;
     unsigned spill[kStack - kPersistLds];
-    unsigned visits = 0, tests = 0;
+    unsigned visits = 0, tests = 0, witer = 0, wleaf = 0;
     bool busy = false, exhausted = false;
     unsigned wnext = 0, wend = 0;
     int set = 0, ii = 0, excl = -1;
@@ -3630,6 +3680,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
                 const bool want = tw == 0 && ((ng & 0xffu) != 0 || sp > 0);
                 if (!__any(want)) break;
                 if (want) {
+                    if (kCount && MCPT_TRACE_DIAG && (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++witer;
                     if ((ng & 0xffu) == 0) ng = pop();
                     const int child = cw8_next(&ng, F.oct);
                     if (ng & 0xffu) push(ng);
@@ -3638,6 +3689,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
                 }
             }
             while (tw != 0) {
+                if (kCount && MCPT_TRACE_DIAG && (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++wleaf;
                 const int bit = __builtin_ctz(tw);
                 tw &= tw - 1;
                 if (kCount) ++tests;
@@ -3647,6 +3699,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
         }
     }
     if (kCount) wave_count2(cnt, visits, cnt + 1, tests);
+    if (kCount && MCPT_TRACE_DIAG) wave_count2(cnt + 6, witer, cnt + 7, wleaf);
 }
 
 template <bool kStale>
@@ -3969,6 +4022,9 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
 constexpr int kBrdfTop = MCPT_BRDF_TOP;
 constexpr int kBrdfBlock = kBrdfTop > 0 ? 256 : kTraceBlock;
 constexpr int kBrdfLds = kBrdfTop > 0 ? 8 : kRayLds;
+#ifndef MCPT_BRDF_CW8
+#define MCPT_BRDF_CW8 0  // A/B: k_extend_brdf traces through the 8-wide tree (trace_cw8) instead of trace4_ww
+#endif
 #ifndef MCPT_BRDF_TIMING
 #define MCPT_BRDF_TIMING 0  // A/B only: 1 = sampling twice, 2 = traversal twice (cost shares, timing builds)
 #endif
@@ -4023,8 +4079,13 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
             // the shading state (N, wo, material, tp, pdf) is dead during it (fewer VGPRs)
             const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
             tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
+#if MCPT_BRDF_CW8
+            h = trace_cw8<kBrdfLds, kCount>(S.bvh8, S.tri8_v, p, wi, f, reinterpret_cast<unsigned*>(stack) + threadIdx.x, kBrdfBlock,
+                                            FLT_MAX, &visits, &tests);
+#else
             h = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
                                                       &tests, top, FLT_MAX, &witer, &wleaf);
+#endif
 #if MCPT_BRDF_TIMING == 2  // timing-only build: the traversal runs twice
             {
                 const Hit h2 = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x,
@@ -4064,46 +4125,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_batch(DScene S, int n, co
 __global__ __launch_bounds__(kTraceBlock) void k_trace_batch_cw8(DScene S, int n, const double* ro_, const double* rd_,
                                                                 const int* ex, int light_only, int* f_out, double* tbg) {
     __shared__ unsigned stack[kRayLds * kTraceBlock];
-    unsigned* lds = stack + threadIdx.x;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const d3 ro = mk3(ro_[3 * i], ro_[3 * i + 1], ro_[3 * i + 2]), rd = mk3(rd_[3 * i], rd_[3 * i + 1], rd_[3 * i + 2]);
-    const BvhNode8Q* nodes = light_only ? S.lbvh8 : S.bvh8;
-    const float4* triv = light_only ? S.ltri8_v : S.tri8_v;
-    Hit best{-1, DBL_MAX, 0, 0};
-    if (!(isnan(rd.x) || isnan(rd.y) || isnan(rd.z))) {
-        unsigned spill[kStack - kRayLds];
-        int sp = 0;
-        const Cw8Frame F = cw8_frame(ro, rd);
-        float tlimit = FLT_MAX;
-        unsigned ng = cw8_root(F.oct), tw = 0;
-        int tb = 0;
-        while (true) {
-            while (true) {
-                const bool want = tw == 0 && ((ng & 0xffu) != 0 || sp > 0);
-                if (!__any(want)) break;
-                if (want) {
-                    if ((ng & 0xffu) == 0) {
-                        --sp;
-                        ng = sp < kRayLds ? lds[sp * kTraceBlock] : spill[sp - kRayLds];
-                    }
-                    const int child = cw8_next(&ng, F.oct);
-                    if (ng & 0xffu) {
-                        if (sp < kRayLds) lds[sp * kTraceBlock] = ng;
-                        else if (sp < kStack) spill[sp - kRayLds] = ng;
-                        sp = sp < kStack ? sp + 1 : sp;
-                    }
-                    cw8_visit(nodes + child, F, tlimit, &ng, &tb, &tw);
-                }
-            }
-            if (tw == 0) break;
-            while (tw != 0) {
-                const int bit = __builtin_ctz(tw);
-                tw &= tw - 1;
-                cw8_tri(triv, tb + bit, ro, rd, ex[i], &best, &tlimit);
-            }
-        }
-    }
+    const Hit best = trace_cw8<kRayLds>(light_only ? S.lbvh8 : S.bvh8, light_only ? S.ltri8_v : S.tri8_v,
+                                        mk3(ro_[3 * i], ro_[3 * i + 1], ro_[3 * i + 2]), mk3(rd_[3 * i], rd_[3 * i + 1], rd_[3 * i + 2]),
+                                        ex[i], stack + threadIdx.x, kTraceBlock);
     f_out[i] = best.f;
     tbg[3 * i] = best.f >= 0 ? best.t : 0.0;
     tbg[3 * i + 1] = best.f >= 0 ? best.beta : 0.0;
@@ -4763,7 +4789,7 @@ int validate_render(const mcpt_render_opts* o) {
     }
     if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
                      MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL |
-                     MCPT_DEBUG_SHARD_RANKS | MCPT_DEBUG_RAYS_CW8 | MCPT_DEBUG_RAYS_BVH4)) {
+                     MCPT_DEBUG_SHARD_RANKS | MCPT_DEBUG_RAYS_PERSIST | MCPT_DEBUG_RAYS_CW8)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
@@ -5177,14 +5203,14 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const dim3 g256((ni + 255) / 256), b256(256);
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
     auto launch_rays = [&](int first_set, int nsets, int seeded) {
-        const bool force_cw8 = (o->flags & MCPT_DEBUG_RAYS_CW8) != 0;
-        const bool pers = force_cw8 || MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
+        const bool force_pers = (o->flags & MCPT_DEBUG_RAYS_PERSIST) != 0;
+        const bool pers = force_pers || MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
         if (pers && !grid) {
             unsigned* pool = (unsigned*)D.work.p + 8;
             (void)hipMemsetAsync(pool, 0, sizeof(unsigned), st);
             const long long items = (long long)nsets * ni;
             const int blocks = (int)std::max<long long>(1, std::min<long long>((items + kRayBlock - 1) / kRayBlock, 2048));
-            if ((force_cw8 || (MCPT_RAYS_CW8 && !(o->flags & MCPT_DEBUG_RAYS_BVH4))) && D.d.bvh8 && D.d.lbvh8) {
+            if ((MCPT_RAYS_CW8 || (o->flags & MCPT_DEBUG_RAYS_CW8)) && D.d.bvh8 && D.d.lbvh8) {
                 if (count_trav)
                     hipLaunchKernelGGL(k_rays_cw8<true>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux, first_set, nsets,
                                        pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);

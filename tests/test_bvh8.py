@@ -100,12 +100,16 @@ def test_edge_and_vertex_rays_through_bvh8(scene, light_only):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,spp", [("mis", 8), ("shade", 8), ("shade_area", 16)])
 def test_render_through_k_rays_cw8_equals_default(scene, mode, spp):
-    """MCPT_DEBUG_RAYS_CW8: the MIS / shade ray sets of the small stand-in through the persistent 8-wide
-    traversal -- the same hits, so the same frame up to fp64 accumulation order"""
+    """MCPT_DEBUG_RAYS_PERSIST | MCPT_DEBUG_RAYS_CW8: the MIS / shade ray sets of the small stand-in through
+    the persistent 8-wide traversal (and the persistent 4-wide one) -- the same hits, so the same frame up to
+    fp64 accumulation order"""
     cam = mcpt.Camera.reference(160, 120)
     a, _ = mcpt.render(scene, cam, spp, mode=mode, seed=SEED)
-    b, _ = mcpt.render(scene, cam, spp, mode=mode, seed=SEED, flags=mcpt.DEBUG_RAYS_CW8)
-    c, sc = mcpt.render(scene, cam, spp, mode=mode, seed=SEED, flags=mcpt.DEBUG_RAYS_CW8 | mcpt.DEBUG_COUNT_TRAVERSAL)
+    cw8 = mcpt.DEBUG_RAYS_PERSIST | mcpt.DEBUG_RAYS_CW8
+    b, _ = mcpt.render(scene, cam, spp, mode=mode, seed=SEED, flags=cw8)
+    c, sc = mcpt.render(scene, cam, spp, mode=mode, seed=SEED, flags=cw8 | mcpt.DEBUG_COUNT_TRAVERSAL)
+    d, _ = mcpt.render(scene, cam, spp, mode=mode, seed=SEED, flags=mcpt.DEBUG_RAYS_PERSIST)
+    assert rel_l2(d, a) <= 1e-12
     print("%s 160x120x%d through k_rays_cw8: rel L2 vs default %.2e; %d visits, %d tests" % (
         mode, spp, rel_l2(b, a), sc.node_visits, sc.tri_tests))
     assert rel_l2(b, a) <= 1e-12 and rel_l2(c, a) <= 1e-12
@@ -114,13 +118,13 @@ def test_render_through_k_rays_cw8_equals_default(scene, mode, spp):
 
 @pytest.mark.gpu
 def test_cornell_1m_cw8_equals_bvh4_persistent():
-    """C5's scene (1M random triangles, trees beyond L2: k_rays_cw8 by default) against the 4-wide
-    persistent kernel (MCPT_DEBUG_RAYS_BVH4) and random rays through both batch queries"""
+    """C5's scene (1M random triangles, trees beyond L2: the persistent traversal) through the 8-wide trees
+    (MCPT_DEBUG_RAYS_CW8) against the 4-wide ones, and random rays through both batch queries"""
     sc = mcpt.Scene.load(*cornell_scene(1000000))
     cam = sc.camera()
     cam.width, cam.height = 128, 96
-    a, sa = mcpt.render(sc, cam, 8, mode="mis", seed=SEED, flags=mcpt.DEBUG_COUNT_TRAVERSAL)
-    b, sb = mcpt.render(sc, cam, 8, mode="mis", seed=SEED, flags=mcpt.DEBUG_RAYS_BVH4 | mcpt.DEBUG_COUNT_TRAVERSAL)
+    a, sa = mcpt.render(sc, cam, 8, mode="mis", seed=SEED, flags=mcpt.DEBUG_RAYS_CW8 | mcpt.DEBUG_COUNT_TRAVERSAL)
+    b, sb = mcpt.render(sc, cam, 8, mode="mis", seed=SEED, flags=mcpt.DEBUG_COUNT_TRAVERSAL)
     print("cornell-1M 128x96x8 MIS: cw8 vs 4-wide rel L2 %.2e; visits per ray %.2f (cw8) vs %.2f (4-wide)" % (
         rel_l2(a, b), sa.node_visits / max(sa.rays + sa.light_rays, 1), sb.node_visits / max(sb.rays + sb.light_rays, 1)))
     assert rel_l2(a, b) <= 1e-12
