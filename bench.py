@@ -228,6 +228,9 @@ def main():
     ap.add_argument("--cpu-single-seconds", type=float, default=20.0,
                     help="budget of the single-thread CPU baseline leg (spp reduced to fit; rate per sample)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and L2 check")
+    ap.add_argument("--no-replay", action="store_true",
+                    help="skip the untimed statistics replay (PMC passes: the profile then holds only the warmup and "
+                         "timed steps' kernel instances; the line has no traversal roofline, whose events it counts)")
     ap.add_argument("--fresh-pdf", action="store_true",
                     help="MIS with the node's own light pdf (MCPT_RENDER_FRESH_PDF) instead of the reference's stale one")
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
@@ -352,17 +355,18 @@ def main():
     # mcpt_render_opts.flags) and the traversal kernel's node-visit / triangle-test counters
     # (MCPT_DEBUG_COUNT_TRAVERSAL); the work both runs counted must be identical.
     rep = {}
-    for k in range(args.steps):
+    for k in range(0 if args.no_replay else args.steps):
         st = mcpt.render_device(scene, cam, frame_spp, scratch.data_ptr(), mode=args.mode, seed=args.seed,
                                 sample_range=(k * world * S, (k + 1) * world * S),
                                 flags=mcpt.DEBUG_COUNT_TRAVERSAL | mode_flags, **multi)
         for key, v in st.as_dict().items():
             rep[key] = rep.get(key, 0) + v
-    for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays",
-                "light_rays", "shading_nodes"):
-        assert rep.get(key) == totals.get(key), (key, rep.get(key), totals.get(key))
-    for key in ("light_evals_culled_backface", "light_evals_culled_plane", "node_visits", "tri_tests"):
-        totals[key] = rep[key]
+    if not args.no_replay:
+        for key in ("light_evals_total", "light_evals_candidates", "light_evals_survived", "prep_full_nodes", "rays",
+                    "light_rays", "shading_nodes"):
+            assert rep.get(key) == totals.get(key), (key, rep.get(key), totals.get(key))
+        for key in ("light_evals_culled_backface", "light_evals_culled_plane", "node_visits", "tri_tests"):
+            totals[key] = rep[key]
 
     log("rank %d totals: %s" % (rank, json.dumps({k: v for k, v in totals.items()})))
     if rank != 0:

@@ -323,9 +323,6 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 // source in round 4): node loads as 32-bit byte offsets (neutral); near / far planes picked once per
 // ray by the inverse direction's sign (97 -> 63 VALU per visit, but k_mis_rays 3.81 -> 4.02 ms); the
 // near / far planes selected after the usual loads (MIS 464.3 -> 463.2, BRDF-only 5 831 -> 5 760).
-#ifndef MCPT_MARGIN_FMA
-#define MCPT_MARGIN_FMA 0  // A/B: the slab test's 1e-5 relative margin as one FMA
-#endif
 #ifndef MCPT_FILTER_MIS
 #define MCPT_FILTER_MIS 1
 #endif
@@ -357,6 +354,9 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 // MCPT_TRACE_DIAG (diagnostics only, with kCount): *witer / *wleaf count the WAVE's iterations of the
 // node-visit loop and of the triangle loop (added by the wave's first active lane), so that visits /
 // (64 witer) is the traversal's SIMD lane utilisation
+#ifndef MCPT_PERSIST_SHADE_AREA
+#define MCPT_PERSIST_SHADE_AREA 1
+#endif
 #ifndef MCPT_TRACE_DIAG
 #define MCPT_TRACE_DIAG 0
 #endif
@@ -437,11 +437,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                     const float tz0 = fmaf(lo[2][k], iz, -oiz), tz1 = fmaf(hi[2][k], iz, -oiz);
                     const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
                     const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlimit));
-#if MCPT_MARGIN_FMA
-                    const bool h = chs[k] != kBvh4Empty && t0 <= fmaf(t1, 1.00001f, 1e-6f);
-#else
                     const bool h = chs[k] != kBvh4Empty && t0 <= t1 * 1.00001f + 1e-6f;
-#endif
                     t[k] = h ? t0 : FLT_MAX;
                     code[k] = h ? chs[k] : kDone;
                 }
@@ -4022,9 +4018,6 @@ __global__ __launch_bounds__(256) void k_brdf_combine(Params P, Queue cur, int n
 constexpr int kBrdfTop = MCPT_BRDF_TOP;
 constexpr int kBrdfBlock = kBrdfTop > 0 ? 256 : kTraceBlock;
 constexpr int kBrdfLds = kBrdfTop > 0 ? 8 : kRayLds;
-#ifndef MCPT_BRDF_CW8
-#define MCPT_BRDF_CW8 0  // A/B: k_extend_brdf traces through the 8-wide tree (trace_cw8) instead of trace4_ww
-#endif
 #ifndef MCPT_BRDF_TIMING
 #define MCPT_BRDF_TIMING 0  // A/B only: 1 = sampling twice, 2 = traversal twice (cost shares, timing builds)
 #endif
@@ -4079,13 +4072,8 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
             // the shading state (N, wo, material, tp, pdf) is dead during it (fewer VGPRs)
             const d3 b = brdf_phong(N, wi, wo, kd, ks, sh);
             tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
-#if MCPT_BRDF_CW8
-            h = trace_cw8<kBrdfLds, kCount>(S.bvh8, S.tri8_v, p, wi, f, reinterpret_cast<unsigned*>(stack) + threadIdx.x, kBrdfBlock,
-                                            FLT_MAX, &visits, &tests);
-#else
             h = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
                                                       &tests, top, FLT_MAX, &witer, &wleaf);
-#endif
 #if MCPT_BRDF_TIMING == 2  // timing-only build: the traversal runs twice
             {
                 const Hit h2 = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x,
@@ -5204,7 +5192,11 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
     auto launch_rays = [&](int first_set, int nsets, int seeded) {
         const bool force_pers = (o->flags & MCPT_DEBUG_RAYS_PERSIST) != 0;
-        const bool pers = force_pers || MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20));
+        // shade() with uniform-area light points: its shadow and bounce rays run 4% faster on the refilling
+        // persistent waves even on the small stand-in (shade_area 2 104-2 126 -> 2 185-2 191 Msamples/s, same
+        // binary, profiles/round5_ab_persistent_veach.txt); MIS and shade() are slower there (-1%, -1%)
+        const bool pers = force_pers || MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20)) ||
+                          (MCPT_PERSIST_SHADE_AREA && o->mode == MCPT_MODE_SHADE_AREA);
         if (pers && !grid) {
             unsigned* pool = (unsigned*)D.work.p + 8;
             (void)hipMemsetAsync(pool, 0, sizeof(unsigned), st);

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--replay", type=int, default=1, help="1 if the profiled bench ran its statistics replay (0: --no-replay)")
     a = ap.parse_args()
     fetch, nf = per_kernel(a.fetch, "FETCH_SIZE")
     write, _ = per_kernel(a.write, "WRITE_SIZE")
@@ -50,7 +51,7 @@ def main():
             tot = json.loads(line.split(":", 1)[1])
     # totals cover the timed steps; the profile also saw the warmup steps and bench.py's untimed
     # replay of the timed steps (the cull statistic pass, MIS/shade) -- same work per step
-    nodes = tot["prep_full_nodes"] * (2 * a.steps + a.warmup) / a.steps
+    nodes = tot["prep_full_nodes"] * ((1 + a.replay) * a.steps + a.warmup) / a.steps
     kernels = [k for k in fetch if k.startswith("k_prep_cull_lanes") or k.startswith("k_prep_pk2")]
     # FETCH_SIZE x2 only for 16-B-per-lane loads (MI355X_MICROARCH.md): k_prep_pk2's light records are
     # buffer_load_dwordx4; k_prep_cull_lanes reads its table with scalar loads (width uncalibrated, x1)
@@ -67,9 +68,9 @@ def main():
         "full_prep_nodes": int(nodes),
         "method": "rocprofv3 --pmc FETCH_SIZE (x2 for k_prep_pk2's 16-B-per-lane record loads, gfx950's 64-B tally of 128-B requests; x1 for the cull's scalar loads) and --pmc WRITE_SIZE in "
                   "separate passes over `bench.py --steps %d --warmup %d --no-cpu`; bytes of both kernels over all "
-                  "dispatches / full-prep nodes (timed-step count scaled to the profiled steps: warmup + timed + replay); "
+                  "dispatches / full-prep nodes (timed-step count scaled to the profiled steps: warmup + timed%s); "
                   "tools/prep_hbm_bytes.py"
-                  % (a.steps, a.warmup),
+                  % (a.steps, a.warmup, " + replay" if a.replay else ", --no-replay: only the timed steps' kernel instances"),
     }
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)

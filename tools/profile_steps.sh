@@ -19,15 +19,15 @@ exec tools/gpu_steps.sh \
 else
 exec tools/gpu_steps.sh \
  "300:prof:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T} -o run --output-format csv -- python3 bench.py --no-cpu" \
- "120:pmc_fetch:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${T}_fetch -o run --output-format csv -- python3 bench.py --no-cpu --steps 2" \
- "120:pmc_write:rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d gpurun_out/pmc_${T}_write -o run --output-format csv -- python3 bench.py --no-cpu --steps 2" \
- "120:pmc_sq:rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/pmc_${T}_sq -o run --output-format csv -- python3 bench.py --no-cpu --steps 2" \
+ "120:pmc_fetch:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${T}_fetch -o run --output-format csv -- python3 bench.py --no-cpu --no-replay --steps 2" \
+ "120:pmc_write:rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d gpurun_out/pmc_${T}_write -o run --output-format csv -- python3 bench.py --no-cpu --no-replay --steps 2" \
+ "120:pmc_sq:rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/pmc_${T}_sq -o run --output-format csv -- python3 bench.py --no-cpu --no-replay --steps 2" \
  "300:prof_brdf:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_brdf -o run --output-format csv -- python3 bench.py --mode brdf --steps 1 --no-cpu" \
- "120:pmc_fetch_brdf:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${T}_fetch_brdf -o run --output-format csv -- python3 bench.py --mode brdf --steps 1 --no-cpu" \
- "120:pmc_write_brdf:rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d gpurun_out/pmc_${T}_write_brdf -o run --output-format csv -- python3 bench.py --mode brdf --steps 1 --no-cpu" \
- "120:pmc_sq_brdf:rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/pmc_${T}_sq_brdf -o run --output-format csv -- python3 bench.py --mode brdf --steps 1 --no-cpu" \
+ "120:pmc_fetch_brdf:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${T}_fetch_brdf -o run --output-format csv -- python3 bench.py --mode brdf --steps 1 --no-cpu --no-replay" \
+ "120:pmc_write_brdf:rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d gpurun_out/pmc_${T}_write_brdf -o run --output-format csv -- python3 bench.py --mode brdf --steps 1 --no-cpu --no-replay" \
+ "120:pmc_sq_brdf:rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/pmc_${T}_sq_brdf -o run --output-format csv -- python3 bench.py --mode brdf --steps 1 --no-cpu --no-replay" \
  "300:prof_cornell:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_cornell -o run --output-format csv -- python3 bench.py --scene cornell1m --no-cpu" \
- "150:pmc_fetch_cornell:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${T}_fetch_cornell -o run --output-format csv -- python3 bench.py --scene cornell1m --no-cpu --steps 1" \
- "150:pmc_write_cornell:rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d gpurun_out/pmc_${T}_write_cornell -o run --output-format csv -- python3 bench.py --scene cornell1m --no-cpu --steps 1" \
- "150:pmc_sq_cornell:rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/pmc_${T}_sq_cornell -o run --output-format csv -- python3 bench.py --scene cornell1m --no-cpu --steps 1"
+ "150:pmc_fetch_cornell:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${T}_fetch_cornell -o run --output-format csv -- python3 bench.py --scene cornell1m --no-cpu --no-replay --steps 1" \
+ "150:pmc_write_cornell:rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d gpurun_out/pmc_${T}_write_cornell -o run --output-format csv -- python3 bench.py --scene cornell1m --no-cpu --no-replay --steps 1" \
+ "150:pmc_sq_cornell:rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/pmc_${T}_sq_cornell -o run --output-format csv -- python3 bench.py --scene cornell1m --no-cpu --no-replay --steps 1"
 fi
