@@ -357,6 +357,9 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 #ifndef MCPT_PERSIST_SHADE_AREA
 #define MCPT_PERSIST_SHADE_AREA 1
 #endif
+#ifndef MCPT_WW_BREAK
+#define MCPT_WW_BREAK 0  // A/B: trace4_ww leaves its node loop when <= this many lanes still search a leaf (0: none)
+#endif
 #ifndef MCPT_TRACE_DIAG
 #define MCPT_TRACE_DIAG 0
 #endif
@@ -459,7 +462,8 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
                 leaf = node;
                 node = pop();
             }
-            if (!__any(leaf >= 0)) break;
+            // go test the postponed leaves once at most MCPT_WW_BREAK lanes are still searching for one
+            if (MCPT_WW_BREAK == 0 ? !__any(leaf >= 0) : __popcll(__ballot(leaf >= 0)) <= MCPT_WW_BREAK) break;
         }
         while (leaf < 0) {
             const int packed = ~leaf, first = packed >> kLeafBits, cnt = packed & ((1 << kLeafBits) - 1);
@@ -907,6 +911,25 @@ __device__ inline Entry entry_eval(const Params& P, bool active, int f, double b
         e.kind = counter_u(key, 0) > MCPT_P_RR ? 0 : 2;
     }
     return e;
+}
+// writes a shading node at queue position slot (from an append), or flags the overflow
+__device__ inline void queue_write(const Params& P, bool push, int slot, const Entry& e, int f, d3 wo, d3 tp, int pixel,
+                                   int sample, uint64_t node, int par, Queue& q, bool write_tp = true) {
+    if (!push) return;
+    if (slot >= q.cap) {
+        atomicOr((unsigned long long*)(P.stats + 4), 1ull);
+        return;
+    }
+    const size_t s = (size_t)slot;
+    st3(q.p, q.cap, s, e.p);
+    st3(q.n, q.cap, s, e.N);
+    st3(q.wo, q.cap, s, wo);
+    if (write_tp) st3(q.tp, q.cap, s, tp);
+    q.f[s] = f;
+    q.pixel[s] = pixel;
+    q.sample[s] = sample;
+    q.node[s] = node;
+    q.par[s] = par;
 }
 // appends a shading node to q.  Must be called by ALL threads of the workgroup (block_append).
 __device__ inline void queue_push(const Params& P, bool push, const Entry& e, int f, d3 wo, d3 tp, int pixel, int sample,
@@ -3365,6 +3388,52 @@ __device__ inline int block_alloc_slot(const Slots& T, bool want) {
     __syncthreads();
     return slot;
 }
+// block_alloc_slot and k_mis_combine's two child appends (light children first, then BRDF children, as two
+// block_append calls would order them) in ONE barrier phase: the workgroup's three counts are reduced
+// together and thread 0 issues the queue atomic and the slot-ring atomics back to back, so the workgroup
+// waits for one round of device-scope atomics instead of three.  Must be called by ALL threads.
+__device__ inline void block_alloc_slot_push2(const Slots& T, bool want, bool push1, bool push2, unsigned* qcount, int* slot_out,
+                                              int* q1_out, int* q2_out) {
+    __shared__ unsigned s_cnt[3][16];
+    __shared__ unsigned s_base, s_ring, s_bump, s_q;
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    const uint64_t m = __ballot(want), m1 = __ballot(push1), m2 = __ballot(push2);
+    if (lane == 0) s_cnt[0][wid] = (unsigned)__popcll(m), s_cnt[1][wid] = (unsigned)__popcll(m1), s_cnt[2][wid] = (unsigned)__popcll(m2);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot[3] = {0, 0, 0};
+        for (int k = 0; k < 3; k++)
+            for (int w = 0; w < nw; w++) {
+                const unsigned c = s_cnt[k][w];
+                s_cnt[k][w] = tot[k];
+                tot[k] += c;
+            }
+        for (int w = 0; w < nw; w++) s_cnt[2][w] += tot[1];  // BRDF children after all light children
+        const unsigned np = tot[1] + tot[2];
+        unsigned q = 0, base = 0, from_ring = 0, bump = 0;
+        unsigned* c = T.ctrl + 16 * (blockIdx.x & (kSlotShards - 1));
+        if (np) q = atomicAdd(qcount, np);
+        if (tot[0]) {
+            base = atomicAdd(&c[1], tot[0]);
+            const unsigned end = c[3];
+            from_ring = base >= end ? 0u : min(tot[0], end - base);
+            if (tot[0] > from_ring) bump = atomicAdd(&c[0], tot[0] - from_ring);
+        }
+        s_base = base, s_ring = from_ring, s_bump = bump, s_q = q;
+    }
+    __syncthreads();
+    const uint64_t below = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
+    const unsigned j = s_cnt[0][wid] + (unsigned)__popcll(m & below);
+    const int sh = blockIdx.x & (kSlotShards - 1);
+    int slot = -1;
+    if (want)
+        slot = j < s_ring ? T.ring[(size_t)sh * T.ring_cap + (s_base + j) % (unsigned)T.ring_cap]
+                          : (int)(((s_bump + (j - s_ring)) << 5) | (unsigned)sh);
+    *slot_out = slot;
+    *q1_out = push1 ? (int)(s_q + s_cnt[1][wid] + (unsigned)__popcll(m1 & below)) : -1;
+    *q2_out = push2 ? (int)(s_q + s_cnt[2][wid] + (unsigned)__popcll(m2 & below)) : -1;
+    __syncthreads();
+}
 
 // The same three ray sets as k_mis_rays, traced by PERSISTENT waves that refill lanes whose ray has
 // finished with the next ray of a shared pool (Aila & Laine's persistent while-while with dynamic
@@ -3698,6 +3767,9 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
     if (kCount && MCPT_TRACE_DIAG) wave_count2(cnt + 6, witer, cnt + 7, wleaf);
 }
 
+#ifndef MCPT_COMBINE_ONE_PHASE
+#define MCPT_COMBINE_ONE_PHASE 1  // A/B: 0 = slot allocation and the two child appends as three barrier phases
+#endif
 template <bool kStale>
 __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
@@ -3740,7 +3812,12 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         double s2 = 0;
         if (c2 && !lsh) s2 = cosb / (pdf + state_light_pdf(S, li, own)) / MCPT_P_RR;
         const bool hold = lsh || bsh;
+#if MCPT_COMBINE_ONE_PHASE
+        int slot, qp1, qp2;
+        block_alloc_slot_push2(T, hold, lsh, bsh, nxt.count, &slot, &qp1, &qp2);
+#else
         const int slot = block_alloc_slot(T, hold);
+#endif
         const int pc = cur.par[ii];
         const bool need = pc >= 0 && (pc & 1);  // this subtree's path end is needed above
         d3 Lbr = mk3(0, 0, 0);
@@ -3765,8 +3842,14 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         const bool need_l = (c2 && li >= 0) || (need && !bsh);
         const bool need_b = need;
         const d3 z = mk3(0, 0, 0);
+#if MCPT_COMBINE_ONE_PHASE
+        // the stale form never reads a node's forward throughput (w1 / w2 carry the edges), so it is not written
+        queue_write(P, lsh, qp1, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt, false);
+        queue_write(P, bsh, qp2, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt, false);
+#else
         queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt);
         queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt);
+#endif
     }
     block_count(ray_stats(P), active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, ray_stats(P) + 1,
                 (active && c2) ? 1u : 0u);
