@@ -1764,13 +1764,25 @@ __device__ inline double prep_weight_buf(__amdgpu_buffer_rsrc_t rw, int li, d3 x
                            mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1, ok);
 }
 // prep_weight_buf with the exact-pick bookkeeping (light_weight_bx); *lsum2 = the record's 2 sum L
+#ifndef MCPT_PK2_TIMING
+#define MCPT_PK2_TIMING 0  // timing-only builds: 1 = the records loaded but no fp64 weight math, 2 = neither
+#endif
 __device__ inline WeightBx prep_weight_buf_bx(__amdgpu_buffer_rsrc_t rw, int li, d3 x1, double* lsum2) {
+    if (MCPT_PK2_TIMING == 2) {
+        *lsum2 = 1.0;
+        return WeightBx{(double)(li + 1) * 1e-6, 1.0, 1.0, true, false};
+    }
     const v4u a = struct_load_b128(rw, li, 0, 0, 0);
     const v4u b = struct_load_b128(rw, li, 16, 0, 0);
     const v4u c = struct_load_b128(rw, li, 32, 0, 0);
     const v4u d = struct_load_b128(rw, li, 48, 0, 0);
     const v4u e = struct_load_b128(rw, li, 64, 0, 0);
     *lsum2 = u2d(e.z, e.w);
+    if (MCPT_PK2_TIMING == 1) {
+        const double w = fabs(u2d(a.x, a.y) + u2d(b.z, b.w) + u2d(c.x, c.y) + u2d(d.z, d.w) + u2d(e.x, e.y) + x1.x) * 1e-9 +
+                         fabs(u2d(e.z, e.w)) + 1e-12;
+        return WeightBx{w, 1.0, 1.0, true, false};
+    }
     return light_weight_bx<true>(mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y)),
                                  mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
                                  mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1);
@@ -2644,9 +2656,6 @@ __global__ __launch_bounds__(256, MCPT_LB_PICK) void k_prep_pick(DScene S, uint6
 #ifndef MCPT_PICK_GROUPS
 #define MCPT_PICK_GROUPS 1  // 0: k_prep_pick (wave per root) for every table size (A/B)
 #endif
-#ifndef MCPT_PICK_PIPE
-#define MCPT_PICK_PIPE 0  // A/B: k_prep_pick_g loads the next iteration's rows while this one's batch is in flight
-#endif
 #ifndef MCPT_LB_PICKG
 #define MCPT_LB_PICKG 4  // 121 VGPRs at 4 slots, no spills
 #endif
@@ -2716,125 +2725,6 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
             inf_[s] = C.info[px_[s]];
         }
     };
-#if MCPT_PICK_PIPE
-    // software pipeline over the wave's iterations: the queue entries two iterations ahead, the rows one
-    // iteration ahead (issued after this iteration's batch loads: vmcnt retires loads in order, so a row
-    // load issued earlier would hold up the wait for the batch), the batch of this iteration
-    double ul = 0;
-    if (gw * kR < n) {
-        fetch(gw * kR);
-        ul = counter_u(counter_key(seed, (uint64_t)f_px, (uint64_t)f_smp, f_nid), 1);  // dim 1
-        load_rows(f_px, px, inf, bv);
-        if (gw * kR + waves * kR < n) fetch(gw * kR + waves * kR);
-    }
-    for (int n0 = gw * kR; n0 < n; n0 += waves * kR) {
-        double wsum[kPickSlots], base[kPickSlots], target[kPickSlots];
-        int kb[kPickSlots];
-#pragma unroll
-        for (int s = 0; s < kPickSlots; s++) {
-            const int nb = inf[s].x;
-            const int lw = max(nb - 1, 0);
-            const double W = bperm_f64(sel4(bv[s], lw >> 4), g0 + (lw & 15));
-            wsum[s] = nb > 0 ? W : 0.0;
-            const bool valid = !(fabs(wsum[s]) < MCPT_EPS);
-            target[s] = bperm_f64(ul, 4 * s + g) * wsum[s];
-            {
-                unsigned c = 64;
-#pragma unroll
-                for (int k = 3; k >= 0; k--)
-                    c = valid && 16 * k + gl < nb && bv[s][k] >= target[s] && bv[s][k] > 0.0 ? 16 * k + gl : c;
-                c = row_min_u32(c);
-                kb[s] = c < 64 ? (int)c : -1;
-            }
-            const int lb = max(kb[s] - 1, 0);
-            const double b = bperm_f64(sel4(bv[s], lb >> 4), g0 + (lb & 15));
-            base[s] = kb[s] > 0 ? b : 0.0;
-        }
-        // the picked batch's signed in-batch prefixes and its 64 list entries
-        double wc[kPickSlots][4];
-        int lj[kPickSlots][4];
-#pragma unroll
-        for (int s = 0; s < kPickSlots; s++) {
-            const size_t off = (size_t)px[s] * C.lstride + 64 * max(kb[s], 0) + gl;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool act = kb[s] >= 0 && 64 * kb[s] + 16 * k + gl < inf[s].y;
-                wc[s][k] = act ? C.w[off + 16 * k] : -0.0;
-                lj[s][k] = act ? (int)C.lst[off + 16 * k] : -1;
-            }
-        }
-        const int n1 = n0 + waves * kR;
-        int px1[kPickSlots];
-        int4 inf1[kPickSlots];
-        double bv1[kPickSlots][4];
-        double ul1 = 0;
-        if (n1 < n) {  // wave-uniform
-            ul1 = counter_u(counter_key(seed, (uint64_t)f_px, (uint64_t)f_smp, f_nid), 1);
-            load_rows(f_px, px1, inf1, bv1);
-            if (n1 + waves * kR < n) fetch(n1 + waves * kR);
-        }
-#pragma unroll
-        for (int s = 0; s < kPickSlots; s++) {
-            int pl;
-            {
-                unsigned cf = 64;
-                int cl = -1;
-#pragma unroll
-                for (int k = 3; k >= 0; k--) {
-                    const bool ok = !signbit(wc[s][k]);
-                    cf = ok && (base[s] + fabs(wc[s][k]) >= target[s]) ? 16 * k + gl : cf;
-                    cl = ok && cl < 0 ? 16 * k + gl : cl;  // the highest k wins
-                }
-                cf = row_min_u32(cf);
-                const int lastv = row_max_i32(cl);  // every lane of the row takes part in the DPP steps
-                pl = cf < 64 ? (int)cf : lastv;
-            }
-            double margin = INFINITY;
-            int pick = -1;
-            {
-                const int l1 = max(pl, 0), l0 = max(pl - 1, 0);
-                double sc[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) sc[k] = fabs(wc[s][k]);
-                const double s1 = bperm_f64(sel4(sc, l1 >> 4), g0 + (l1 & 15));
-                const double s0 = bperm_f64(sel4(sc, l0 >> 4), g0 + (l0 & 15));
-                const int pk = bperm_i32(sel4(lj[s], l1 >> 4), g0 + (l1 & 15));
-                if (pl >= 0) {  // pick_margin's terms
-                    const double c_hi = base[s] + s1;
-                    const double c_lo = pl > 0 ? base[s] + s0 : base[s];
-                    const double m_lo = c_lo == 0.0 ? INFINITY : target[s] - c_lo;
-                    margin = fmin(m_lo, c_hi - target[s]);
-                    pick = pk;
-                }
-            }
-            const int node = n0 + 4 * s + g;
-            bool amb = false;
-            if (gl == 0 && node < n) {
-                wsum_out[node] = wsum[s];
-                pick_out[node] = pick;
-                if (C.exact) {  // exact pick: the band stored by the cache build + this sum's rounding
-                    const double band = (double)__int_as_float(inf[s].w) + band_round(inf[s].y, wsum[s]);
-                    amb = !(pick_slack(margin, wsum[s]) > band);
-                }
-            }
-            if (C.exact) {  // one list atomic per wave (C.exact is launch-uniform)
-                const int q = wave_append(reinterpret_cast<unsigned*>(C.exact), amb);
-                if (amb) C.exact[kExactHead + q] = C.exact_off + node;
-            }
-        }
-        cached += (unsigned long long)min(kR, n - n0);
-        if (n1 < n) {
-            ul = ul1;
-#pragma unroll
-            for (int s = 0; s < kPickSlots; s++) {
-                px[s] = px1[s];
-                inf[s] = inf1[s];
-#pragma unroll
-                for (int k = 0; k < 4; k++) bv[s][k] = bv1[s][k];
-            }
-        }
-    }
-#else
     if (gw * kR < n) fetch(gw * kR);
     for (int n0 = gw * kR; n0 < n; n0 += waves * kR) {
         const int pxl = f_px;
@@ -2927,7 +2817,6 @@ __global__ __launch_bounds__(256, MCPT_LB_PICKG) void k_prep_pick_g(DScene S, ui
         }
         cached += (unsigned long long)min(kR, n - n0);
     }
-#endif
     if (lane == 0 && stats && cached) atomicAdd(stats + 0, cached);
 }
 
