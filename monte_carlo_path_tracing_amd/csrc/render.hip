@@ -4249,6 +4249,7 @@ struct DeviceState {
     DevBuf lit_slot, lit_pool;        // exact pick: roots' literal sums per pixel (RootLit)
     DevBuf sc_cum, sc_wsum, sc_last;  // small-table root-point cache (SmallCache)
     int spill_cap = 0;  // nodes the spill stack qs holds (grown on demand)
+    bool bvh8_tried = false;  // ensure_bvh8 ran on this device
     DevBuf g_start, g_tri;  // the scene's uniform grid (MCPT_ACCEL_GRID), version grid_version
     int grid_version = 0;
     unsigned* pinned_count = nullptr;
@@ -4260,7 +4261,9 @@ struct DeviceState {
 struct mcpt_scene {
     HostScene host;
     Bvh bvh, lbvh;
-    Bvh8 bvh8, lbvh8;  // 8-wide compressed trees of bvh / lbvh (k_rays_cw8)
+    Bvh8 bvh8, lbvh8;  // 8-wide compressed trees of bvh / lbvh (k_rays_cw8), built on first use (ensure_bvh8)
+    bool bvh8_built = false;
+    std::mutex bvh8_mu;
     Grid grid;             // Myobj::cal_scene_boundingbox(eye) + meshing(n0) (mcpt_scene_meshing)
     int grid_version = 0;  // bumped by every rebuild; devices re-upload on mismatch
     std::vector<std::unique_ptr<DeviceState>> devs;
@@ -4559,23 +4562,6 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, quantize_bvh4(b4), &d.bvh4q))) return rc;
     if ((rc = upload(*D, quantize_bvh4(lb4), &d.lbvh4q))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->lbvh), &d.lleaf_v))) return rc;
-    // the 8-wide trees (k_rays_cw8); a tree whose reserved node slots exceed the 24-bit stack base stays null
-    for (int t = 0; t < 2; t++) {
-        const Bvh8& b8 = t == 0 ? sc->bvh8 : sc->lbvh8;
-        if (b8.nodes.empty() || b8.nodes.size() >= (1u << 24)) continue;
-        std::vector<float4> tv8(3 * std::max<size_t>(b8.tri_facets.size(), 1), make_float4(0.f, 0.f, 0.f, 0.f));
-        for (size_t q = 0; q < b8.tri_facets.size(); q++) {
-            const int f = b8.tri_facets[q];
-            if (f < 0) continue;
-            for (int k = 0; k < 3; k++) {
-                float w;
-                std::memcpy(&w, &f, 4);
-                tv8[3 * q + k] = make_float4(s.pos[9 * f + 3 * k], s.pos[9 * f + 3 * k + 1], s.pos[9 * f + 3 * k + 2], k == 0 ? w : 0.0f);
-            }
-        }
-        if ((rc = upload(*D, b8.nodes, t == 0 ? &d.bvh8 : &d.lbvh8))) return rc;
-        if ((rc = upload(*D, tv8, t == 0 ? &d.tri8_v : &d.ltri8_v))) return rc;
-    }
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc(&D->pinned_count, 64 + kCtrlBytes));
     HIP_OK(hipEventCreate(&D->ev0));
@@ -4860,6 +4846,43 @@ int use_grid(mcpt_scene* sc, DeviceState& D, const double eye[3], int n0) {
 // every option a render checks before it starts (spp, sample range, mode, acceleration, flags) --
 // called first by every path, and by every rank of a communicator before any collective, so that a
 // bad option fails on all ranks alike instead of leaving some of them in the reduce
+// the 8-wide trees (k_rays_cw8, MCPT_DEBUG_RAYS_CW8 / MCPT_DEBUG_HIT_CW8, mcpt_debug_bvh8_check): built on the
+// host on first use (1.2 s for the 1 M-triangle scene, so only runs that ask for them pay it) and uploaded to
+// a device on its first use there; a tree whose reserved node slots exceed the 24-bit stack base stays null
+void ensure_bvh8_host(mcpt_scene* sc) {
+    std::lock_guard<std::mutex> lk(sc->bvh8_mu);
+    if (sc->bvh8_built) return;
+    sc->bvh8 = build_bvh8(sc->host, sc->bvh);
+    sc->lbvh8 = build_bvh8(sc->host, sc->lbvh);
+    sc->bvh8_built = true;
+}
+int ensure_bvh8(mcpt_scene* sc, DeviceState* D) {
+    ensure_bvh8_host(sc);
+    if (D->d.bvh8 || D->bvh8_tried) return MCPT_OK;
+    D->bvh8_tried = true;
+    DScene& d = D->d;
+    const HostScene& s = sc->host;
+    int rc;
+    HIP_OK(hipSetDevice(D->device));
+    for (int t = 0; t < 2; t++) {
+        const Bvh8& b8 = t == 0 ? sc->bvh8 : sc->lbvh8;
+        if (b8.nodes.empty() || b8.nodes.size() >= (1u << 24)) continue;
+        std::vector<float4> tv8(3 * std::max<size_t>(b8.tri_facets.size(), 1), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t q = 0; q < b8.tri_facets.size(); q++) {
+            const int f = b8.tri_facets[q];
+            if (f < 0) continue;
+            for (int k = 0; k < 3; k++) {
+                float w;
+                std::memcpy(&w, &f, 4);
+                tv8[3 * q + k] = make_float4(s.pos[9 * f + 3 * k], s.pos[9 * f + 3 * k + 1], s.pos[9 * f + 3 * k + 2], k == 0 ? w : 0.0f);
+            }
+        }
+        if ((rc = upload(*D, b8.nodes, t == 0 ? &d.bvh8 : &d.lbvh8))) return rc;
+        if ((rc = upload(*D, tv8, t == 0 ? &d.tri8_v : &d.ltri8_v))) return rc;
+    }
+    return MCPT_OK;
+}
+
 int validate_render(const mcpt_render_opts* o) {
     const int s0 = (o->sample_begin == 0 && o->sample_end == 0) ? 0 : o->sample_begin;
     const int s1 = (o->sample_begin == 0 && o->sample_end == 0) ? o->spp : o->sample_end;
@@ -5047,6 +5070,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         rl.slot = (int*)D.lit_slot.p;
         rl.pool = (double*)D.lit_pool.p;
     }
+    if ((MCPT_RAYS_CW8 || (o->flags & MCPT_DEBUG_RAYS_CW8)) && (rc = ensure_bvh8(sc, &D))) return rc;
     // every buffer is allocated above (first-call hipMalloc of the cache is not device work); the
     // timed region (seconds, HIP events) starts at the primary-hit kernel
     HIP_OK(hipMemsetAsync(D.stats.p, 0, kStatBytes, st));
@@ -5917,8 +5941,6 @@ static int finish_scene(HostScene&& hs, mcpt_scene** out) {
     constexpr int kMaxLeaf = 2;
     sc->bvh = build_bvh(sc->host, all, kMaxLeaf);
     sc->lbvh = build_bvh(sc->host, lights, kMaxLeaf);
-    sc->bvh8 = build_bvh8(sc->host, sc->bvh);
-    sc->lbvh8 = build_bvh8(sc->host, sc->lbvh);
     *out = sc;
     return MCPT_OK;
 }
@@ -6194,6 +6216,7 @@ int mcpt_closest_hit(mcpt_scene* sc, int32_t n, const double* ro, const double* 
     HIP_OK(hipMemcpy(drd, rd, 24ull * n, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(dex, ex, 4ull * n, hipMemcpyHostToDevice));
     if (flags & MCPT_DEBUG_HIT_CW8) {
+        if ((rc = ensure_bvh8(sc, D))) return rc;
         if (!D->d.bvh8 || !D->d.lbvh8) {
             set_error("MCPT_DEBUG_HIT_CW8: no 8-wide tree for this scene");
             return MCPT_E_INVALID;
@@ -6256,6 +6279,8 @@ int mcpt_debug_bvh8_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
         set_error("invalid argument");
         return MCPT_E_INVALID;
     }
+    std::lock_guard<std::mutex> lk(sc->mu);
+    ensure_bvh8_host(sc);
     const Bvh8& b = light_only ? sc->lbvh8 : sc->bvh8;
     const Bvh& bb = light_only ? sc->lbvh : sc->bvh;
     const HostScene& hs = sc->host;
