@@ -338,6 +338,9 @@ def main():
                                 sample_range=(k * world * S, (k + 1) * world * S), flags=flags, **multi)
         for key, v in st.as_dict().items():
             totals[key] = totals.get(key, 0) + v
+        # device time of the step: a device list runs its distinct devices concurrently, so its wall time on
+        # each of them (the shards' kernel times are summed in the other fields)
+        totals["device_seconds"] = totals.get("device_seconds", 0.0) + st.seconds * max(st.devices_used, 1)
         if rank == 0 and time.perf_counter() - tlog > 30:
             tlog = time.perf_counter()
             log("step %d/%d, %.1f s" % (k + 1, args.steps, tlog - t0))
@@ -373,10 +376,6 @@ def main():
         comm.close()
         dist.destroy_process_group()
         return
-    if devices is not None:
-        # every distinct device's shard ran concurrently: the device time of the run is its wall time
-        # on each of them (render_multi's stats sum the shards' kernel times)
-        totals["seconds"] = totals.get("seconds", 0.0) * max(totals.get("devices_used", 1) // max(args.steps, 1), 1)
     pmc = load_json(os.path.join(ROOT, "profiles", "pmc_latest.json")) or {"kernels": {}}
     # the PMC figures of this workload when they were profiled (tools/summarize_profiles.py), else the
     # headline's
@@ -395,7 +394,7 @@ def main():
     def pmc_src(*names):  # the summaries the matched kernels' PMC figures came from
         srcs = sorted({pk[k].get("source") or pmc.get("source") for n in names for k in busy(n)})
         return "; ".join(s for s in srcs if s) or None
-    dev_s = max(totals.get("seconds", 0.0), 1e-12)
+    dev_s = max(totals.get("device_seconds", 0.0), 1e-12)
     # ---- roofline of the light prep (rank 0's launches; HIP events on its stream) ----
     roof_prep = None
     prep_s = totals.get("prep_seconds", 0.0)
