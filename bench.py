@@ -446,8 +446,9 @@ def main():
     if tr_s > 0 and visits > 0:
         accel = scene.accel_bytes()
         # the library traces MIS / shade rays with persistent refilling waves when the BVHs exceed an
-        # XCD's 4 MiB L2 (render.hip MCPT_RAYS_PERSISTENT), one ray per thread otherwise
-        pers = accel > (4 << 20)
+        # XCD's 4 MiB L2 (render.hip MCPT_RAYS_PERSISTENT) and always for shade-area's rays
+        # (MCPT_PERSIST_SHADE_AREA, round 5), one ray per thread otherwise
+        pers = accel > (4 << 20) or args.mode == "shade_area"
         kname = "k_extend_brdf" if args.mode == "brdf" else ("k_rays_persistent" if pers else "k_mis_rays")
         t_launch = tr_s / tr_n
         fl = (visits * FLOPS_NODE_VISIT + tests * FLOPS_TRI_TEST_FP64 * 2) / tr_n

@@ -14,6 +14,12 @@ namespace mcpt {
 #define MCPT_PI 3.141592653589793
 #define MCPT_P_RR 0.6
 #define MCPT_MAX_DEPTH 48  // counter-RNG trees: deeper nodes contribute 0 (oracle COUNTER_MAX_DEPTH)
+#ifndef MCPT_PHONG_SQRT
+#define MCPT_PHONG_SQRT 1  // sample_phong: sin / cos of theta by identities (see there)
+#endif
+#ifndef MCPT_PHONG_SINCOSPI
+#define MCPT_PHONG_SINCOSPI 1  // sample_phong: phi's sin / cos as sincospi(2 k2)
+#endif
 
 struct d3 {
     double x, y, z;
@@ -141,9 +147,22 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
     double carg;
     if (ind == 0) carg = 1 - 2 * k1;
     else carg = pow(k1, 1 / (sh + 1));
+#if MCPT_PHONG_SQRT
+    // sin / cos of theta by the identities instead of acos + sincos (~180 fp64 VALU): for the cosine lobe
+    // theta = acos(x) / 2 with cos = sqrt((1 + x) / 2), sin = sqrt((1 - x) / 2); for the specular lobe theta =
+    // acos(c) with cos = c, sin = sqrt((1 - c)(1 + c)) (1 - c exact near c = 1, no cancellation).  Equal to the
+    // reference's acos -> sin / cos chain (BRDF.cpp:51-54, 71, 80, 99) up to a few ulp, as the pow below
+    (void)theta;
+    {
+        const double c = fmax(-1.0, fmin(1.0, carg));
+        st = sqrt(ind == 0 ? (1 - c) * 0.5 : (1 - c) * (1 + c));
+        ct = ind == 0 ? sqrt((1 + c) * 0.5) : c;
+    }
+#else
     theta = acos(fmax(-1.0, fmin(1.0, carg)));
     if (ind == 0) theta = 0.5 * theta;
     sincos(theta, &st, &ct);
+#endif
     if (ind == 0) {
         pdf *= ct / MCPT_PI;
     } else {
@@ -153,7 +172,12 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
         pdf *= (sh + 1) / (2 * MCPT_PI) * (carg > 0 ? k1 / carg : 0.0);
         axis = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
     }
+#if MCPT_PHONG_SINCOSPI
+    (void)phi;
+    sincospi(2 * k2, &sp, &cp);
+#else
     sincos(phi, &sp, &cp);
+#endif
     d3 nx;
     if (fabs(dot(axis, mk3(1, 0, 0)) - 1) > MCPT_EPS) nx = normalized(cross(axis, mk3(1, 0, 0)));
     else nx = normalized(cross(axis, mk3(0, 1, 0)));

@@ -1764,25 +1764,13 @@ __device__ inline double prep_weight_buf(__amdgpu_buffer_rsrc_t rw, int li, d3 x
                            mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1, ok);
 }
 // prep_weight_buf with the exact-pick bookkeeping (light_weight_bx); *lsum2 = the record's 2 sum L
-#ifndef MCPT_PK2_TIMING
-#define MCPT_PK2_TIMING 0  // timing-only builds: 1 = the records loaded but no fp64 weight math, 2 = neither
-#endif
 __device__ inline WeightBx prep_weight_buf_bx(__amdgpu_buffer_rsrc_t rw, int li, d3 x1, double* lsum2) {
-    if (MCPT_PK2_TIMING == 2) {
-        *lsum2 = 1.0;
-        return WeightBx{(double)(li + 1) * 1e-6, 1.0, 1.0, true, false};
-    }
     const v4u a = struct_load_b128(rw, li, 0, 0, 0);
     const v4u b = struct_load_b128(rw, li, 16, 0, 0);
     const v4u c = struct_load_b128(rw, li, 32, 0, 0);
     const v4u d = struct_load_b128(rw, li, 48, 0, 0);
     const v4u e = struct_load_b128(rw, li, 64, 0, 0);
     *lsum2 = u2d(e.z, e.w);
-    if (MCPT_PK2_TIMING == 1) {
-        const double w = fabs(u2d(a.x, a.y) + u2d(b.z, b.w) + u2d(c.x, c.y) + u2d(d.z, d.w) + u2d(e.x, e.y) + x1.x) * 1e-9 +
-                         fabs(u2d(e.z, e.w)) + 1e-12;
-        return WeightBx{w, 1.0, 1.0, true, false};
-    }
     return light_weight_bx<true>(mk3(u2d(a.x, a.y), u2d(a.z, a.w), u2d(b.x, b.y)),
                                  mk3(u2d(b.z, b.w), u2d(c.x, c.y), u2d(c.z, c.w)),
                                  mk3(u2d(d.x, d.y), u2d(d.z, d.w), u2d(e.x, e.y)), u2d(e.z, e.w), x1);

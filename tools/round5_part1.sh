@@ -1,6 +1,8 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 exec tools/gpu_steps.sh \
+ "300:r5l_ab_phong_brdf:ROUNDS=3 VARIANTS=\"S0 S1 S2\" tools/ab_run.sh --mode brdf --steps 1" \
+ "300:r5l_ab_phong_mis:ROUNDS=2 VARIANTS=\"S0 S1 S2\" tools/ab_run.sh" \
  "300:r5k_ab_pk2_timing:ROUNDS=2 VARIANTS=\"C T1 T2\" tools/ab_run.sh" \
  "600:r5_gputests:python -u -m pytest tests -m gpu -v -s --timeout 200 --timeout-method thread" \
  "300:r5_bench_default:python3 bench.py" \
