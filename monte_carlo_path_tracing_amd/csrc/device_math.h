@@ -14,11 +14,14 @@ namespace mcpt {
 #define MCPT_PI 3.141592653589793
 #define MCPT_P_RR 0.6
 #define MCPT_MAX_DEPTH 48  // counter-RNG trees: deeper nodes contribute 0 (oracle COUNTER_MAX_DEPTH)
+#ifndef MCPT_PHONG_SKIP_ZERO
+#define MCPT_PHONG_SKIP_ZERO 1  // brdf_phong / phong_pdf: no pow for a specular term that is exactly zero
+#endif
 #ifndef MCPT_PHONG_SQRT
-#define MCPT_PHONG_SQRT 1  // sample_phong: sin / cos of theta by identities (see there)
+#define MCPT_PHONG_SQRT 1  // BRDF-only sample_phong<true>: sin / cos of theta by identities (see there)
 #endif
 #ifndef MCPT_PHONG_SINCOSPI
-#define MCPT_PHONG_SINCOSPI 1  // sample_phong: phi's sin / cos as sincospi(2 k2)
+#define MCPT_PHONG_SINCOSPI 1  // BRDF-only sample_phong<true>: phi's sin / cos as sincospi(2 k2)
 #endif
 
 struct d3 {
@@ -105,11 +108,16 @@ __device__ __host__ inline double counter_u(uint64_t key, uint32_t dim) {
 }
 
 // ---- Phong BRDF (BRDF.cpp) --------------------------------------------------------------
+// a specular term that is exactly zero: with c <= 1 + 1e-9 (unit vectors give c <= 1 + a few ulp) and
+// 0 <= sh <= 1e6, pow(c, sh) lies in [0, 1.002), so a zero factor (ks = 0, or the pdf's lobe weight 0) makes the
+// term +-0, and x + +-0 = x for the non-negative diffuse part -- skipping the fp64 pow (~220 VALU) there is
+// bit-exact; a wave of diffuse-only lanes (the stand-in's floor and backdrop) branches round it
+__device__ inline bool phong_pow_bounded(double c, double sh) { return c <= 1.000000001 && sh >= 0 && sh <= 1e6; }
 __device__ inline d3 brdf_phong(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:17-25
     d3 R = add(mul(wi, -1), mul(n, 2 * dot(wi, n)));
     d3 ans = mul(kd, 1.0 / MCPT_PI);
     double c = dot(wr, R);
-    if (c > 0) ans = add(ans, mul(ks, (sh + 1) * pow(c, sh) / (2 * MCPT_PI)));
+    if (c > 0 && !(MCPT_PHONG_SKIP_ZERO && ks.x == 0 && ks.y == 0 && ks.z == 0 && phong_pow_bounded(c, sh))) ans = add(ans, mul(ks, (sh + 1) * pow(c, sh) / (2 * MCPT_PI)));
     return ans;
 }
 __device__ inline double phong_pdf(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:107-133
@@ -123,11 +131,16 @@ __device__ inline double phong_pdf(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) 
     d3 R = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
     double cs = dot(wi, R);
     if (cs < 0) ps *= 0;
-    else ps *= (sh + 1) / (2 * MCPT_PI) * pow(cs, sh);
+    else if (!(MCPT_PHONG_SKIP_ZERO && ps == 0 && phong_pow_bounded(cs, sh))) ps *= (sh + 1) / (2 * MCPT_PI) * pow(cs, sh);  // else +0 stays
     return pd + ps;
 }
 // sample_from_phong (BRDF.cpp:28-104) with explicit uniforms: lobe pick u0 (lower_bound on the
 // normalised {p0, 1}), xi1, xi2.  May return directions below the surface (reference).
+// kIdent (the BRDF-only kernels): theta's and phi's sin / cos without acos / sincos (MCPT_PHONG_SQRT,
+// MCPT_PHONG_SINCOSPI), a few ulp from the reference's chain.  The MIS and shade() kernels keep the chain:
+// there a sampled direction that hits a sliver light feeds the light pdf's ill-conditioned solid angle,
+// and a few-ulp direction change moved two C1 MIS pixels by 2.9e-3 (tests/test_c1_frame.py)
+template <bool kIdent = false>
 __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u0, double k1, double k2,
                                   double* pdf_out) {
     double d = dot(kd, mk3(1, 1, 1)) / 3;
@@ -147,22 +160,19 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
     double carg;
     if (ind == 0) carg = 1 - 2 * k1;
     else carg = pow(k1, 1 / (sh + 1));
-#if MCPT_PHONG_SQRT
-    // sin / cos of theta by the identities instead of acos + sincos (~180 fp64 VALU): for the cosine lobe
-    // theta = acos(x) / 2 with cos = sqrt((1 + x) / 2), sin = sqrt((1 - x) / 2); for the specular lobe theta =
-    // acos(c) with cos = c, sin = sqrt((1 - c)(1 + c)) (1 - c exact near c = 1, no cancellation).  Equal to the
-    // reference's acos -> sin / cos chain (BRDF.cpp:51-54, 71, 80, 99) up to a few ulp, as the pow below
-    (void)theta;
-    {
+    if (kIdent && MCPT_PHONG_SQRT) {
+        // sin / cos of theta by the identities instead of acos + sincos (~180 fp64 VALU): for the cosine lobe
+        // theta = acos(x) / 2 with cos = sqrt((1 + x) / 2), sin = sqrt((1 - x) / 2); for the specular lobe
+        // theta = acos(c) with cos = c, sin = sqrt((1 - c)(1 + c)) (1 - c exact near c = 1, no cancellation).
+        // Equal to the reference's acos -> sin / cos chain (BRDF.cpp:51-54, 71, 80, 99) up to a few ulp
         const double c = fmax(-1.0, fmin(1.0, carg));
         st = sqrt(ind == 0 ? (1 - c) * 0.5 : (1 - c) * (1 + c));
         ct = ind == 0 ? sqrt((1 + c) * 0.5) : c;
+    } else {
+        theta = acos(fmax(-1.0, fmin(1.0, carg)));
+        if (ind == 0) theta = 0.5 * theta;
+        sincos(theta, &st, &ct);
     }
-#else
-    theta = acos(fmax(-1.0, fmin(1.0, carg)));
-    if (ind == 0) theta = 0.5 * theta;
-    sincos(theta, &st, &ct);
-#endif
     if (ind == 0) {
         pdf *= ct / MCPT_PI;
     } else {
@@ -172,12 +182,8 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
         pdf *= (sh + 1) / (2 * MCPT_PI) * (carg > 0 ? k1 / carg : 0.0);
         axis = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
     }
-#if MCPT_PHONG_SINCOSPI
-    (void)phi;
-    sincospi(2 * k2, &sp, &cp);
-#else
-    sincos(phi, &sp, &cp);
-#endif
+    if (kIdent && MCPT_PHONG_SINCOSPI) sincospi(2 * k2, &sp, &cp);
+    else sincos(phi, &sp, &cp);
     d3 nx;
     if (fabs(dot(axis, mk3(1, 0, 0)) - 1) > MCPT_EPS) nx = normalized(cross(axis, mk3(1, 0, 0)));
     else nx = normalized(cross(axis, mk3(0, 1, 0)));

@@ -4064,7 +4064,7 @@ __global__ __launch_bounds__(256) void k_brdf_gen(Params P, Queue cur, int n, Au
     const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
     const double sh = m[6];
     double pdf;
-    const d3 wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+    const d3 wi = sample_phong<true>(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
     int flags = 0;
     d3 w2 = mk3(0, 0, 0);
     if (!(dot(wi, N) < 0)) {
@@ -4139,11 +4139,11 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
         const d3 kd = mk3(m[0], m[1], m[2]), ks = mk3(m[3], m[4], m[5]);
         const double sh = m[6];
         double pdf;
-        wi = sample_phong(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
+        wi = sample_phong<true>(N, wo, kd, ks, sh, counter_u(key, 4), counter_u(key, 5), counter_u(key, 6), &pdf);
 #if MCPT_BRDF_TIMING == 1  // timing-only build: the sampling and shading run twice (cost share of that region)
         {
             double pdf2;
-            const d3 wi2 = sample_phong(N, wo, kd, ks, sh, counter_u(key, 7), counter_u(key, 8), counter_u(key, 9), &pdf2);
+            const d3 wi2 = sample_phong<true>(N, wo, kd, ks, sh, counter_u(key, 7), counter_u(key, 8), counter_u(key, 9), &pdf2);
             const d3 b2 = brdf_phong(N, wi2, wo, kd, ks, sh);
             if (P.mode == 12345) wi = wi2, pdf = pdf2 + b2.x;
         }
