@@ -111,13 +111,16 @@ __device__ __host__ inline double counter_u(uint64_t key, uint32_t dim) {
 // a specular term that is exactly zero: with c <= 1 + 1e-9 (unit vectors give c <= 1 + a few ulp) and
 // 0 <= sh <= 1e6, pow(c, sh) lies in [0, 1.002), so a zero factor (ks = 0, or the pdf's lobe weight 0) makes the
 // term +-0, and x + +-0 = x for the non-negative diffuse part -- skipping the fp64 pow (~220 VALU) there is
-// bit-exact; a wave of diffuse-only lanes (the stand-in's floor and backdrop) branches round it
+// bit-exact; a wave of diffuse-only lanes (the stand-in's floor and backdrop) branches round it.  kSkip = false in
+// the BRDF-only kernels, where the branch cost more than it saved (C2 -1.7%; C3 +0.35%, C5 +0.5%:
+// profiles/round5_ab_phong_skip.txt)
 __device__ inline bool phong_pow_bounded(double c, double sh) { return c <= 1.000000001 && sh >= 0 && sh <= 1e6; }
+template <bool kSkip = true>
 __device__ inline d3 brdf_phong(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:17-25
     d3 R = add(mul(wi, -1), mul(n, 2 * dot(wi, n)));
     d3 ans = mul(kd, 1.0 / MCPT_PI);
     double c = dot(wr, R);
-    if (c > 0 && !(MCPT_PHONG_SKIP_ZERO && ks.x == 0 && ks.y == 0 && ks.z == 0 && phong_pow_bounded(c, sh))) ans = add(ans, mul(ks, (sh + 1) * pow(c, sh) / (2 * MCPT_PI)));
+    if (c > 0 && !(kSkip && MCPT_PHONG_SKIP_ZERO && ks.x == 0 && ks.y == 0 && ks.z == 0 && phong_pow_bounded(c, sh))) ans = add(ans, mul(ks, (sh + 1) * pow(c, sh) / (2 * MCPT_PI)));
     return ans;
 }
 __device__ inline double phong_pdf(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:107-133
