@@ -12,6 +12,8 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <memory>
+#include <thread>
 
 #include "mcpt_internal.h"
 
@@ -47,7 +49,16 @@ struct Prim {
     int32_t facet;
 };
 
-constexpr int kBins = 16;
+#ifndef MCPT_BVH_BINS
+#define MCPT_BVH_BINS 32
+#endif
+#ifndef MCPT_BVH_ALL_AXES
+#define MCPT_BVH_ALL_AXES 1  // binned SAH over all three centroid axes (0: the widest only, rounds 1-4)
+#endif
+#ifndef MCPT_BVH_SWEEP
+#define MCPT_BVH_SWEEP 65536  // nodes of at most this many triangles: exact SAH sweep over all three axes
+#endif
+constexpr int kBins = MCPT_BVH_BINS;
 constexpr int kMaxDepth = 40;  // device traversal stack is 48 entries
 
 struct Builder {
@@ -83,24 +94,20 @@ struct Builder {
         if (n <= max_leaf) return -1;
         Box cb;
         for (int i = b; i < e; i++) cb.grow(prims[i].c);
-        int axis = 0;
-        double ext = -1;
-        for (int c = 0; c < 3; c++)
-            if (cb.hi[c] - cb.lo[c] > ext) {
-                ext = cb.hi[c] - cb.lo[c];
-                axis = c;
-            }
-        int mid = -1;
-        if (ext > 0) {
+        int widest = 0;
+        for (int c = 1; c < 3; c++)
+            if (cb.hi[c] - cb.lo[c] > cb.hi[widest] - cb.lo[widest]) widest = c;
+        // the best binned split along one axis: (cost, first bin of the right side), bin index of a prim
+        auto bin_of = [&](const Prim& p, int axis) {
+            const double ext = cb.hi[axis] - cb.lo[axis];
+            const int i = static_cast<int>((p.c[axis] - cb.lo[axis]) * (kBins * (1 - 1e-9) / ext));
+            return std::min(kBins - 1, std::max(0, i));
+        };
+        auto sweep = [&](int axis, double* cost_out) {
             Box bb[kBins];
             int cnt[kBins] = {0};
-            const double k = kBins * (1 - 1e-9) / ext;
-            auto bin_of = [&](const Prim& p) {
-                int i = static_cast<int>((p.c[axis] - cb.lo[axis]) * k);
-                return std::min(kBins - 1, std::max(0, i));
-            };
             for (int i = b; i < e; i++) {
-                int q = bin_of(prims[i]);
+                const int q = bin_of(prims[i], axis);
                 cnt[q]++;
                 bb[q].grow(prims[i].box);
             }
@@ -122,19 +129,68 @@ struct Builder {
                 acc.grow(bb[s - 1]);
                 ac += cnt[s - 1];
                 if (ac == 0 || right_cnt[s] == 0) continue;
-                double cost = acc.area() * ac + right_area[s] * right_cnt[s];
+                const double cost = acc.area() * ac + right_area[s] * right_cnt[s];
                 if (cost < best) {
                     best = cost;
                     best_s = s;
                 }
             }
+            *cost_out = best;
+            return best_s;
+        };
+        if (n <= MCPT_BVH_SWEEP) {  // exact SAH: every split position of the centroid order on every axis
+            struct AxisBest {
+                double cost = DBL_MAX;
+                int k = -1;
+                std::vector<std::pair<double, int>> key;
+            } ab[3];
+            auto sweep_axis = [&](int c) {
+                AxisBest& r = ab[c];
+                r.key.resize(n);
+                for (int i = 0; i < n; i++) r.key[i] = {prims[b + i].c[c], i};
+                std::sort(r.key.begin(), r.key.end());  // ties by index: a stable order
+                std::vector<double> right(n);
+                Box acc;
+                for (int i = n - 1; i > 0; i--) acc.grow(prims[b + r.key[i].second].box), right[i] = acc.area() * (n - i);
+                acc = Box();
+                for (int i = 1; i < n; i++) {
+                    acc.grow(prims[b + r.key[i - 1].second].box);
+                    const double cost = acc.area() * i + right[i];
+                    if (cost < r.cost) r.cost = cost, r.k = i;
+                }
+            };
+            if (n >= 8192) {  // large nodes: the three axes on three threads
+                std::thread t1(sweep_axis, 1), t2(sweep_axis, 2);
+                sweep_axis(0);
+                t1.join();
+                t2.join();
+            } else {
+                for (int c = 0; c < 3; c++) sweep_axis(c);
+            }
+            int bax = -1;
+            for (int c = 0; c < 3; c++)
+                if (ab[c].k > 0 && (bax < 0 || ab[c].cost < ab[bax].cost)) bax = c;
+            if (bax < 0 || !(ab[bax].cost < box.area() * n || n > 4 * max_leaf)) return -1;
+            std::vector<Prim> tmp(n);
+            for (int i = 0; i < n; i++) tmp[i] = prims[b + ab[bax].key[i].second];
+            std::copy(tmp.begin(), tmp.end(), prims.begin() + b);
+            return b + ab[bax].k;
+        }
+        int axis = widest, best_s = -1;
+        double best = DBL_MAX;
+        for (int c = 0; c < 3; c++) {
+            if (!(cb.hi[c] - cb.lo[c] > 0) || (!MCPT_BVH_ALL_AXES && c != widest)) continue;
+            double cost;
+            const int s_c = sweep(c, &cost);
+            if (s_c > 0 && cost < best) best = cost, best_s = s_c, axis = c;
+        }
+        int mid = -1;
+        if (cb.hi[widest] - cb.lo[widest] > 0) {
             const double leaf_cost = box.area() * n;
             if (best_s > 0 && (best < leaf_cost || n > 4 * max_leaf)) {
                 auto it = std::partition(prims.begin() + b, prims.begin() + e,
-                                         [&](const Prim& p) { return bin_of(p) < best_s; });
+                                         [&](const Prim& p) { return bin_of(p, axis) < best_s; });
                 mid = static_cast<int>(it - prims.begin());
-            } else if (best_s <= 0 || n <= max_leaf) {
-                return -1;
             } else {
                 return -1;
             }
@@ -148,29 +204,48 @@ struct Builder {
         return mid;
     }
 
-    // builds the subtree of [b, e) as the child slot `slot` of node `parent`
-    void build(int b, int e, int32_t parent, int slot, int depth) {
-        Box box = bounds(b, e);
-        BvhNode& pn = out->nodes[parent];
-        to_float_box(box, pn.lo[slot], pn.hi[slot]);
-        int mid = (depth >= kMaxDepth) ? -1 : split(b, e, box);
+    // Two phases, so that the (dominant) split searches of disjoint ranges run in parallel while the
+    // node / leaf order stays the serial DFS order: plan() decides every split of [b, e) (split() only
+    // permutes prims[b, e)), ranges above kParallelPrims on their own thread; emit() writes the nodes.
+    struct Plan {
+        int mid = -1;  // < 0: leaf
+        std::unique_ptr<Plan> l, r;
+    };
+    static constexpr int kParallelPrims = 1 << 17;
+    std::unique_ptr<Plan> plan(int b, int e, int depth) {
+        auto p = std::make_unique<Plan>();
+        int mid = (depth >= kMaxDepth) ? -1 : split(b, e, bounds(b, e));
         if (mid < 0) {
-            if (e - b > 64) {  // depth cap reached with a fat leaf: force a median split anyway
-                mid = b + (e - b) / 2;
-            } else {
-                int32_t cnt;
-                int32_t leaf = make_leaf(b, e, cnt);
-                out->nodes[parent].child[slot] = leaf;
-                out->nodes[parent].count[slot] = cnt;
-                return;
-            }
+            if (e - b <= 64) return p;
+            mid = b + (e - b) / 2;  // depth cap reached with a fat leaf: force a median split anyway
+        }
+        p->mid = mid;
+        if (e - b > kParallelPrims) {
+            std::thread t([&] { p->l = plan(b, mid, depth + 1); });
+            p->r = plan(mid, e, depth + 1);
+            t.join();
+        } else {
+            p->l = plan(b, mid, depth + 1);
+            p->r = plan(mid, e, depth + 1);
+        }
+        return p;
+    }
+    // writes the planned subtree of [b, e) as the child slot `slot` of node `parent`
+    void emit(int b, int e, int32_t parent, int slot, const Plan& p) {
+        to_float_box(bounds(b, e), out->nodes[parent].lo[slot], out->nodes[parent].hi[slot]);
+        if (p.mid < 0) {
+            int32_t cnt;
+            int32_t leaf = make_leaf(b, e, cnt);
+            out->nodes[parent].child[slot] = leaf;
+            out->nodes[parent].count[slot] = cnt;
+            return;
         }
         int32_t me = static_cast<int32_t>(out->nodes.size());
         out->nodes.push_back(BvhNode{});
         out->nodes[parent].child[slot] = me;
         out->nodes[parent].count[slot] = 0;
-        build(b, mid, me, 0, depth + 1);
-        build(mid, e, me, 1, depth + 1);
+        emit(b, p.mid, me, 0, *p.l);
+        emit(p.mid, e, me, 1, *p.r);
     }
 };
 
@@ -216,8 +291,12 @@ Bvh build_bvh(const HostScene& s, const std::vector<int32_t>& facets, int max_le
         bvh.nodes[0].child[0] = B.make_leaf(0, n, cnt);
         bvh.nodes[0].count[0] = cnt;
     } else {
-        B.build(0, mid, 0, 0, 1);
-        B.build(mid, n, 0, 1, 1);
+        std::unique_ptr<Builder::Plan> pl, pr;
+        std::thread t([&] { pl = B.plan(0, mid, 1); });
+        pr = B.plan(mid, n, 1);
+        t.join();
+        B.emit(0, mid, 0, 0, *pl);
+        B.emit(mid, n, 0, 1, *pr);
     }
     return bvh;
 }

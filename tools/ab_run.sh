@@ -9,6 +9,6 @@ VARIANTS=${VARIANTS:-A B}
 for r in $(seq "$ROUNDS"); do
     for v in $VARIANTS; do
         out=$(MCPT_LIB_PATH=ab/lib$v.so timeout -k 10 200 python bench.py --no-cpu "$@" 2>/dev/null | grep '^{') || exit 1
-        echo "$v $(echo "$out" | python -c 'import sys,json; d=json.loads(sys.stdin.read()); p=d.get("roofline_prep") or {}; t=d.get("roofline_trace") or {}; print(d["value"], "prep_ms", p.get("avg_launch_ms"), "trace_ms", t.get("avg_launch_ms"))')"
+        echo "$v $(echo "$out" | python -c 'import sys,json; d=json.loads(sys.stdin.read()); p=d.get("roofline_prep") or {}; t=d.get("roofline_trace") or {}; print(d["value"], "prep_ms", p.get("avg_launch_ms"), "trace_ms", t.get("avg_launch_ms"), "visits", t.get("node_visits_per_ray"), "tests", t.get("tri_tests_per_ray"))')"
     done
 done
