@@ -58,6 +58,9 @@ struct Prim {
 #ifndef MCPT_BVH_SWEEP
 #define MCPT_BVH_SWEEP 65536  // nodes of at most this many triangles: exact SAH sweep over all three axes
 #endif
+#ifndef MCPT_BVH_CTRAV
+#define MCPT_BVH_CTRAV 0.0  // SAH: cost of an inner node in triangle tests (0: split whenever the children test fewer)
+#endif
 constexpr int kBins = MCPT_BVH_BINS;
 constexpr int kMaxDepth = 40;  // device traversal stack is 48 entries
 
@@ -170,7 +173,7 @@ struct Builder {
             int bax = -1;
             for (int c = 0; c < 3; c++)
                 if (ab[c].k > 0 && (bax < 0 || ab[c].cost < ab[bax].cost)) bax = c;
-            if (bax < 0 || !(ab[bax].cost < box.area() * n || n > 4 * max_leaf)) return -1;
+            if (bax < 0 || !(ab[bax].cost + MCPT_BVH_CTRAV * box.area() < box.area() * n || n > 4 * max_leaf)) return -1;
             std::vector<Prim> tmp(n);
             for (int i = 0; i < n; i++) tmp[i] = prims[b + ab[bax].key[i].second];
             std::copy(tmp.begin(), tmp.end(), prims.begin() + b);
@@ -187,7 +190,7 @@ struct Builder {
         int mid = -1;
         if (cb.hi[widest] - cb.lo[widest] > 0) {
             const double leaf_cost = box.area() * n;
-            if (best_s > 0 && (best < leaf_cost || n > 4 * max_leaf)) {
+            if (best_s > 0 && (best + MCPT_BVH_CTRAV * box.area() < leaf_cost || n > 4 * max_leaf)) {
                 auto it = std::partition(prims.begin() + b, prims.begin() + e,
                                          [&](const Prim& p) { return bin_of(p, axis) < best_s; });
                 mid = static_cast<int>(it - prims.begin());

@@ -5926,7 +5926,10 @@ static int finish_scene(HostScene&& hs, mcpt_scene** out) {
     // triangle costs a fp64 Cramer test, a box only fp32 slabs (same-box A/B of the leaf bound:
     // 1 -> Veach MIS -1% / Cornell-1M +20%, 2 -> +1.5% / +16%, 3 -> +1% / +7%, 8 -> -5% / -24%,
     // each against 4)
-    constexpr int kMaxLeaf = 2;
+#ifndef MCPT_BVH_MAX_LEAF
+#define MCPT_BVH_MAX_LEAF 2
+#endif
+    constexpr int kMaxLeaf = MCPT_BVH_MAX_LEAF;
     sc->bvh = build_bvh(sc->host, all, kMaxLeaf);
     sc->lbvh = build_bvh(sc->host, lights, kMaxLeaf);
     *out = sc;
