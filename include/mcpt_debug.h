@@ -82,6 +82,10 @@ int mcpt_debug_tri_filter(int32_t n, const float* tri, const double* ro, const d
  * facets reached more than once, errors (bad indices, or a triangle vertex outside the decoded box of a slot
  * on its path), depth. */
 int mcpt_debug_bvh8_check(mcpt_scene* scene, int32_t light_only, int64_t out[6]);
+// The 4-wide tree of every traversal kernel (collapse_bvh4) and its quantized form (quantize_bvh4), walked on
+// the host: out = {nodes, facets reached, facets in the binary tree, facets reached twice, errors (a vertex
+// outside an ancestor slot's box, a quantized slot box not containing its fp32 box, a bad index), depth}.
+int mcpt_debug_bvh4_check(mcpt_scene* scene, int32_t light_only, int64_t out[6]);
 
 #ifdef __cplusplus
 }

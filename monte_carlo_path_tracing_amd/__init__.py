@@ -97,7 +97,7 @@ EXPORTS = ["mcpt_version", "mcpt_last_error", "mcpt_scene_load", "mcpt_scene_cre
            "mcpt_closest_hit", "mcpt_light_prep", "mcpt_primary_hits", "mcpt_tone_map",
            "mcpt_write_bmp", "mcpt_comm_unique_id", "mcpt_comm_init_rank", "mcpt_comm_destroy"]
 DEBUG_EXPORTS = ["mcpt_debug_prep_bench", "mcpt_debug_tri_filter", "mcpt_debug_light_prep_exact", "mcpt_debug_light_literal",
-                 "mcpt_debug_set_collective_lib", "mcpt_debug_bvh8_check"]  # include/mcpt_debug.h
+                 "mcpt_debug_set_collective_lib", "mcpt_debug_bvh8_check", "mcpt_debug_bvh4_check"]  # include/mcpt_debug.h
 
 
 def lib():
@@ -147,7 +147,8 @@ def lib():
                "mcpt_debug_light_prep_exact": [P, I, dp, dp, dp, dp, ip, ip],
                "mcpt_debug_light_literal": [P, dp, dp, dp],
                "mcpt_debug_set_collective_lib": [C.c_char_p],
-               "mcpt_debug_bvh8_check": [P, I, np.ctypeslib.ndpointer(np.int64, flags="C")]}
+               "mcpt_debug_bvh8_check": [P, I, np.ctypeslib.ndpointer(np.int64, flags="C")],
+               "mcpt_debug_bvh4_check": [P, I, np.ctypeslib.ndpointer(np.int64, flags="C")]}
         for name, argt in dbg.items():
             if hasattr(L, name):
                 getattr(L, name).argtypes = argt
@@ -377,6 +378,14 @@ def debug_bvh8_check(scene, light_only=False):
     nodes, tris, facets, duplicates, errors, depth."""
     out = np.zeros(6, np.int64)
     _check(lib().mcpt_debug_bvh8_check(scene.h, 1 if light_only else 0, out))
+    return dict(zip(("nodes", "tris", "facets", "duplicates", "errors", "depth"), (int(v) for v in out)))
+
+
+def debug_bvh4_check(scene, light_only=False):
+    """Diagnostics (host only): the 4-wide tree every traversal reads and its quantized form against the
+    binary tree (include/mcpt_debug.h).  Returns dict nodes, tris, facets, duplicates, errors, depth."""
+    out = np.zeros(6, np.int64)
+    _check(lib().mcpt_debug_bvh4_check(scene.h, 1 if light_only else 0, out))
     return dict(zip(("nodes", "tris", "facets", "duplicates", "errors", "depth"), (int(v) for v in out)))
 
 

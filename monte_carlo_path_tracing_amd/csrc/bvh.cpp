@@ -361,6 +361,7 @@ int32_t collapse(const Bvh& b, int32_t n2, std::vector<BvhNode4>& out) {
     }
     return me;
 }
+
 }  // namespace
 
 std::vector<BvhNode4> collapse_bvh4(const Bvh& b) {

@@ -6335,6 +6335,81 @@ int mcpt_debug_bvh8_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
     return MCPT_OK;
 }
 
+// the 4-wide tree every traversal kernel reads (collapse_bvh4 of the binary tree) and its quantized form
+// (quantize_bvh4), walked on the host: every facet of the binary tree reached exactly once, each vertex
+// inside every ancestor slot's box, and every quantized slot box containing its fp32 box (the conservative
+// rounding the persistent traversal relies on)
+int mcpt_debug_bvh4_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
+    if (!sc || !out) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(sc->mu);
+    const Bvh& bb = light_only ? sc->lbvh : sc->bvh;
+    const std::vector<BvhNode4> b4 = collapse_bvh4(bb);
+    const std::vector<BvhNode4Q> q4 = quantize_bvh4(b4);
+    const HostScene& hs = sc->host;
+    int64_t nodes = 0, tris = 0, dup = 0, bad = 0, maxd = 0;
+    std::vector<int> seen(hs.F, 0);
+    struct Box {
+        float lo[3], hi[3];
+    };
+    std::vector<Box> path;
+    std::function<void(int32_t, int)> walk = [&](int32_t ni, int depth) {
+        if (ni < 0 || (size_t)ni >= b4.size()) {
+            bad++;
+            return;
+        }
+        nodes++;
+        maxd = std::max<int64_t>(maxd, depth);
+        const BvhNode4& n = b4[ni];
+        const BvhNode4Q& q = q4[ni];
+        for (int k = 0; k < 4; k++) {
+            if (n.child[k] == kBvh4Empty || (n.child[k] < 0 && n.count[k] == 0)) continue;
+            Box bx;
+            for (int a = 0; a < 3; a++) {
+                bx.lo[a] = n.lo[a][k], bx.hi[a] = n.hi[a][k];
+                const uint32_t bits = ((q.ex >> (8 * a)) & 0xffu) << 23;
+                float sc_;
+                std::memcpy(&sc_, &bits, 4);
+                const float ql = std::fmaf((float)((q.q[2 * a] >> (8 * k)) & 0xffu), sc_, q.org[a]);
+                const float qh = std::fmaf((float)((q.q[2 * a + 1] >> (8 * k)) & 0xffu), sc_, q.org[a]);
+                if (!(ql <= bx.lo[a] && qh >= bx.hi[a])) bad++;
+            }
+            path.push_back(bx);
+            if (n.child[k] >= 0) {
+                walk(n.child[k], depth + 1);
+            } else {
+                const int32_t first = ~n.child[k];
+                for (int32_t j = first; j < first + n.count[k]; j++) {
+                    if (j < 0 || (size_t)j >= bb.leaf_facets.size() || bb.leaf_facets[j] < 0 || bb.leaf_facets[j] >= hs.F) {
+                        bad++;
+                        continue;
+                    }
+                    const int f = bb.leaf_facets[j];
+                    tris++;
+                    if (seen[f]++) dup++;
+                    for (const Box& p : path)
+                        for (int v = 0; v < 3; v++)
+                            for (int a = 0; a < 3; a++) {
+                                const float x = hs.pos[9 * (size_t)f + 3 * v + a];
+                                if (!(x >= p.lo[a] && x <= p.hi[a])) bad++;
+                            }
+                }
+            }
+            path.pop_back();
+        }
+    };
+    if (!b4.empty()) walk(0, 1);
+    out[0] = nodes;
+    out[1] = tris;
+    out[2] = (int64_t)bb.leaf_facets.size();
+    out[3] = dup;
+    out[4] = bad;
+    out[5] = maxd;
+    return MCPT_OK;
+}
+
 int mcpt_debug_tri_filter(int32_t n, const float* tri, const double* ro, const double* rd, const float* tlim,
                           int32_t* verdict, float* tup) {
     if (n < 0 || (n > 0 && (!tri || !ro || !rd || !tlim || !verdict || !tup))) return MCPT_E_INVALID;

@@ -1,0 +1,43 @@
+"""The 4-wide tree every traversal kernel reads (collapse_bvh4 of the binary SAH tree, bvh.cpp) and its
+quantized form (quantize_bvh4, the persistent traversal's 64-B nodes), checked on the host through
+mcpt_debug_bvh4_check: every facet of the binary tree reached exactly once, every vertex inside the fp32
+box of every slot on its path, and every quantized slot box containing its fp32 box -- the conservative
+pruning that keeps the closest hits equal to the reference's (Myobj.cpp:334-474 / :476-622 replaced by the
+BVH).  The GPU side (the same trees' hits against the reference's golden rays and the
+brute force) is test_gpu_parity.py."""
+import pytest
+
+from conftest import SCENE_OBJ, SCENE_XML, cornell_scene
+import monte_carlo_path_tracing_amd as mcpt
+import scenegen
+
+
+def ok(r, nf):
+    return r["tris"] == r["facets"] == nf and r["duplicates"] == 0 and r["errors"] == 0 and r["nodes"] > 0
+
+
+@pytest.mark.parametrize("light_only", [False, True])
+def test_bvh4_structure_veach(light_only):
+    sc = mcpt.Scene.load(SCENE_OBJ, SCENE_XML)
+    r = mcpt.debug_bvh4_check(sc, light_only)
+    print("veach bvh4 (light_only=%s): %s" % (light_only, r))
+    assert ok(r, sc.nlights if light_only else sc.nfacets), r
+
+
+@pytest.mark.parametrize("name", ["occluded_room", "sphere_mix", "slivers", "tiny_far", "dense_sphere", "light_panel"])
+def test_bvh4_structure_generated(tmp_path, name):
+    gen = getattr(scenegen, name, None)
+    if gen is None:
+        pytest.skip("no scene %s" % name)
+    sc = mcpt.Scene.load(*gen(str(tmp_path)))
+    for lo in (False, True):
+        r = mcpt.debug_bvh4_check(sc, lo)
+        assert ok(r, sc.nlights if lo else sc.nfacets), (name, lo, r)
+
+
+def test_bvh4_structure_cornell_1m():
+    sc = mcpt.Scene.load(*cornell_scene(1000000))
+    r = mcpt.debug_bvh4_check(sc)
+    print("cornell-1M bvh4: %s" % r)
+    assert ok(r, sc.nfacets), r
+    assert r["depth"] <= 40  # the traversal stacks hold 48 entries
