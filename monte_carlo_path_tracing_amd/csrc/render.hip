@@ -6265,6 +6265,114 @@ int mcpt_debug_light_literal(mcpt_scene* sc, const double* x1, const double* nrm
 // host-only check of an 8-wide tree (include/mcpt_debug.h): every facet of the binary tree is reached exactly
 // once, and every reached triangle's vertices lie inside the decoded box of every slot on its path (the
 // traversal prunes with those boxes, so this is what keeps its hits the binary tree's)
+// references beyond the first of each facet in a binary tree's leaf list (spatial splits repeat facets)
+static int64_t dup_refs(const Bvh& b) {
+    std::vector<int32_t> f(b.leaf_facets);
+    std::sort(f.begin(), f.end());
+    return (int64_t)(f.size() - (std::unique(f.begin(), f.end()) - f.begin()));
+}
+// A facet may sit in several leaves (spatial splits, each reference with its triangle clipped to one side):
+// then its references' regions (the intersection of the slot boxes on each one's path) must together cover
+// the triangle -- checked at the vertices, edge points and interior points; a facet with one reference
+// needs all three vertices inside every box on its path.
+struct RefRegion {
+    int32_t f;
+    float lo[3], hi[3];
+};
+static int64_t check_coverage(const HostScene& hs, std::vector<RefRegion>& refs) {
+    std::sort(refs.begin(), refs.end(), [](const RefRegion& x, const RefRegion& y) { return x.f < y.f; });
+    int64_t bad = 0;
+    static const double kW[][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {.5, .5, 0}, {0, .5, .5}, {.5, 0, .5}, {1. / 3, 1. / 3, 1. / 3},
+                                   {.8, .1, .1}, {.1, .8, .1}, {.1, .1, .8}, {.25, .75, 0}, {.75, .25, 0}, {0, .25, .75},
+                                   {0, .75, .25}, {.25, 0, .75}, {.75, 0, .25}};
+    for (size_t i = 0; i < refs.size();) {
+        size_t j = i;
+        while (j < refs.size() && refs[j].f == refs[i].f) j++;
+        const float* v = &hs.pos[9 * (size_t)refs[i].f];
+        const int npts = j - i == 1 ? 3 : (int)(sizeof(kW) / sizeof(kW[0]));
+        for (int w = 0; w < npts; w++) {
+            float x[3];
+            for (int a = 0; a < 3; a++)
+                x[a] = j - i == 1 ? v[3 * w + a] : (float)(kW[w][0] * v[a] + kW[w][1] * v[3 + a] + kW[w][2] * v[6 + a]);
+            bool in = false;
+            for (size_t r = i; r < j && !in; r++)
+                in = x[0] >= refs[r].lo[0] && x[0] <= refs[r].hi[0] && x[1] >= refs[r].lo[1] && x[1] <= refs[r].hi[1] &&
+                     x[2] >= refs[r].lo[2] && x[2] <= refs[r].hi[2];
+            if (!in) bad++;
+        }
+        i = j;
+    }
+    return bad;
+}
+// the 4-wide tree every traversal kernel reads (collapse_bvh4 of the binary tree) and its quantized form
+// (quantize_bvh4), walked on the host: every facet of the binary tree reached, each reference's triangle
+// covered by the slot boxes on its path (check_coverage), and every quantized slot box containing its fp32
+// box (the conservative rounding the persistent traversal relies on)
+int mcpt_debug_bvh4_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
+    if (!sc || !out) {
+        set_error("invalid argument");
+        return MCPT_E_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(sc->mu);
+    const Bvh& bb = light_only ? sc->lbvh : sc->bvh;
+    const std::vector<BvhNode4> b4 = collapse_bvh4(bb);
+    const std::vector<BvhNode4Q> q4 = quantize_bvh4(b4);
+    const HostScene& hs = sc->host;
+    int64_t nodes = 0, tris = 0, dup = 0, bad = 0, maxd = 0;
+    std::vector<int> seen(hs.F, 0);
+    std::vector<RefRegion> refs;
+    RefRegion cur{0, {-FLT_MAX, -FLT_MAX, -FLT_MAX}, {FLT_MAX, FLT_MAX, FLT_MAX}};
+    std::function<void(int32_t, int)> walk = [&](int32_t ni, int depth) {
+        if (ni < 0 || (size_t)ni >= b4.size()) {
+            bad++;
+            return;
+        }
+        nodes++;
+        maxd = std::max<int64_t>(maxd, depth);
+        const BvhNode4& n = b4[ni];
+        const BvhNode4Q& q = q4[ni];
+        for (int k = 0; k < 4; k++) {
+            if (n.child[k] == kBvh4Empty || (n.child[k] < 0 && n.count[k] == 0)) continue;
+            const RefRegion saved = cur;
+            for (int a = 0; a < 3; a++) {
+                cur.lo[a] = std::max(cur.lo[a], n.lo[a][k]), cur.hi[a] = std::min(cur.hi[a], n.hi[a][k]);
+                const uint32_t bits = ((q.ex >> (8 * a)) & 0xffu) << 23;
+                float sc_;
+                std::memcpy(&sc_, &bits, 4);
+                const float ql = std::fmaf((float)((q.q[2 * a] >> (8 * k)) & 0xffu), sc_, q.org[a]);
+                const float qh = std::fmaf((float)((q.q[2 * a + 1] >> (8 * k)) & 0xffu), sc_, q.org[a]);
+                if (!(ql <= n.lo[a][k] && qh >= n.hi[a][k])) bad++;
+            }
+            if (n.child[k] >= 0) {
+                walk(n.child[k], depth + 1);
+            } else {
+                const int32_t first = ~n.child[k];
+                for (int32_t j = first; j < first + n.count[k]; j++) {
+                    if (j < 0 || (size_t)j >= bb.leaf_facets.size() || bb.leaf_facets[j] < 0 || bb.leaf_facets[j] >= hs.F) {
+                        bad++;
+                        continue;
+                    }
+                    const int f = bb.leaf_facets[j];
+                    tris++;
+                    if (seen[f]++) dup++;
+                    cur.f = f;
+                    refs.push_back(cur);
+                }
+            }
+            cur = saved;
+        }
+    };
+    if (!b4.empty()) walk(0, 1);
+    bad += check_coverage(hs, refs);
+    out[0] = nodes;
+    out[1] = tris - dup;  // distinct facets reached
+    out[2] = (int64_t)bb.leaf_facets.size() - dup_refs(bb);
+    out[3] = dup;
+    out[4] = bad;
+    out[5] = maxd;
+    return MCPT_OK;
+}
+
 int mcpt_debug_bvh8_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
     if (!sc || !out) {
         set_error("invalid argument");
@@ -6281,6 +6389,7 @@ int mcpt_debug_bvh8_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
         float lo[3], hi[3];
     };
     std::vector<Box> path;
+    std::vector<RefRegion> refs;
     auto decode = [](const BvhNode8Q& n, int a, int k, bool hi) {
         const uint32_t w = hi ? n.qhi[a][k >> 2] : n.qlo[a][k >> 2];
         const uint32_t bits = ((n.ex >> (8 * a)) & 0xffu) << 23;
@@ -6314,21 +6423,20 @@ int mcpt_debug_bvh8_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
                     const int f = b.tri_facets[q];
                     tris++;
                     if (seen[f]++) dup++;
+                    RefRegion r{f, {-FLT_MAX, -FLT_MAX, -FLT_MAX}, {FLT_MAX, FLT_MAX, FLT_MAX}};
                     for (const Box& p : path)
-                        for (int v = 0; v < 3; v++)
-                            for (int a = 0; a < 3; a++) {
-                                const float x = hs.pos[9 * (size_t)f + 3 * v + a];
-                                if (!(x >= p.lo[a] && x <= p.hi[a])) bad++;
-                            }
+                        for (int a = 0; a < 3; a++) r.lo[a] = std::max(r.lo[a], p.lo[a]), r.hi[a] = std::min(r.hi[a], p.hi[a]);
+                    refs.push_back(r);
                 }
             }
             path.pop_back();
         }
     };
     if (!b.nodes.empty()) walk(0, 1);
+    bad += check_coverage(hs, refs);
     out[0] = nodes;
-    out[1] = tris;
-    out[2] = (int64_t)bb.leaf_facets.size();
+    out[1] = tris - dup;  // distinct facets reached
+    out[2] = (int64_t)bb.leaf_facets.size() - dup_refs(bb);
     out[3] = dup;
     out[4] = bad;
     out[5] = maxd;
@@ -6339,77 +6447,6 @@ int mcpt_debug_bvh8_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
 // (quantize_bvh4), walked on the host: every facet of the binary tree reached exactly once, each vertex
 // inside every ancestor slot's box, and every quantized slot box containing its fp32 box (the conservative
 // rounding the persistent traversal relies on)
-int mcpt_debug_bvh4_check(mcpt_scene* sc, int32_t light_only, int64_t* out) {
-    if (!sc || !out) {
-        set_error("invalid argument");
-        return MCPT_E_INVALID;
-    }
-    std::lock_guard<std::mutex> lk(sc->mu);
-    const Bvh& bb = light_only ? sc->lbvh : sc->bvh;
-    const std::vector<BvhNode4> b4 = collapse_bvh4(bb);
-    const std::vector<BvhNode4Q> q4 = quantize_bvh4(b4);
-    const HostScene& hs = sc->host;
-    int64_t nodes = 0, tris = 0, dup = 0, bad = 0, maxd = 0;
-    std::vector<int> seen(hs.F, 0);
-    struct Box {
-        float lo[3], hi[3];
-    };
-    std::vector<Box> path;
-    std::function<void(int32_t, int)> walk = [&](int32_t ni, int depth) {
-        if (ni < 0 || (size_t)ni >= b4.size()) {
-            bad++;
-            return;
-        }
-        nodes++;
-        maxd = std::max<int64_t>(maxd, depth);
-        const BvhNode4& n = b4[ni];
-        const BvhNode4Q& q = q4[ni];
-        for (int k = 0; k < 4; k++) {
-            if (n.child[k] == kBvh4Empty || (n.child[k] < 0 && n.count[k] == 0)) continue;
-            Box bx;
-            for (int a = 0; a < 3; a++) {
-                bx.lo[a] = n.lo[a][k], bx.hi[a] = n.hi[a][k];
-                const uint32_t bits = ((q.ex >> (8 * a)) & 0xffu) << 23;
-                float sc_;
-                std::memcpy(&sc_, &bits, 4);
-                const float ql = std::fmaf((float)((q.q[2 * a] >> (8 * k)) & 0xffu), sc_, q.org[a]);
-                const float qh = std::fmaf((float)((q.q[2 * a + 1] >> (8 * k)) & 0xffu), sc_, q.org[a]);
-                if (!(ql <= bx.lo[a] && qh >= bx.hi[a])) bad++;
-            }
-            path.push_back(bx);
-            if (n.child[k] >= 0) {
-                walk(n.child[k], depth + 1);
-            } else {
-                const int32_t first = ~n.child[k];
-                for (int32_t j = first; j < first + n.count[k]; j++) {
-                    if (j < 0 || (size_t)j >= bb.leaf_facets.size() || bb.leaf_facets[j] < 0 || bb.leaf_facets[j] >= hs.F) {
-                        bad++;
-                        continue;
-                    }
-                    const int f = bb.leaf_facets[j];
-                    tris++;
-                    if (seen[f]++) dup++;
-                    for (const Box& p : path)
-                        for (int v = 0; v < 3; v++)
-                            for (int a = 0; a < 3; a++) {
-                                const float x = hs.pos[9 * (size_t)f + 3 * v + a];
-                                if (!(x >= p.lo[a] && x <= p.hi[a])) bad++;
-                            }
-                }
-            }
-            path.pop_back();
-        }
-    };
-    if (!b4.empty()) walk(0, 1);
-    out[0] = nodes;
-    out[1] = tris;
-    out[2] = (int64_t)bb.leaf_facets.size();
-    out[3] = dup;
-    out[4] = bad;
-    out[5] = maxd;
-    return MCPT_OK;
-}
-
 int mcpt_debug_tri_filter(int32_t n, const float* tri, const double* ro, const double* rd, const float* tlim,
                           int32_t* verdict, float* tup) {
     if (n < 0 || (n > 0 && (!tri || !ro || !rd || !tlim || !verdict || !tup))) return MCPT_E_INVALID;

@@ -2,8 +2,9 @@
 (render.hip), which replaces the reference's grid DDA (Myobj.cpp:334-474 closest hit, :476-622 light-only
 hit) for scenes beyond an XCD's L2 (config C5).
 
-CPU: the tree against its binary tree (mcpt_debug_bvh8_check, host only): every facet reached once, every
-triangle inside the decoded box of every slot on its path (the conservative pruning that keeps hits exact).
+CPU: the tree against its binary tree (mcpt_debug_bvh8_check, host only): every facet reached, each reference's
+triangle covered by the decoded boxes of the slots on its path (the conservative pruning that keeps hits exact;
+a facet split spatially sits in several leaves, test_bvh4.py).
 GPU: hits bit-identical to the 4-wide traversal -- the reference's golden rays (which the 4-wide traversal
 matches, test_gpu_parity.py) and rays aimed at vertices / edges -- and renders through k_rays_cw8 equal to
 the default kernels' up to fp64 accumulation order (<= 1e-12 relative L2).
@@ -13,6 +14,12 @@ import pytest
 
 from conftest import GOLDEN, SCENE_OBJ, SCENE_XML, cornell_scene
 import monte_carlo_path_tracing_amd as mcpt
+
+def max_dup(r):
+    """repeated references a tree may hold: none, except where the builder makes spatial splits (trees of at
+    least 65 536 triangles, bvh.cpp MCPT_BVH_SPATIAL_MIN; at most 0.3 per triangle)"""
+    return 0 if r["facets"] < 65536 else 0.3 * r["facets"]
+
 import scenegen
 
 SEED = 20240430
@@ -32,7 +39,7 @@ def test_bvh8_structure_veach(scene, light_only):
     r = mcpt.debug_bvh8_check(scene, light_only)
     print("veach bvh8 (light_only=%s): %s" % (light_only, r))
     assert r["tris"] == r["facets"] == (scene.nlights if light_only else scene.nfacets)
-    assert r["duplicates"] == 0 and r["errors"] == 0 and r["nodes"] > 0
+    assert r["duplicates"] <= max_dup(r) and r["errors"] == 0 and r["nodes"] > 0
 
 
 @pytest.mark.parametrize("name", ["occluded_room", "sphere_mix", "slivers", "tiny_far", "dense_sphere", "light_panel"])
@@ -43,14 +50,14 @@ def test_bvh8_structure_generated(tmp_path, name):
     sc = mcpt.Scene.load(*gen(str(tmp_path)))
     for lo in (False, True):
         r = mcpt.debug_bvh8_check(sc, lo)
-        assert r["tris"] == r["facets"] and r["duplicates"] == 0 and r["errors"] == 0, (name, lo, r)
+        assert r["tris"] == r["facets"] and r["duplicates"] <= max_dup(r) and r["errors"] == 0, (name, lo, r)
 
 
 def test_bvh8_structure_cornell_1m():
     sc = mcpt.Scene.load(*cornell_scene(1000000))
     r = mcpt.debug_bvh8_check(sc)
     print("cornell-1M bvh8: %s" % r)
-    assert r["tris"] == r["facets"] == sc.nfacets and r["duplicates"] == 0 and r["errors"] == 0
+    assert r["tris"] == r["facets"] == sc.nfacets and r["duplicates"] <= max_dup(r) and r["errors"] == 0
     assert r["depth"] <= 12  # 8-wide: ~log8(1M) levels (the stack holds 48 groups)
 
 

@@ -37,14 +37,18 @@ static int run_library(const char* obj, const char* xml, const std::string& out_
         const std::vector<BvhNode4> b4 = collapse_bvh4(b), lb4 = collapse_bvh4(lb);
         const std::vector<BvhNode4Q> q = quantize_bvh4(b4), lq = quantize_bvh4(lb4);
         if (q.size() != b4.size() || lq.size() != lb4.size()) return 3;
-        // the 8-wide trees (leaf 8: binary leaves of up to 8 triangles, split by build_bvh8): every facet once
+        // the 8-wide trees (leaf 8: binary leaves of up to 8 triangles, split by build_bvh8): every reference of
+        // the binary tree once (a facet split spatially -- this build makes spatial splits in every tree -- has
+        // several references)
         for (const Bvh* bb : {&b, &lb}) {
             const Bvh8 b8 = build_bvh8(hs, *bb);
-            std::vector<int> seen(hs.F, 0);
+            std::vector<int> seen(hs.F, 0), want(hs.F, 0);
+            for (int32_t f : bb->leaf_facets)
+                if (f >= 0 && f < hs.F) want[f]++;
             size_t used = 0;
             for (int32_t f : b8.tri_facets)
                 if (f >= 0) {
-                    if (f >= hs.F || seen[f]++) return 6;
+                    if (f >= hs.F || ++seen[f] > want[f]) return 6;
                     used++;
                 }
             if (used != bb->leaf_facets.size() || b8.nodes.empty()) return 6;
