@@ -68,6 +68,9 @@ struct Prim {
 #ifndef MCPT_BVH_SPATIAL_MIN
 #define MCPT_BVH_SPATIAL_MIN 65536  // ... in trees of at least this many triangles (Cornell-1M +4%, Veach -7%)
 #endif
+#ifndef MCPT_BVH_SPATIAL_ALPHA
+#define MCPT_BVH_SPATIAL_ALPHA 1e-5  // overlap (of the root's area) above which spatial splits are tried
+#endif
 #ifndef MCPT_BVH_SPATIAL_BUDGET
 #define MCPT_BVH_SPATIAL_BUDGET 0.3  // at most this many duplicated references per triangle
 #endif
@@ -252,7 +255,7 @@ struct Builder {
     const HostScene* hs = nullptr;
     double root_area = 0;
     std::atomic<int64_t> spatial_budget{0};  // duplicates still allowed
-    static constexpr double kSpatialAlpha = 1e-5;
+    static constexpr double kSpatialAlpha = MCPT_BVH_SPATIAL_ALPHA;
     static constexpr int kSBins = 32;
     // the box of facet f's part inside [lo, hi] along axis, intersected with `clip` (empty if none)
     Box clip_box(int32_t f, const Box& clip, int axis, double lo, double hi) const {
