@@ -3350,44 +3350,8 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
     }
 }
 
-// workgroup-aggregated slot allocation: ring entries freed by earlier passes first, then new
-// slots from the bump counter.  Must be called by ALL threads of the workgroup.
-__device__ inline int block_alloc_slot(const Slots& T, bool want) {
-    __shared__ unsigned s_cnt[16];
-    __shared__ unsigned s_base, s_ring, s_bump;
-    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    const uint64_t m = __ballot(want);
-    if (lane == 0) s_cnt[wid] = (unsigned)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned tot = 0;
-        for (int w = 0; w < nw; w++) {
-            const unsigned c = s_cnt[w];
-            s_cnt[w] = tot;
-            tot += c;
-        }
-        unsigned base = 0, from_ring = 0, bump = 0;
-        if (tot) {
-            unsigned* c = T.ctrl + 16 * (blockIdx.x & (kSlotShards - 1));
-            base = atomicAdd(&c[1], tot);
-            const unsigned end = c[3];
-            from_ring = base >= end ? 0u : min(tot, end - base);
-            if (tot > from_ring) bump = atomicAdd(&c[0], tot - from_ring);
-        }
-        s_base = base, s_ring = from_ring, s_bump = bump;
-    }
-    __syncthreads();
-    const uint64_t below = lane == 0 ? 0ull : (m & ((~0ull) >> (64 - lane)));
-    const unsigned j = s_cnt[wid] + (unsigned)__popcll(below);
-    const int sh = blockIdx.x & (kSlotShards - 1);
-    int slot = -1;
-    if (want)
-        slot = j < s_ring ? T.ring[(size_t)sh * T.ring_cap + (s_base + j) % (unsigned)T.ring_cap]
-                          : (int)(((s_bump + (j - s_ring)) << 5) | (unsigned)sh);
-    __syncthreads();
-    return slot;
-}
-// block_alloc_slot and k_mis_combine's two child appends (light children first, then BRDF children, as two
+// workgroup-aggregated slot allocation (ring entries freed by earlier passes first, then new slots from the
+// bump counter) and k_mis_combine's two child appends (light children first, then BRDF children, as two
 // block_append calls would order them) in ONE barrier phase: the workgroup's three counts are reduced
 // together and thread 0 issues the queue atomic and the slot-ring atomics back to back, so the workgroup
 // waits for one round of device-scope atomics instead of three.  Must be called by ALL threads.
@@ -3766,9 +3730,6 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
     if (kCount && MCPT_TRACE_DIAG) wave_count2(cnt + 6, witer, cnt + 7, wleaf);
 }
 
-#ifndef MCPT_COMBINE_ONE_PHASE
-#define MCPT_COMBINE_ONE_PHASE 1  // A/B: 0 = slot allocation and the two child appends as three barrier phases
-#endif
 template <bool kStale>
 __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
@@ -3811,12 +3772,10 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         double s2 = 0;
         if (c2 && !lsh) s2 = cosb / (pdf + state_light_pdf(S, li, own)) / MCPT_P_RR;
         const bool hold = lsh || bsh;
-#if MCPT_COMBINE_ONE_PHASE
+        // the slot and both child appends in one barrier phase (round 5; three phases before: ±0, one
+        // phase kept, profiles/round5_ab_combine_phase.txt)
         int slot, qp1, qp2;
         block_alloc_slot_push2(T, hold, lsh, bsh, nxt.count, &slot, &qp1, &qp2);
-#else
-        const int slot = block_alloc_slot(T, hold);
-#endif
         const int pc = cur.par[ii];
         const bool need = pc >= 0 && (pc & 1);  // this subtree's path end is needed above
         d3 Lbr = mk3(0, 0, 0);
@@ -3841,14 +3800,9 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         const bool need_l = (c2 && li >= 0) || (need && !bsh);
         const bool need_b = need;
         const d3 z = mk3(0, 0, 0);
-#if MCPT_COMBINE_ONE_PHASE
         // the stale form never reads a node's forward throughput (w1 / w2 carry the edges), so it is not written
         queue_write(P, lsh, qp1, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt, false);
         queue_write(P, bsh, qp2, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt, false);
-#else
-        queue_push(P, lsh, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt);
-        queue_push(P, bsh, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt);
-#endif
     }
     block_count(ray_stats(P), active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, ray_stats(P) + 1,
                 (active && c2) ? 1u : 0u);
