@@ -179,7 +179,7 @@ constexpr int kRayLds = 16;  // LDS stack entries per lane of trace4_ww (16 KB p
 #define MCPT_LB_GEN 1
 #endif
 #ifndef MCPT_LB_RAYS
-#define MCPT_LB_RAYS 7
+#define MCPT_LB_RAYS 6  // 6 waves/SIMD (80 VGPRs, fewer spills) on the round-5 trees: k_mis_rays 3.54 -> 3.41 ms (was 7)
 #endif
 // 4: 128 VGPRs (141 / 140 without: the literal survival chain of state_light_pdf; 44 / 12 B of
 // scratch): k_mis_combine<true> 314 -> 308, k_mis_complete 121 -> 110 ms per profile run, MIS +0.6%
