@@ -115,12 +115,25 @@ __device__ __host__ inline double counter_u(uint64_t key, uint32_t dim) {
 // the BRDF-only kernels, where the branch cost more than it saved (C2 -1.7%; C3 +0.35%, C5 +0.5%:
 // profiles/round5_ab_phong_skip.txt)
 __device__ inline bool phong_pow_bounded(double c, double sh) { return c <= 1.000000001 && sh >= 0 && sh <= 1e6; }
-template <bool kSkip = true>
+// x^y as exp2(y log2 x) for the BRDF-only kernels (MCPT_PHONG_EXP2LOG; x > 0 or x = 0 with y > 0): relative
+// error ~ln 2 |y log2 x| 2^-53 on top of two ~1-ulp functions -- a few ulp for these arguments (Phong lobes:
+// |y log2 x| <~ 50) -- against ~220 fp64 VALU for pow's double-double logarithm
+#ifndef MCPT_PHONG_BASIS
+#define MCPT_PHONG_BASIS 1  // BRDF-only sample_phong<true>: the frame's constant cross products written out
+#endif
+#ifndef MCPT_PHONG_EXP2LOG
+#define MCPT_PHONG_EXP2LOG 1
+#endif
+template <bool kFast>
+__device__ inline double phong_pow(double x, double y) {
+    return (kFast && MCPT_PHONG_EXP2LOG) ? exp2(y * log2(x)) : pow(x, y);
+}
+template <bool kSkip = true, bool kFast = false>
 __device__ inline d3 brdf_phong(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:17-25
     d3 R = add(mul(wi, -1), mul(n, 2 * dot(wi, n)));
     d3 ans = mul(kd, 1.0 / MCPT_PI);
     double c = dot(wr, R);
-    if (c > 0 && !(kSkip && MCPT_PHONG_SKIP_ZERO && ks.x == 0 && ks.y == 0 && ks.z == 0 && phong_pow_bounded(c, sh))) ans = add(ans, mul(ks, (sh + 1) * pow(c, sh) / (2 * MCPT_PI)));
+    if (c > 0 && !(kSkip && MCPT_PHONG_SKIP_ZERO && ks.x == 0 && ks.y == 0 && ks.z == 0 && phong_pow_bounded(c, sh))) ans = add(ans, mul(ks, (sh + 1) * phong_pow<kFast>(c, sh) / (2 * MCPT_PI)));
     return ans;
 }
 __device__ inline double phong_pdf(d3 n, d3 wi, d3 wr, d3 kd, d3 ks, double sh) {  // BRDF.cpp:107-133
@@ -162,7 +175,7 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
     // theta = 0.5 acos(1 - 2 k1) or acos(k1^(1/(sh+1))); a wave with both lobes runs them once)
     double carg;
     if (ind == 0) carg = 1 - 2 * k1;
-    else carg = pow(k1, 1 / (sh + 1));
+    else carg = phong_pow<kIdent>(k1, 1 / (sh + 1));
     if (kIdent && MCPT_PHONG_SQRT) {
         // sin / cos of theta by the identities instead of acos + sincos (~180 fp64 VALU): for the cosine lobe
         // theta = acos(x) / 2 with cos = sqrt((1 + x) / 2), sin = sqrt((1 - x) / 2); for the specular lobe
@@ -187,10 +200,18 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
     }
     if (kIdent && MCPT_PHONG_SINCOSPI) sincospi(2 * k2, &sp, &cp);
     else sincos(phi, &sp, &cp);
-    d3 nx;
-    if (fabs(dot(axis, mk3(1, 0, 0)) - 1) > MCPT_EPS) nx = normalized(cross(axis, mk3(1, 0, 0)));
-    else nx = normalized(cross(axis, mk3(0, 1, 0)));
-    d3 ny = normalized(cross(axis, nx));
+    d3 nx, ny;
+    if (kIdent && MCPT_PHONG_BASIS) {
+        // the same frame with the constant cross products written out (axis x e_x = (0, a.z, -a.y), axis x e_y =
+        // (-a.z, 0, a.x)) and ny = axis x nx left unnormalised (unit up to rounding: axis and nx are orthonormal)
+        const bool ex = fabs(axis.x - 1) > MCPT_EPS;  // dot(axis, e_x) is axis.x
+        nx = normalized(ex ? mk3(0.0, axis.z, -axis.y) : mk3(-axis.z, 0.0, axis.x));
+        ny = cross(axis, nx);
+    } else {
+        if (fabs(dot(axis, mk3(1, 0, 0)) - 1) > MCPT_EPS) nx = normalized(cross(axis, mk3(1, 0, 0)));
+        else nx = normalized(cross(axis, mk3(0, 1, 0)));
+        ny = normalized(cross(axis, nx));
+    }
     *pdf_out = pdf;
     return normalized(cols_mul(nx, ny, axis, mk3(st * cp, st * sp, ct)));
 }

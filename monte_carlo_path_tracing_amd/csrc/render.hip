@@ -4023,7 +4023,7 @@ __global__ __launch_bounds__(256) void k_brdf_gen(Params P, Queue cur, int n, Au
     d3 w2 = mk3(0, 0, 0);
     if (!(dot(wi, N) < 0)) {
         flags = 2;
-        w2 = mul(hmul(tp, brdf_phong<false>(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
+        w2 = mul(hmul(tp, brdf_phong<false, true>(N, wi, wo, kd, ks, sh)), dot(wi, N) / pdf / MCPT_P_RR);
     }
     st3(A.d2, A.cap, i, wi);
     st3(A.w2, A.cap, i, w2);
@@ -4098,7 +4098,7 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
         {
             double pdf2;
             const d3 wi2 = sample_phong<true>(N, wo, kd, ks, sh, counter_u(key, 7), counter_u(key, 8), counter_u(key, 9), &pdf2);
-            const d3 b2 = brdf_phong<false>(N, wi2, wo, kd, ks, sh);
+            const d3 b2 = brdf_phong<false, true>(N, wi2, wo, kd, ks, sh);
             if (P.mode == 12345) wi = wi2, pdf = pdf2 + b2.x;
         }
 #endif
@@ -4106,7 +4106,7 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
             traced = 1;
             // the child's throughput does not depend on the hit: computed before the traversal, so
             // the shading state (N, wo, material, tp, pdf) is dead during it (fewer VGPRs)
-            const d3 b = brdf_phong<false>(N, wi, wo, kd, ks, sh);
+            const d3 b = brdf_phong<false, true>(N, wi, wo, kd, ks, sh);
             tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
             h = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
                                                       &tests, top, FLT_MAX, &witer, &wleaf);
