@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <system_error>
 #include <thread>
 
 #include "mcpt_internal.h"
@@ -76,6 +77,22 @@ struct Prim {
 #endif
 constexpr int kBins = MCPT_BVH_BINS;
 constexpr int kMaxDepth = 40;  // device traversal stack is 48 entries
+
+// runs a() on a new thread and b() on this one, or both here if no thread can be started (a library call
+// must not terminate its host process over a thread limit)
+template <class A, class B>
+void run_pair(A&& a, B&& b) {
+    std::thread t;
+    try {
+        t = std::thread(a);  // a copy: `a` stays callable if the thread cannot start
+    } catch (const std::system_error&) {
+        a();
+        b();
+        return;
+    }
+    b();
+    t.join();
+}
 
 struct Builder {
     std::vector<Prim> prims;
@@ -176,10 +193,7 @@ struct Builder {
                 }
             };
             if (n >= 8192) {  // large nodes: the three axes on three threads
-                std::thread t1(sweep_axis, 1), t2(sweep_axis, 2);
-                sweep_axis(0);
-                t1.join();
-                t2.join();
+                run_pair([&] { sweep_axis(1); }, [&] { run_pair([&] { sweep_axis(2); }, [&] { sweep_axis(0); }); });
             } else {
                 for (int c = 0; c < 3; c++) sweep_axis(c);
             }
@@ -237,9 +251,7 @@ struct Builder {
         }
         p->mid = mid;
         if (e - b > kParallelPrims) {
-            std::thread t([&] { p->l = plan(b, mid, depth + 1); });
-            p->r = plan(mid, e, depth + 1);
-            t.join();
+            run_pair([&] { p->l = plan(b, mid, depth + 1); }, [&] { p->r = plan(mid, e, depth + 1); });
         } else {
             p->l = plan(b, mid, depth + 1);
             p->r = plan(mid, e, depth + 1);
@@ -386,9 +398,7 @@ struct Builder {
         }
         std::vector<Prim>().swap(refs);
         if (n > kParallelPrims) {
-            std::thread t([&] { p->l = splan(std::move(L), depth + 1); });
-            p->r = splan(std::move(R), depth + 1);
-            t.join();
+            run_pair([&] { p->l = splan(std::move(L), depth + 1); }, [&] { p->r = splan(std::move(R), depth + 1); });
         } else {
             p->l = splan(std::move(L), depth + 1);
             p->r = splan(std::move(R), depth + 1);
@@ -488,9 +498,7 @@ Bvh build_bvh(const HostScene& s, const std::vector<int32_t>& facets, int max_le
         bvh.nodes[0].count[0] = cnt;
     } else {
         std::unique_ptr<Builder::Plan> pl, pr;
-        std::thread t([&] { pl = B.plan(0, mid, 1); });
-        pr = B.plan(mid, n, 1);
-        t.join();
+        run_pair([&] { pl = B.plan(0, mid, 1); }, [&] { pr = B.plan(mid, n, 1); });
         B.emit(0, mid, 0, 0, *pl);
         B.emit(mid, n, 0, 1, *pr);
     }
