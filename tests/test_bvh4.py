@@ -48,3 +48,15 @@ def test_bvh4_structure_cornell_1m():
     print("cornell-1M bvh4: %s" % r)
     assert ok(r, sc.nfacets), r
     assert r["depth"] <= 40  # the traversal stacks hold 48 entries
+
+
+def test_builder_is_deterministic():
+    """the parallel plan phase (split searches of disjoint ranges on their own threads) and the spatial splits
+    of a >= 65 536-triangle tree give the same tree on every load"""
+    paths = cornell_scene(200000)
+    a, b = mcpt.Scene.load(*paths), mcpt.Scene.load(*paths)
+    assert a.accel_bytes() == b.accel_bytes()
+    for lo in (False, True):
+        assert mcpt.debug_bvh4_check(a, lo) == mcpt.debug_bvh4_check(b, lo)
+        assert mcpt.debug_bvh8_check(a, lo) == mcpt.debug_bvh8_check(b, lo)
+    assert mcpt.debug_bvh4_check(a)["duplicates"] > 0  # spatial splits did happen
