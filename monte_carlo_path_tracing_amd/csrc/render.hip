@@ -4057,12 +4057,19 @@ constexpr int kBrdfLds = kBrdfTop > 0 ? 8 : kRayLds;
 #ifndef MCPT_BRDF_TIMING
 #define MCPT_BRDF_TIMING 0  // A/B only: 1 = sampling twice, 2 = traversal twice (cost shares, timing builds)
 #endif
+#ifndef MCPT_BRDF_PARK
+#define MCPT_BRDF_PARK 1  // the child throughput in LDS during the traversal: 14 spilled VGPRs -> 0, C2 +6% (profiles/round5_ab_brdf_park.txt)
+#endif
 #ifndef MCPT_BRDF_WAVES
 #define MCPT_BRDF_WAVES 5  // 96 VGPRs (10 spilled): 4 -> 5 waves/SIMD, +5% BRDF-only (profiles/round2b_ab_brdf.txt)
 #endif
 template <bool kCount = false>
 __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Params P, Queue cur, int n, Queue nxt) {
     __shared__ int stack[kBrdfLds * kBrdfBlock];
+#if MCPT_BRDF_PARK
+    // the child's throughput waits out the traversal in LDS, not in VGPRs (MCPT_BRDF_PARK)
+    __shared__ double park[3 * kBrdfBlock];
+#endif
     __shared__ BvhNode4 top[kBrdfTop > 0 ? kBrdfTop : 1];
     const DScene& S = P.S;
     if (kBrdfTop > 0) {  // the tree's top levels into LDS (as k_mis_rays)
@@ -4108,6 +4115,9 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
             // the shading state (N, wo, material, tp, pdf) is dead during it (fewer VGPRs)
             const d3 b = brdf_phong<false, true>(N, wi, wo, kd, ks, sh);
             tpc = mul(hmul(tp, b), dot(wi, N) / pdf / MCPT_P_RR);
+#if MCPT_BRDF_PARK
+            park[threadIdx.x] = tpc.x, park[kBrdfBlock + threadIdx.x] = tpc.y, park[2 * kBrdfBlock + threadIdx.x] = tpc.z;
+#endif
             h = trace4_ww<kBrdfLds, kCount, kBrdfTop, MCPT_FILTER_BRDF>(S.bvh4, S.leaf_v, p, wi, f, stack + threadIdx.x, kBrdfBlock, &visits,
                                                       &tests, top, FLT_MAX, &witer, &wleaf);
 #if MCPT_BRDF_TIMING == 2  // timing-only build: the traversal runs twice
@@ -4120,6 +4130,9 @@ __global__ __launch_bounds__(kBrdfBlock, MCPT_BRDF_WAVES) void k_extend_brdf(Par
             c = h.f >= 0;
         }
     }
+#if MCPT_BRDF_PARK
+    if (traced) tpc = mk3(park[threadIdx.x], park[kBrdfBlock + threadIdx.x], park[2 * kBrdfBlock + threadIdx.x]);
+#endif
     node_entry(P, c, h.f, h.beta, h.gamma, mul(wi, -1), tpc, pixel, sample, node + 1, nxt);
     block_count(ray_stats(P), traced);
     if (kCount) wave_count2(P.stats + 8, visits, P.stats + 9, tests);
