@@ -3730,9 +3730,6 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
     if (kCount && MCPT_TRACE_DIAG) wave_count2(cnt + 6, witer, cnt + 7, wleaf);
 }
 
-#ifndef MCPT_COMBINE_PARK
-#define MCPT_COMBINE_PARK 0
-#endif
 template <bool kStale>
 __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
@@ -3778,66 +3775,23 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         // the slot and both child appends in one barrier phase (round 5; three phases before: ±0, one
         // phase kept, profiles/round5_ab_combine_phase.txt)
         int slot, qp1, qp2;
-#if MCPT_COMBINE_PARK
-        // the children's points and normals wait out the barrier phase in LDS, and the node's own inputs are
-        // re-read after it, instead of ~50 VGPRs held across it (MCPT_COMBINE_PARK)
-        __shared__ double pk[12][256];
-        pk[0][threadIdx.x] = e1.p.x, pk[1][threadIdx.x] = e1.p.y, pk[2][threadIdx.x] = e1.p.z;
-        pk[3][threadIdx.x] = e1.N.x, pk[4][threadIdx.x] = e1.N.y, pk[5][threadIdx.x] = e1.N.z;
-        pk[6][threadIdx.x] = e2.p.x, pk[7][threadIdx.x] = e2.p.y, pk[8][threadIdx.x] = e2.p.z;
-        pk[9][threadIdx.x] = e2.N.x, pk[10][threadIdx.x] = e2.N.y, pk[11][threadIdx.x] = e2.N.z;
-#endif
         block_alloc_slot_push2(T, hold, lsh, bsh, nxt.count, &slot, &qp1, &qp2);
-#if MCPT_COMBINE_PARK
-        asm volatile("" ::: "memory");
-        Entry e1p = e1, e2p = e2;
-        e1p.p = mk3(pk[0][threadIdx.x], pk[1][threadIdx.x], pk[2][threadIdx.x]);
-        e1p.N = mk3(pk[3][threadIdx.x], pk[4][threadIdx.x], pk[5][threadIdx.x]);
-        e2p.p = mk3(pk[6][threadIdx.x], pk[7][threadIdx.x], pk[8][threadIdx.x]);
-        e2p.N = mk3(pk[9][threadIdx.x], pk[10][threadIdx.x], pk[11][threadIdx.x]);
-        const double ownp[7] = {cur.p[ii], cur.p[cur.cap + ii], cur.p[2 * (size_t)cur.cap + ii], cur.n[ii],
-                                cur.n[cur.cap + ii], cur.n[2 * (size_t)cur.cap + ii], cur.wsum[ii]};
-        const d3 w1p = ld3(A.w1, A.cap, ii), w2p = ld3(A.w2, A.cap, ii), d1p = ld3(A.d1, A.cap, ii), d2p = ld3(A.d2, A.cap, ii);
-        const int pixelp = cur.pixel[ii], samplep = cur.sample[ii];
-        const uint64_t nodep = cur.node[ii];
-#define K_E1 e1p
-#define K_E2 e2p
-#define K_OWN ownp
-#define K_W1 w1p
-#define K_W2 w2p
-#define K_D1 d1p
-#define K_D2 d2p
-#define K_PIXEL pixelp
-#define K_SAMPLE samplep
-#define K_NODE nodep
-#else
-#define K_E1 e1
-#define K_E2 e2
-#define K_OWN own
-#define K_W1 w1
-#define K_W2 w2
-#define K_D1 d1
-#define K_D2 d2
-#define K_PIXEL pixel
-#define K_SAMPLE sample
-#define K_NODE node
-#endif
         const int pc = cur.par[ii];
         const bool need = pc >= 0 && (pc & 1);  // this subtree's path end is needed above
         d3 Lbr = mk3(0, 0, 0);
-        if (e2.kind == 1) Lbr = mul(hmul(mk3(S.light_rad[3 * e2.li], S.light_rad[3 * e2.li + 1], S.light_rad[3 * e2.li + 2]), K_W2), s2);
+        if (e2.kind == 1) Lbr = mul(hmul(mk3(S.light_rad[3 * e2.li], S.light_rad[3 * e2.li + 1], S.light_rad[3 * e2.li + 2]), w2), s2);
         // finished now (no shading child): L = L_light + L_brdf (main.cpp:493); its path end is itself
-        mis_report(P, T, active && !hold, pc, K_PIXEL, add(Llight, Lbr), K_OWN, rp);
+        mis_report(P, T, active && !hold, pc, pixel, add(Llight, Lbr), own, rp);
         if (active && hold) {
             const size_t q = (size_t)slot;
             T.pend[q] = (int)lsh + (int)bsh;
             double* r = T.rec + kSlotRec * q;
-            *reinterpret_cast<int4*>(r) = make_int4(pc, K_PIXEL,
+            *reinterpret_cast<int4*>(r) = make_int4(pc, pixel,
                                                     (int)lsh | ((int)bsh << 1) | ((e2.kind == 1) << 2) | ((int)c2 << 3) | ((int)need << 4),
                                                     li);
             double* w = r + 2;
-            w[0] = K_W1.x, w[1] = K_W1.y, w[2] = K_W1.z, w[3] = A.s1[ii];
-            w[4] = K_W2.x, w[5] = K_W2.y, w[6] = K_W2.z, w[7] = pdf, w[8] = cosb, w[9] = s2;
+            w[0] = w1.x, w[1] = w1.y, w[2] = w1.z, w[3] = A.s1[ii];
+            w[4] = w2.x, w[5] = w2.y, w[6] = w2.z, w[7] = pdf, w[8] = cosb, w[9] = s2;
             if (!lsh) T.Ll[3 * q] = Llight.x, T.Ll[3 * q + 1] = Llight.y, T.Ll[3 * q + 2] = Llight.z;
             if (e2.kind == 1) r[12] = S.light_rad[3 * e2.li], r[13] = S.light_rad[3 * e2.li + 1], r[14] = S.light_rad[3 * e2.li + 2];
         }
@@ -3847,19 +3801,8 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
         const bool need_b = need;
         const d3 z = mk3(0, 0, 0);
         // the stale form never reads a node's forward throughput (w1 / w2 carry the edges), so it is not written
-        queue_write(P, lsh, qp1, K_E1, f1, mul(K_D1, -1), z, K_PIXEL, K_SAMPLE, 2 * K_NODE, 4 * slot + (int)need_l, nxt, false);
-        queue_write(P, bsh, qp2, K_E2, f2, mul(K_D2, -1), z, K_PIXEL, K_SAMPLE, 2 * K_NODE + 1, 4 * slot + 2 + (int)need_b, nxt,
-                    false);
-#undef K_E1
-#undef K_E2
-#undef K_OWN
-#undef K_W1
-#undef K_W2
-#undef K_D1
-#undef K_D2
-#undef K_PIXEL
-#undef K_SAMPLE
-#undef K_NODE
+        queue_write(P, lsh, qp1, e1, f1, mul(d1, -1), z, pixel, sample, 2 * node, 4 * slot + (int)need_l, nxt, false);
+        queue_write(P, bsh, qp2, e2, f2, mul(d2, -1), z, pixel, sample, 2 * node + 1, 4 * slot + 2 + (int)need_b, nxt, false);
     }
     block_count(ray_stats(P), active ? (unsigned)((fl & 1) + ((fl >> 1) & 1)) : 0u, ray_stats(P) + 1,
                 (active && c2) ? 1u : 0u);

@@ -17,8 +17,4 @@ tools/gpu_steps.sh \
 rc=$?
 case $rc in 124|134|137|139) exit $rc ;; esac
 [ $rc -gt 128 ] && exit $rc
-TAG=round5j PART=2 tools/profile_steps.sh
-rc=$?
-case $rc in 124|134|137|139) exit $rc ;; esac
-[ $rc -gt 128 ] && exit $rc
-exec tools/round5_part20.sh
+TAG=round5j PART=2 exec tools/profile_steps.sh
