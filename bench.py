@@ -288,12 +288,15 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     comm = None
+    comm_init_s = 0.0  # communicator creation: mcpt_comm_init_rank here, ncclCommInitAll in the first device-list call
     if devices is None:
         # the library's RCCL communicator (one rank per process); a 1-rank communicator at N=1
         uid = [mcpt.Comm.unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
+        tc = time.perf_counter()
         comm = mcpt.Comm(world, rank, uid[0], device=local)
+        comm_init_s = time.perf_counter() - tc
     multi = dict(comm=comm) if devices is None else dict(devices=devices)
     list_flags = mcpt.DEBUG_SHARD_RANKS if devices is not None and rehearsal else 0
 
@@ -325,10 +328,15 @@ def main():
         mcpt.RENDER_PRECISION_FP32 if args.precision == "fp32" else 0) | (
         mcpt.DEBUG_NO_ROOT_CACHE if args.no_root_cache else 0) | args.debug_flags | list_flags
     flags = mcpt.RENDER_NO_BACKFACE_STATS | mode_flags
+    setup_s = None  # the first call's device setup (scene upload, BVH, buffers): outside the timed region
     for k in range(args.warmup):  # warmup renders (same kernels and flags as the timed steps) go to scratch
-        mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
-                           sample_range=(0, world * S), flags=flags, **multi)
+        wst = mcpt.render_device(scene, cam, world * S, scratch.data_ptr(), mode=args.mode, seed=args.seed + 1,
+                                 sample_range=(0, world * S), flags=flags, **multi)
+        comm_init_s += wst.comm_init_seconds
+        if setup_s is None:
+            setup_s = wst.device_setup_seconds
     totals = {}
+    per_dev = None  # per rank: sum over the timed steps of its shard wall time (mcpt_stats.device_seconds)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -338,6 +346,9 @@ def main():
                                 sample_range=(k * world * S, (k + 1) * world * S), flags=flags, **multi)
         for key, v in st.as_dict().items():
             totals[key] = totals.get(key, 0) + v
+        pd = st.per_device_seconds()
+        per_dev = pd if per_dev is None else [a + b for a, b in zip(per_dev, pd)]
+        comm_init_s += st.comm_init_seconds  # 0 unless the timed steps created a communicator (they must not)
         # device time of the step: a device list runs its distinct devices concurrently, so its wall time on
         # each of them (the shards' kernel times are summed in the other fields)
         totals["device_seconds"] = totals.get("device_seconds", 0.0) + st.seconds * max(st.devices_used, 1)
@@ -351,6 +362,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # one process per GPU: every rank's shard time and communicator creation, gathered to all
+        g = [None] * world
+        dist.all_gather_object(g, (per_dev[0] if per_dev else 0.0, comm_init_s))
+        per_dev = [x[0] for x in g]
+        comm_init_s = max(x[1] for x in g)
     samples = float(W * H) * frame_spp
     value = samples / elapsed / 1e6
     # Untimed statistics replay: the same steps (same seed and sample ranges, so the same nodes and
@@ -524,6 +540,14 @@ def main():
         "l2_vs_cpu_max_pixel": l2max,
         "device_seconds": round(totals.get("seconds", 0.0), 4),
         "samples": samples,
+        # where a multi-GPU step's time went (mcpt_stats ABI 2.2): each rank's shard wall time summed over the
+        # timed steps (setup and reduce excluded; max/min = load imbalance), the reduces' time, and -- outside the
+        # timed region -- the communicator's creation and the first call's device setup
+        "per_device_seconds": [round(v, 4) for v in (per_dev or [])],
+        "device_imbalance": round(max(per_dev) / max(min(per_dev), 1e-12), 4) if per_dev else None,
+        "reduce_seconds": round(totals.get("reduce_seconds", 0.0), 4),
+        "comm_init_seconds": round(comm_init_s, 4),
+        "device_setup_seconds": round(setup_s, 4) if setup_s is not None else None,
     }
     print(json.dumps(line), flush=True)
     if comm is not None:

@@ -23,7 +23,10 @@
 extern "C" {
 #endif
 
-#define MCPT_VERSION 20100 /* 2.1.0: mcpt_stats gains prep_exact_nodes, cache_build_seconds and prep_band_nodes
+#define MCPT_VERSION 20200 /* 2.2.0: mcpt_stats gains comm_init_seconds, device_setup_seconds and
+                               * device_seconds[MCPT_STATS_MAX_DEVICES] (appended): where a multi-device call's
+                               * time went;
+                               * 2.1.0: mcpt_stats gains prep_exact_nodes, cache_build_seconds and prep_band_nodes
                                * (appended);
                                * 2.0.0: mcpt_render_opts carries struct_size (checked first), a device list
                                * and a multi-process communicator; debug entry points moved to mcpt_debug.h */
@@ -160,6 +163,7 @@ enum { MCPT_RENDER_PRECISION_FP32 = 4 };
  * mode = MCPT_MODE_MIS */
 void mcpt_render_opts_init(mcpt_render_opts* opts);
 
+#define MCPT_STATS_MAX_DEVICES 16
 typedef struct {
     double seconds;         /* device time of the render (HIP events) */
     uint64_t camera_samples;
@@ -193,9 +197,20 @@ typedef struct {
     double cache_build_seconds; /* device time building the per-pixel root-point cache (in prep_seconds) */
     uint64_t prep_band_nodes;   /* light preps whose slack the whole-table band bound could not clear and
                                  * that took the per-chunk band test (prep_exact_nodes of them failed it) */
+    /* ABI 2.2: where a multi-device / multi-rank call's time went */
+    double comm_init_seconds;    /* device list: wall time of ncclCommInitAll in THIS call (first call over a
+                                  * device set; 0 when the cached communicator is reused).  Created on the
+                                  * calling thread before any device work starts.  0 for single-device and
+                                  * mcpt_comm calls (mcpt_comm_init_rank is the caller's) */
+    double device_setup_seconds; /* device list: max over devices of the worker's setup wall time (device state:
+                                  * scene upload + BVH on first use; framebuffer) */
+    double device_seconds[MCPT_STATS_MAX_DEVICES]; /* per rank of the call's communicator (distinct devices
+                                  * in order of first appearance; entries beyond 16 not recorded): wall time of
+                                  * its shards, setup and reduce excluded -- max/min is the load imbalance.
+                                  * Single device / mcpt_comm rank: [0] = this call's render time */
 } mcpt_stats;
-/* With several devices, `seconds` is the wall time of the whole call (shards + reduce), counts are
- * summed over devices and prep_seconds is summed device time. */
+/* With several devices, `seconds` is the wall time of the whole call (setup + shards + reduce; comm init
+ * excluded), counts are summed over devices and prep_seconds is summed device time. */
 
 int mcpt_version(void);
 const char* mcpt_last_error(void);

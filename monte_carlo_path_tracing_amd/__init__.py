@@ -26,8 +26,9 @@ MODES = {"mis": MODE_MIS, "brdf": MODE_BRDF, "shade": MODE_SHADE, "shade_area": 
 ACCEL_BVH, ACCEL_GRID = 0, 1  # mcpt_render_opts.accel: BVH, or the reference's uniform grid (Myobj.cpp:78-162)
 HIT_LIGHT_ONLY, HIT_GRID = 1, 2  # mcpt_closest_hit flags
 DEFAULT_SEED = 20240430
-MCPT_VERSION = 20100  # include/mcpt.h MCPT_VERSION this mirror is written against
+MCPT_VERSION = 20200  # include/mcpt.h MCPT_VERSION this mirror is written against
 COMM_ID_BYTES = 128  # MCPT_COMM_ID_BYTES
+STATS_MAX_DEVICES = 16  # MCPT_STATS_MAX_DEVICES
 
 
 class MCPTError(RuntimeError):
@@ -82,10 +83,16 @@ class Stats(C.Structure):
                 ("spilled_nodes", C.c_uint64), ("reduce_seconds", C.c_double), ("devices_used", C.c_int32),
                 ("trace_seconds", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("prep_exact_nodes", C.c_uint64), ("cache_build_seconds", C.c_double),
-                ("prep_band_nodes", C.c_uint64)]
+                ("prep_band_nodes", C.c_uint64), ("comm_init_seconds", C.c_double),
+                ("device_setup_seconds", C.c_double), ("device_seconds", C.c_double * STATS_MAX_DEVICES)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        """scalar fields (summable); device_seconds is in per_device_seconds()"""
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "device_seconds"}
+
+    def per_device_seconds(self):
+        """device_seconds[:devices_used]: each rank's shard wall time (setup and reduce excluded)"""
+        return [float(v) for v in self.device_seconds[:max(1, min(self.devices_used, STATS_MAX_DEVICES))]]
 
 
 _lib = None

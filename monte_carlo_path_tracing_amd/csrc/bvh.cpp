@@ -266,7 +266,7 @@ struct Builder {
     // traversal's closest-hit rule (t, then the lower facet id) makes a repeated test a no-op.
     const HostScene* hs = nullptr;
     double root_area = 0;
-    std::atomic<int64_t> spatial_budget{0};  // duplicates still allowed
+    int64_t spatial_budget = 0;  // duplicates allowed over the whole tree (MCPT_BVH_SPATIAL_BUDGET per facet)
     static constexpr double kSpatialAlpha = MCPT_BVH_SPATIAL_ALPHA;
     static constexpr int kSBins = 32;
     // the box of facet f's part inside [lo, hi] along axis, intersected with `clip` (empty if none)
@@ -351,7 +351,11 @@ struct Builder {
         for (int i = b; i < e; i++) r.grow(v[i].box);
         return r;
     }
-    std::unique_ptr<SPlan> splan(std::vector<Prim> refs, int depth) {
+    // budget: the duplicates this subtree may still create.  It is passed down by value -- what a node does not
+    // spend is shared between its children in proportion to their references -- so the tree depends only on the
+    // scene, never on which builder thread got to a shared counter first, and the whole tree never exceeds the
+    // budget it started with (a split that would is taken as the object split instead)
+    std::unique_ptr<SPlan> splan(std::vector<Prim> refs, int depth, int64_t budget) {
         auto p = std::make_unique<SPlan>();
         const int n = static_cast<int>(refs.size());
         p->box = vbounds(refs, 0, n);
@@ -368,7 +372,8 @@ struct Builder {
         const bool overlap = ov.lo[0] <= ov.hi[0] && ov.lo[1] <= ov.hi[1] && ov.lo[2] <= ov.hi[2];
         double scost = 0, plane = 0;
         int sax = 0;
-        if (depth < kMaxDepth && overlap && ov.area() > kSpatialAlpha * root_area && spatial_budget.load() > 0 &&
+        int64_t dup = 0;
+        if (depth < kMaxDepth && overlap && ov.area() > kSpatialAlpha * root_area && budget > 0 &&
             spatial_split(refs, p->box, &scost, &sax, &plane) && scost < bl.area() * mid + br.area() * (n - mid)) {
             for (const Prim& q : refs) {
                 if (q.box.hi[sax] <= plane) {
@@ -385,23 +390,29 @@ struct Builder {
                     if (ha) L.push_back(a);
                     if (hb) R.push_back(b);
                     if (!ha && !hb) L.push_back(q);  // (clipping lost it to rounding: keep it whole)
-                    if (ha && hb) spatial_budget.fetch_sub(1);
+                    if (ha && hb) dup++;
                 }
             }
-            if (L.empty() || R.empty() || static_cast<int>(L.size()) >= n || static_cast<int>(R.size()) >= n) {
-                L.assign(refs.begin(), refs.begin() + mid);  // no progress: the object split after all
+            if (L.empty() || R.empty() || static_cast<int>(L.size()) >= n || static_cast<int>(R.size()) >= n ||
+                dup > budget) {
+                L.assign(refs.begin(), refs.begin() + mid);  // no progress, or over budget: the object split after all
                 R.assign(refs.begin() + mid, refs.end());
+                dup = 0;
             }
         } else {
             L.assign(refs.begin(), refs.begin() + mid);
             R.assign(refs.begin() + mid, refs.end());
         }
         std::vector<Prim>().swap(refs);
+        const int64_t left = budget - dup;
+        const int64_t bl_share = static_cast<int64_t>(static_cast<double>(left) * L.size() / (L.size() + R.size()));
+        const int64_t br_share = left - bl_share;
         if (n > kParallelPrims) {
-            run_pair([&] { p->l = splan(std::move(L), depth + 1); }, [&] { p->r = splan(std::move(R), depth + 1); });
+            run_pair([&] { p->l = splan(std::move(L), depth + 1, bl_share); },
+                     [&] { p->r = splan(std::move(R), depth + 1, br_share); });
         } else {
-            p->l = splan(std::move(L), depth + 1);
-            p->r = splan(std::move(R), depth + 1);
+            p->l = splan(std::move(L), depth + 1, bl_share);
+            p->r = splan(std::move(R), depth + 1, br_share);
         }
         return p;
     }
@@ -478,7 +489,7 @@ Bvh build_bvh(const HostScene& s, const std::vector<int32_t>& facets, int max_le
         B.hs = &s;
         B.root_area = all.area();
         B.spatial_budget = static_cast<int64_t>(MCPT_BVH_SPATIAL_BUDGET * n);
-        std::unique_ptr<Builder::SPlan> root_plan = B.splan(std::move(B.prims), 0);
+        std::unique_ptr<Builder::SPlan> root_plan = B.splan(std::move(B.prims), 0, B.spatial_budget);
         if (!root_plan->l) {  // one leaf: the root's slot 0 (slot 1 stays empty)
             B.to_float_box(root_plan->box, bvh.nodes[0].lo[0], bvh.nodes[0].hi[0]);
             bvh.nodes[0].child[0] = ~0;
@@ -695,7 +706,8 @@ struct Bvh8Builder {
     static double area(const BN& x) { return box_area(x.lo, x.hi); }
 
     // fills node `self` from the children of binary node `root` (collapsed up to eight)
-    void node(int32_t root, int32_t self) {
+    void node(int32_t root, int32_t self, int depth = 1) {
+        out.depth = std::max(out.depth, depth);
         std::vector<int32_t> cand;
         for (int32_t c : {bn[root].l, bn[root].r})
             if (c >= 0) cand.push_back(c);
@@ -816,7 +828,7 @@ struct Bvh8Builder {
         o.base_tri = base_tri;
         o.tvalid = tvalid;
         out.nodes[self] = o;
-        for (auto& t : todo) node(t.first, t.second);
+        for (auto& t : todo) node(t.first, t.second, depth + 1);
     }
 };
 }  // namespace

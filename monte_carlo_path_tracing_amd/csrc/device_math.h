@@ -194,8 +194,10 @@ __device__ inline d3 sample_phong(d3 n, d3 wr, d3 kd, d3 ks, double sh, double u
     } else {
         // k1^(sh/(sh+1)) = k1 / k1^(1/(sh+1)) = k1 / carg: one fp64 pow (~220 VALU) instead of two, equal up to
         // ~2 ulp (BRDF.cpp:97 evaluates the pow; pow(0, y > 0) = 0).  C2 +0.9%, C3 +0.2% same-box
-        // (profiles/round5_ab_pow_margin.txt)
-        pdf *= (sh + 1) / (2 * MCPT_PI) * (carg > 0 ? k1 / carg : 0.0);
+        // (profiles/round5_ab_pow_margin.txt).  Every kernel uses it (kIdent or not); the identity holds only
+        // for sh > 0 with carg > 0, so anything else -- sh <= 0 (pow(0, 0) = 1; sh in (-1, 0) where carg can
+        // underflow while k1 > 0) or k1 = 0 -- takes the reference's pow itself
+        pdf *= (sh + 1) / (2 * MCPT_PI) * (sh > 0 && carg > 0 ? k1 / carg : pow(k1, sh / (sh + 1)));
         axis = normalized(add(mul(wr, -1), mul(n, 2 * dot(wr, n))));
     }
     if (kIdent && MCPT_PHONG_SINCOSPI) sincospi(2 * k2, &sp, &cp);

@@ -168,6 +168,12 @@ int main(int argc, char** argv) {
                 mode == MCPT_MODE_MIS ? "MIS" : mode == MCPT_MODE_BRDF ? "BRDF" : mode == MCPT_MODE_SHADE ? "shade" : "shade-area",
                 sec, st.seconds,
                 st.camera_samples / st.seconds * 1e-6, st.devices_used);
+    if (st.devices_used > 1) {  // where a multi-device call's time went
+        std::printf("  comm init %.3f s, device setup %.3f s (max), reduce %.4f s; per device:", st.comm_init_seconds,
+                    st.device_setup_seconds, st.reduce_seconds);
+        for (int u = 0; u < st.devices_used && u < MCPT_STATS_MAX_DEVICES; u++) std::printf(" %.3f", st.device_seconds[u]);
+        std::printf(" s\n");
+    }
     std::vector<uint8_t> rgb8(hdr.size());
     mcpt_tone_map(hdr.data(), W, H, 380.0, 0.25, rgb8.data());  // main.cpp:583
     if (mcpt_write_bmp(out.c_str(), rgb8.data(), W, H) != MCPT_OK) {

@@ -107,6 +107,7 @@ static_assert(sizeof(BvhNode8Q) == 128, "BvhNode8Q must be 128 B");
 struct Bvh8 {
     std::vector<BvhNode8Q> nodes;      // node 0 = root
     std::vector<int32_t> tri_facets;   // facet of each triangle slot (-1: unused)
+    int depth = 0;                     // levels of nodes (the 8-wide traversal stack holds at most one entry per level)
 };
 // the 8-wide tree of a binary BVH built by build_bvh over the same facets (boxes conservative: every decoded
 // child box contains the fp32 box the binary tree holds for it, or its triangles' for a split leaf)

@@ -4259,10 +4259,33 @@ template <class T>
 int upload(DeviceState& D, const std::vector<T>& v, const T** out) {
     void* p = nullptr;
     HIP_OK(hipMalloc(&p, std::max<size_t>(v.size() * sizeof(T), 64)));
+    D.allocs.push_back(p);  // owned by D from here on, even if the copy fails
     if (!v.empty()) HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    D.allocs.push_back(p);
     *out = static_cast<const T*>(p);
     return MCPT_OK;
+}
+
+// the deepest the traversal stacks (trace4_ww, k_rays_persistent) can get on a 4-wide tree: at each node a
+// lane pushes every hit child but the nearest, which it follows, so the stack never holds more than the sum
+// over a root-to-node path of (children - 1).  A tree that could overflow the kStack entries is refused at
+// device setup (a dropped push would lose a subtree, and with it possibly the closest hit), so no traversal
+// ever drops one: the builder's depth cap keeps real scenes far below (Veach 8 levels, Cornell-1M 12: at
+// most 33 entries)
+int bvh4_stack_need(const std::vector<BvhNode4>& t) {
+    if (t.empty()) return 0;
+    int need = 0;
+    std::vector<std::pair<int, int>> st{{0, 0}};  // (node, entries its ancestors may have pushed)
+    while (!st.empty()) {
+        const auto [v, above] = st.back();
+        st.pop_back();
+        int used = 0;
+        for (int k = 0; k < 4; k++) used += t[v].child[k] != kBvh4Empty;
+        const int here = above + std::max(used - 1, 0);
+        need = std::max(need, here);
+        for (int k = 0; k < 4; k++)
+            if (t[v].child[k] >= 0 && t[v].child[k] != kBvh4Empty) st.push_back({t[v].child[k], here});
+    }
+    return need;
 }
 
 // renumbers a 4-wide BVH breadth-first (root 0, then each level in order), so the first nodes are
@@ -4509,6 +4532,14 @@ int get_device_state(mcpt_scene* sc, int device, DeviceState** out) {
     if ((rc = upload(*D, lf, &d.lt_f))) return rc;
     if ((rc = upload(*D, leaf_vertices(s, sc->bvh), &d.leaf_v))) return rc;
     std::vector<BvhNode4> b4 = bfs_order(collapse_bvh4(sc->bvh)), lb4 = bfs_order(collapse_bvh4(sc->lbvh));
+    for (const auto* t : {&b4, &lb4}) {
+        const int need = bvh4_stack_need(*t);
+        if (need > kStack) {
+            set_error("the scene's %sBVH needs %d traversal stack entries, more than the %d the kernels hold "
+                      "(degenerate geometry: too many coincident triangles)", t == &lb4 ? "light-only " : "", need, kStack);
+            return MCPT_E_SCENE;
+        }
+    }
     if ((rc = pack_leaf_codes(b4)) || (rc = pack_leaf_codes(lb4))) return rc;
     d.nbvh4 = (int)b4.size();
     d.nlbvh4 = (int)lb4.size();
@@ -4813,15 +4844,25 @@ void ensure_bvh8_host(mcpt_scene* sc) {
 }
 int ensure_bvh8(mcpt_scene* sc, DeviceState* D) {
     ensure_bvh8_host(sc);
-    if (D->d.bvh8 || D->bvh8_tried) return MCPT_OK;
-    D->bvh8_tried = true;
+    if (D->bvh8_tried) return MCPT_OK;
     DScene& d = D->d;
     const HostScene& s = sc->host;
     int rc;
     HIP_OK(hipSetDevice(D->device));
+    // a failed upload (e.g. out of memory) leaves no half-uploaded tree behind and is retried by the next call,
+    // so its error is reported each time instead of a later "no 8-wide tree"; only success marks the device tried
+    // (a tree too large for the 24-bit stack base then stays null by design)
+    struct Undo {
+        DScene& d;
+        bool armed = true;
+        ~Undo() {
+            if (armed) d.bvh8 = d.lbvh8 = nullptr, d.tri8_v = d.ltri8_v = nullptr;
+        }
+    } undo{d};
     for (int t = 0; t < 2; t++) {
         const Bvh8& b8 = t == 0 ? sc->bvh8 : sc->lbvh8;
-        if (b8.nodes.empty() || b8.nodes.size() >= (1u << 24)) continue;
+        // trace_cw8 / k_rays_cw8 push at most one node group per level: a tree deeper than kStack could drop one
+        if (b8.nodes.empty() || b8.nodes.size() >= (1u << 24) || b8.depth > kStack) continue;
         std::vector<float4> tv8(3 * std::max<size_t>(b8.tri_facets.size(), 1), make_float4(0.f, 0.f, 0.f, 0.f));
         for (size_t q = 0; q < b8.tri_facets.size(); q++) {
             const int f = b8.tri_facets[q];
@@ -4835,6 +4876,8 @@ int ensure_bvh8(mcpt_scene* sc, DeviceState* D) {
         if ((rc = upload(*D, b8.nodes, t == 0 ? &d.bvh8 : &d.lbvh8))) return rc;
         if ((rc = upload(*D, tv8, t == 0 ? &d.tri8_v : &d.ltri8_v))) return rc;
     }
+    undo.armed = false;
+    D->bvh8_tried = true;
     return MCPT_OK;
 }
 
@@ -5365,6 +5408,7 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         HIP_OK(hipMemcpy(hs, D.stats.p, kStatBytes, hipMemcpyDeviceToHost));
         for (int k = 1; k <= kStatShards; k++) hs[2] += hs[16 * k], hs[3] += hs[16 * k + 1];  // ray_stats shards
         stats->seconds = ms * 1e-3;
+        stats->device_seconds[0] = stats->seconds;
         stats->camera_samples = (uint64_t)(s1 - s0) * npx;
         stats->light_evals_survived = hs[1];
         stats->rays = hs[2];
@@ -5581,6 +5625,19 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
     std::vector<mcpt_stats> sst(nshards);
     std::vector<int> urc(nu, MCPT_OK);
     std::vector<std::string> uerr(nu);
+    std::vector<double> setup_s(nu, 0.0), render_s(nu, 0.0);
+    // the RCCL communicators over exactly these devices (cached per scene handle), created on this thread
+    // BEFORE any worker touches a device: ncclCommInitAll allocates and launches on every device of the
+    // clique, and never runs concurrently with the workers' scene uploads and queue allocations
+    double comm_init_s = 0.0;
+    if (sc->comm_devices != uniq) {
+        const auto c0 = std::chrono::steady_clock::now();
+        comm_all_destroy(sc->comms);
+        sc->comm_devices.clear();
+        if ((rc = comm_all_init(uniq, sc->comms))) return rc;  // nothing rendered yet: a clean failure
+        sc->comm_devices = uniq;
+        comm_init_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+    }
     const auto t0 = std::chrono::steady_clock::now();
     // one worker thread per distinct device: its scene state (the uploads of a 1M-triangle scene run
     // on all devices at once, not one after another), its framebuffer, then its shards in order
@@ -5592,6 +5649,7 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
         };
         int r;
         std::lock_guard<std::mutex> dev_lock(dev_mu[lock_of[u]]);
+        const auto w0 = std::chrono::steady_clock::now();
         if ((r = get_device_state(sc, uniq[u], &Ds[u]))) return fail(r);
         DeviceState& D = *Ds[u];
         if (hipDeviceSynchronize() != hipSuccess) {  // the caller's buffers may still be written by other streams
@@ -5619,6 +5677,13 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
                 return fail(MCPT_E_DEVICE);
             }
         }
+        const auto w1 = std::chrono::steady_clock::now();
+        setup_s[u] = std::chrono::duration<double>(w1 - w0).count();
+        struct RenderClock {  // the rank's shard time, recorded on every way out of the loop
+            double& out;
+            std::chrono::steady_clock::time_point a;
+            ~RenderClock() { out = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count(); }
+        } rclock{render_s[u], w1};
         for (int k = 0; k < nshards; k++) {
             if (shard_dev[k] != u) continue;
             int a, b;
@@ -5638,16 +5703,6 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
     };
     std::vector<std::thread> th;
     for (int u = 0; u < nu; u++) th.emplace_back(worker, u);
-    int crc = MCPT_OK;  // meanwhile: the RCCL communicators over exactly these devices (cached)
-    std::string cerr;
-    if (sc->comm_devices != uniq) {
-        comm_all_destroy(sc->comms);
-        sc->comm_devices.clear();
-        if ((crc = comm_all_init(uniq, sc->comms)))
-            cerr = mcpt_last_error();
-        else
-            sc->comm_devices = uniq;
-    }
     for (auto& t : th) t.join();
     // report the first real failure: a shard stopped by another's failure reports MCPT_E_CANCELLED,
     // which is the answer only when the user's progress callback asked for it
@@ -5657,10 +5712,6 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
     if (fu >= 0) {
         set_error("device %d: %s", uniq[fu], uerr[fu].c_str());
         return urc[fu];
-    }
-    if (crc) {
-        set_error("%s", cerr.c_str());
-        return crc;
     }
     const auto t1 = std::chrono::steady_clock::now();
     std::vector<hipStream_t> streams(nu);
@@ -5682,6 +5733,11 @@ int render_multi(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts*
         t.seconds = std::chrono::duration<double>(t2 - t0).count();
         t.reduce_seconds = std::chrono::duration<double>(t2 - t1).count();
         t.devices_used = nu;
+        t.comm_init_seconds = comm_init_s;
+        for (int u = 0; u < nu; u++) {
+            t.device_setup_seconds = std::max(t.device_setup_seconds, setup_s[u]);
+            if (u < MCPT_STATS_MAX_DEVICES) t.device_seconds[u] = render_s[u];
+        }
         *stats = t;
     }
     return MCPT_OK;

@@ -181,3 +181,23 @@ def tiny_far(outdir):
 
 STRESS = {"sphmix": (sphere_mix, 5200), "slivers": (slivers, 8 * 24 * 2 + 80), "tinyfar": (tiny_far, 12 * 48 + 224),
           "dense": (dense_sphere, 14160)}
+
+
+def needles(outdir, n=70000, seed=7, length=1.0):
+    """n thin random triangles ("needles", up to `length` long) in a 10-unit box in every direction, plus the floor:
+    nearly every object split of such a tree overlaps, so a >= 65 536-triangle build wants far more spatial-split
+    duplicates than its budget (bvh.cpp MCPT_BVH_SPATIAL_BUDGET) allows -- the budget-exhausting case of the
+    builder's determinism test"""
+    import random
+    rng = random.Random(seed)
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    ni = obj.normal((0.0, 1.0, 0.0))
+    faces = []
+    for _ in range(n):
+        a = tuple(rng.uniform(-5.0, 5.0) for _ in range(3))
+        b = tuple(min(5.0, max(-5.0, x + rng.uniform(-length, length))) for x in a)
+        c = tuple(x + rng.uniform(-0.02, 0.02) for x in a)
+        faces.append(((obj.vert(a), ni), (obj.vert(b), ni), (obj.vert(c), ni)))
+    obj.groups.append(("needles", "floor", faces))
+    return _write(outdir, "needles", obj, mtls, [], CAM)

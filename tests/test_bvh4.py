@@ -60,3 +60,17 @@ def test_builder_is_deterministic():
         assert mcpt.debug_bvh4_check(a, lo) == mcpt.debug_bvh4_check(b, lo)
         assert mcpt.debug_bvh8_check(a, lo) == mcpt.debug_bvh8_check(b, lo)
     assert mcpt.debug_bvh4_check(a)["duplicates"] > 0  # spatial splits did happen
+
+
+def test_builder_is_deterministic_when_the_spatial_budget_runs_out(tmp_path):
+    """a scene whose spatial splits want more duplicates than the budget (0.3 per triangle) allows: the budget is
+    handed down the tree by value (bvh.cpp splan), so the exhausted budget still gives the same tree on every load
+    -- parallel builder threads never race for it -- and the cap holds for the whole tree"""
+    paths = scenegen.needles(str(tmp_path))
+    a, b = mcpt.Scene.load(*paths), mcpt.Scene.load(*paths)
+    assert a.accel_bytes() == b.accel_bytes()
+    ra, rb = mcpt.debug_bvh4_check(a), mcpt.debug_bvh4_check(b)
+    print("needles bvh4: %s" % ra)
+    assert ra == rb and ok(ra, a.nfacets), ra
+    assert ra["duplicates"] > 0.2 * ra["facets"]  # the budget was (nearly) used up
+    assert mcpt.debug_bvh8_check(a) == mcpt.debug_bvh8_check(b)

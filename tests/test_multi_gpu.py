@@ -69,6 +69,25 @@ def test_device_list_equals_single_call(scene, single, devices):
     assert nodes(st) == nodes(st1) and st.shading_nodes == st1.shading_nodes
 
 
+def test_device_list_reports_where_the_time_went():
+    """mcpt_stats ABI 2.2: the first device-list call over a device set creates the communicator
+    (ncclCommInitAll, on the calling thread before any device work) and reports its wall time; the next
+    call reuses it (0).  Per-rank shard times are recorded and lie within the call's wall time."""
+    sc = mcpt.Scene.load(SCENE_OBJ, SCENE_XML)  # its own handle: the communicator is cached per scene
+    cam = mcpt.Camera.reference(80, 60)
+    _, st1 = mcpt.render(sc, cam, 8, mode="mis", seed=SEED, devices=[0, 0])
+    _, st2 = mcpt.render(sc, cam, 8, mode="mis", seed=SEED, devices=[0, 0])
+    print("comm init %.4f s then %.4f s; setup %.4f / %.4f s; per device %s / %s; call %.4f / %.4f s" % (
+        st1.comm_init_seconds, st2.comm_init_seconds, st1.device_setup_seconds, st2.device_setup_seconds,
+        st1.per_device_seconds(), st2.per_device_seconds(), st1.seconds, st2.seconds))
+    assert st1.comm_init_seconds > 0 and st2.comm_init_seconds == 0
+    for st in (st1, st2):
+        pd = st.per_device_seconds()
+        assert len(pd) == 1 and 0 < pd[0] <= st.seconds and st.device_setup_seconds <= st.seconds
+    assert st1.device_setup_seconds > st2.device_setup_seconds  # the first call uploads the scene
+    sc.close()
+
+
 def test_device_list_into_device_buffer(scene, single):
     import torch
     cam = mcpt.Camera.reference(80, 60)

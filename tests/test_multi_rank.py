@@ -265,6 +265,9 @@ def test_bench_two_ranks_under_torchrun(tmp_path):
     line = json.loads([ln for ln in text.splitlines() if ln.startswith("{\"metric\"")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["samples"] == 800 * 600 * 2 * 8
     assert line["config"]["job_spp_per_step"] == 16
+    # every rank's shard time, gathered over torch.distributed; mcpt_comm_init_rank timed by the caller
+    assert len(line["per_device_seconds"]) == 2 and min(line["per_device_seconds"]) > 0
+    assert line["comm_init_seconds"] > 0 and line["reduce_seconds"] > 0
 
 
 def test_bench_plain_launch_uses_n_gpus(tmp_path):
@@ -286,3 +289,36 @@ def test_bench_plain_launch_uses_n_gpus(tmp_path):
     assert line["config"]["job_spp_per_step"] == 16 and line["config"]["launch"] == "single process"
     assert "device list [0, 0]" in line["config"]["parallelism"]
 
+
+
+@pytest.mark.parametrize("config", ["c3", "c4"])
+def test_bench_plain_launch_eight_ranks(tmp_path, config):
+    """The driver's whole-node command, `python3 bench.py --gpus 8` (no torchrun), rehearsed on the one GPU:
+    one process, a device list of 8 entries, each its own rank of an 8-rank ncclCommInitAll clique of the
+    collective shim (RCCL refuses ranks sharing a device), one grouped reduce per step.  c3: 8 x 800x600 x S
+    samples per step (weak scaling); c4: BASELINE's C4 job, 1600x1200 x 4096 spp per step split into 8
+    shards of 512 spp (strong scaling).  The line must carry per-rank shard times, the reduce time and the
+    communicator's creation time (created before any device work, outside the timed region)."""
+    out = tmp_path / ("bench_plain8_%s.log" % config)
+    extra = ["--spp-per-step", "2"] if config == "c3" else ["--config", "c4"]
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1", "--no-cpu",
+           "--no-replay", "--collective-lib", SHIM] + extra
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MCPT_COLLSHIM_TIMEOUT"] = "120"
+    with open(out, "w") as f:
+        rc = subprocess.run(cmd, stdout=f, stderr=subprocess.STDOUT, timeout=420, env=env).returncode
+    text = out.read_text()
+    assert rc == 0, text[-3000:]
+    line = json.loads([ln for ln in text.splitlines() if ln.startswith("{\"metric\"")][-1])
+    print("bench --gpus 8 --config %s (rehearsal): %.1f Msamples/s, per rank %s s, reduce %.4f s, comm init %.4f s, "
+          "setup %.3f s" % (config, line["value"], line["per_device_seconds"], line["reduce_seconds"],
+                            line["comm_init_seconds"], line["device_setup_seconds"]))
+    samples = 8 * 800 * 600 * 2 if config == "c3" else 1600 * 1200 * 4096
+    assert line["n_gpus"] == 8 and line["value"] > 0 and line["samples"] == samples
+    assert line["config"]["launch"] == "single process" and line["config"]["config"] == config
+    assert "device list [0, 0, 0, 0, 0, 0, 0, 0]" in line["config"]["parallelism"]
+    assert line["config"]["job_spp_per_step"] == (16 if config == "c3" else 4096)
+    assert line["config"]["spp_per_step"] == (2 if config == "c3" else 512)
+    pd = line["per_device_seconds"]
+    assert len(pd) == 8 and min(pd) > 0 and line["device_imbalance"] >= 1.0
+    assert line["comm_init_seconds"] > 0 and line["reduce_seconds"] > 0 and line["device_setup_seconds"] is not None
