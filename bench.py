@@ -267,6 +267,9 @@ def main():
 
     import monte_carlo_path_tracing_amd as mcpt
 
+    import hashlib
+    with open(mcpt.LIB_PATH, "rb") as f:  # the binary this run times (the PMC profiles name theirs the same way)
+        lib_sha = hashlib.sha256(f.read()).hexdigest()
     rehearsal = bool(args.collective_lib)
     if rehearsal:
         mcpt.set_collective_lib(args.collective_lib)
@@ -407,9 +410,18 @@ def main():
                 if (k == n or (tail and k.startswith(head) and k.endswith(tail))) and v.get("valu_issue_frac") is not None:
                     out[k] = v["valu_issue_frac"]
         return out
-    def pmc_src(*names):  # the summaries the matched kernels' PMC figures came from
-        srcs = sorted({pk[k].get("source") or pmc.get("source") for n in names for k in busy(n)})
-        return "; ".join(s for s in srcs if s) or None
+    def pmc_src(*names):  # the summaries the matched kernels' PMC figures came from, and whether their binary is this one
+        ks = [k for n in names for k in busy(n)]
+        srcs = sorted({pk[k].get("source") or pmc.get("source") for k in ks})
+        if not srcs:
+            return None
+        shas = {pk[k].get("lib_sha256") for k in ks}
+        same = shas == {lib_sha}
+        return "; ".join(s for s in srcs if s) + (" -- profiled binary sha256 %s %s this run's" % (
+            "/".join(sorted(str(x)[:12] for x in shas)), "==" if same else "!="))
+    def pmc_same_binary(*names):
+        ks = [k for n in names for k in busy(n)]
+        return bool(ks) and {pk[k].get("lib_sha256") for k in ks} == {lib_sha}
     dev_s = max(totals.get("device_seconds", 0.0), 1e-12)
     # ---- roofline of the light prep (rank 0's launches; HIP events on its stream) ----
     roof_prep = None
@@ -433,12 +445,14 @@ def main():
         lane_k = [k for k in busy(*prep_k) if pk[k].get("hbm_bytes_per_dispatch")] if small else []
         if lane_k:
             traffic = pk[lane_k[0]]["hbm_bytes_per_dispatch"]
-            tsrc = "PMC profile, not this run: %s HBM bytes per dispatch (%s)" % (lane_k[0], pk[lane_k[0]].get("source"))
+            tsrc = "PMC profile, not this run: %s HBM bytes per dispatch (%s)" % (lane_k[0], pmc_src(*prep_k))
         elif hb and hb.get("hbm_bytes_per_node") is not None:
             traffic = hb["hbm_bytes_per_node"] * nodes / launches
             tsrc = ("PMC profile, not this run: %.1f HBM B/node (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
-                    "profiles/k_prep_hbm_bytes_per_node.json) x this run's %.0f full-prep nodes per launch"
-                    % (hb["hbm_bytes_per_node"], nodes / launches))
+                    "profiles/k_prep_hbm_bytes_per_node.json%s) x this run's %.0f full-prep nodes per launch"
+                    % (hb["hbm_bytes_per_node"], ", profiled binary sha256 %s %s this run's" % (
+                        str(hb.get("lib_sha256"))[:12], "==" if hb.get("lib_sha256") == lib_sha else "!="),
+                       nodes / launches))
         alg_gbs = nodes * PREP_BYTES_PER_NODE / prep_s / 1e9
         # the opt-in fp32 precision runs the full stage in packed fp32: its roof is the fp32 vector peak
         fp32 = args.precision == "fp32"
@@ -449,6 +463,7 @@ def main():
             "traffic": traffic, "traffic_source": tsrc,
             "valu_issue_frac": busy(*prep_k),
             "valu_issue_frac_source": pmc_src(*prep_k),
+            "pmc_same_binary": pmc_same_binary(*prep_k) and bool(hb is None or hb.get("lib_sha256") == lib_sha),
             "hbm_frac_algorithmic": round(alg_gbs / HBM_PEAK_GBS, 5),
             "hbm_frac_measured": round(traffic / t_launch / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
             "avg_launch_ms": round(t_launch * 1e3, 3), "launches": launches, "flop_per_launch": flops / launches,
@@ -487,8 +502,9 @@ def main():
             "frac": round(max(v_frac, h_frac), 4), "valu_frac": round(v_frac, 4), "mem_model_frac": round(h_frac, 4),
             "accel_bytes": accel, "bytes_per_node_visit": BYTES_NODE_VISIT[kname], "structure_level": level,
             "hbm_model_frac": hbm_model,
-            "traffic": hbm_meas, "traffic_source": ("PMC profile, not this run: %s" % (pk.get(pk_name, {}).get("source") or pmc.get("source"))) if hbm_meas else None,
+            "traffic": hbm_meas, "traffic_source": ("PMC profile, not this run: %s" % pmc_src(pk_name)) if hbm_meas else None,
             "valu_issue_frac": busy(pk_name), "valu_issue_frac_source": pmc_src(pk_name),
+            "pmc_same_binary": pmc_same_binary(pk_name),
             "avg_launch_ms": round(t_launch * 1e3, 3), "launches": tr_n,
             "node_visits_per_ray": round(visits / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),
             "tri_tests_per_ray": round(tests / max(totals.get("rays", 0) + totals.get("light_rays", 0), 1), 2),
@@ -540,6 +556,7 @@ def main():
         "l2_vs_cpu_max_pixel": l2max,
         "device_seconds": round(totals.get("seconds", 0.0), 4),
         "samples": samples,
+        "lib_sha256": lib_sha,
         # where a multi-GPU step's time went (mcpt_stats ABI 2.2): each rank's shard wall time summed over the
         # timed steps (setup and reduce excluded; max/min = load imbalance), the reduces' time, and -- outside the
         # timed region -- the communicator's creation and the first call's device setup

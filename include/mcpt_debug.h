@@ -18,8 +18,12 @@ enum {
     MCPT_DEBUG_COUNT_TRAVERSAL = 1 << 18,
     MCPT_DEBUG_SHARD_RANKS = 1 << 19,
     MCPT_DEBUG_RAYS_PERSIST = 1 << 20,
-    MCPT_DEBUG_RAYS_CW8 = 1 << 21
+    MCPT_DEBUG_RAYS_CW8 = 1 << 21,
+    MCPT_DEBUG_FUSED_CULL = 1 << 22
 };
+/* MCPT_DEBUG_FUSED_CULL: the MIS children's light prep runs its cheap stages inside k_prep_pk2, one wave per
+ * node (prep variant 8, chunks below the node's tangent plane skipped), instead of k_prep_cull_lanes' lane per
+ * node writing candidate words that k_prep_pk2 reads back (variant 17). */
 /* MCPT_DEBUG_RAYS_PERSIST: the MIS / shade ray sets of every scene go through the persistent refilling
  * traversal (by default only trees beyond an XCD's L2 do; smaller ones take k_mis_rays, one ray per thread).
  * MCPT_DEBUG_RAYS_CW8: the persistent traversal walks the 8-wide compressed trees (k_rays_cw8) instead of the

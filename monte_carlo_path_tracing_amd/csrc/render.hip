@@ -360,7 +360,10 @@ __host__ __device__ inline int tri_filter(float4 a4, float4 b4, float4 c4, const
 #ifndef MCPT_TRACE_DIAG
 #define MCPT_TRACE_DIAG 0
 #endif
-template <int kLds, bool kCount = false, int kTop = 0, bool kFilter = true>
+// kLazyBG: the running best keeps its leaf slot instead of (beta, gamma) -- 1 VGPR for 4 across the whole
+// traversal -- and the winner's (beta, gamma) are recomputed once at the end by the same operations on the same
+// triangle, so they are bit-identical (MCPT_RAYS_LAZY_BG, k_mis_rays)
+template <int kLds, bool kCount = false, int kTop = 0, bool kFilter = true, bool kLazyBG = false>
 __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4* __restrict__ leafv, d3 ro, d3 rd,
                                 int exclude, int* __restrict__ lds, int stride, unsigned* visits = nullptr,
                                 unsigned* tests = nullptr, const BvhNode4* top = nullptr, float tlimit0 = FLT_MAX,
@@ -381,6 +384,7 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     // tlimit0: at least the t of a triangle tri_hit accepts (or FLT_MAX) -- boxes beyond it hold no
     // closest hit
     float tlimit = tlimit0;
+    int best_q = -1;  // kLazyBG: the winner's leaf slot
     // the reference's fp64 test of leaf triangle q (the facet is not `exclude`): a sign pre-test
     // rejects beta < 0, gamma < 0 and t < 0 before the three divisions, which are tri_hit's
     auto exact = [&](int q) {
@@ -398,8 +402,12 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
         if (tt < best.t || (tt == best.t && fac < best.f)) {
             best.f = fac;
             best.t = tt;
-            best.beta = beta;
-            best.gamma = gamma;
+            if (kLazyBG) {
+                best_q = q;
+            } else {
+                best.beta = beta;
+                best.gamma = gamma;
+            }
             tlimit = fminf(tlimit, (float)tt * 1.0001f + 1e-5f);
         }
     };
@@ -489,6 +497,13 @@ __device__ inline Hit trace4_ww(const BvhNode4* __restrict__ nodes, const float4
     }
     if (kFilter && pend0 >= 0) exact(pend0);
     if (kFilter && pend1 >= 0) exact(pend1);
+    if (kLazyBG && best_q >= 0) {  // the winner's (beta, gamma): exact()'s operations on its triangle
+        const float4 a4 = leafv[3 * best_q], b4 = leafv[3 * best_q + 1], c4 = leafv[3 * best_q + 2];
+        const d3 a = f3(a4), ab = sub(a, f3(b4)), ac = sub(a, f3(c4)), ar = sub(a, ro);
+        const double detA = det3(ab, ac, rd);
+        best.beta = det3(ar, ac, rd) / detA;
+        best.gamma = det3(ab, ar, rd) / detA;
+    }
     return best;
 }
 
@@ -2256,6 +2271,9 @@ struct CullOrder {
     unsigned* count = nullptr;
 };
 
+#ifndef MCPT_FUSED_CLASSES
+#define MCPT_FUSED_CLASSES 1
+#endif
 // an all-zero candidate word skips its list append by a scalar branch (same-box A/B: 410.6 / 425.0 /
 // 425.1 vs 423.8 / 415.8 / 421.9 Msamples/s, profiles/round2b_ab_zero_words.txt)
 constexpr int kMaskBatch = kMaskLine;  // candidate words per batch of scalar loads (k_prep_pk2): one line
@@ -2326,13 +2344,21 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
         const v2f nx2{nf.nx, nf.nx}, ny2{nf.ny, nf.ny}, nz2{nf.nz, nf.nz};
         const v2f nxs{nf.nx, nf.x}, nys{nf.ny, nf.y}, nzs{nf.nz, nf.z};
         // phase A: cheap stages over all chunks, kChunkUnroll chunks' table loads in flight at a
-        // time (the loop is L2-latency-bound; the tables are padded to whole groups of 4 chunks)
+        // time (the loop is L2-latency-bound; the tables are padded to whole groups of 4 chunks).
+        // MCPT_FUSED_CLASSES: a chunk wholly below the node's tangent plane (chunk_class, the node is the
+        // wave's, so the class is wave-uniform) holds no candidate and is skipped, loads included
+        const float ncls = -(float)(dot(nn, x1) + MCPT_EPS);  // chunk_class's form, as k_prep_cull_lanes
         for (int c = 0; c < nchunks; c += kChunkUnroll) {
             float4 X[kChunkUnroll], Y[kChunkUnroll], Z[kChunkUnroll];
             float dl[kChunkUnroll];
+            bool skip[kChunkUnroll];
 #pragma unroll
             for (int q = 0; q < kChunkUnroll; q++) {
                 const int cq = c + q;
+                skip[q] = MCPT_FUSED_CLASSES && cq < nchunks &&
+                          __builtin_amdgcn_readfirstlane(chunk_class(nf.nx, nf.ny, nf.nz, ncls, nf.err, S.chunk_sph[cq])) ==
+                              kChunkBelow;
+                if (skip[q]) continue;
                 X[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48, cq * 3072, 0));
                 Y[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 16, cq * 3072, 0));
                 Z[q] = u4f(__builtin_amdgcn_raw_buffer_load_b128(rpk, lane * 48 + 32, cq * 3072, 0));
@@ -2340,6 +2366,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_prep_pk2(DScene S, ui
             }
 #pragma unroll
             for (int q = 0; q < kChunkUnroll; q++) {
+                if (skip[q]) continue;
                 const int li = (c + q) * 64 + lane;
                 const int stage = prep_stage_pk_bf(S, li, X[q], Y[q], Z[q], dl[q], nx2, ny2, nz2, nxs, nys, nzs, cn, x1, nn, nf.err);
                 const uint64_t m = __ballot(stage == 0);
@@ -3256,6 +3283,9 @@ __global__ __launch_bounds__(256, MCPT_LB_GEN) void k_mis_gen(Params P, Queue cu
     A.flags[i] = flags;
 }
 
+#ifndef MCPT_RAYS_LAZY_BG
+#define MCPT_RAYS_LAZY_BG 1
+#endif
 // closest hits of ray set blockIdx.y (0: d1, 1: d2, 2: d2 against the light-only BVH) from the
 // queue's shading points, excluding the origin facet
 // kCount: counts node visits / triangle tests into cnt[0] / cnt[1] (statistics replay only)
@@ -3326,7 +3356,7 @@ __global__ __launch_bounds__(kRayBlock, MCPT_LB_RAYS) void k_mis_rays(DScene S, 
                 const double t0 = A.hbg[2 * ((size_t)set * A.cap + i)];
                 if (t0 > 0) tl0 = (float)t0 * 1.0001f + 1e-5f;
             }
-            h = trace4_ww<kRayTopLds, kCount, kTop, MCPT_FILTER_MIS>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
+            h = trace4_ww<kRayTopLds, kCount, kTop, MCPT_FILTER_MIS, MCPT_RAYS_LAZY_BG>(set == 2 ? S.lbvh4 : S.bvh4, leafv, ro, rd, cur.f[i],
                                                     stack + threadIdx.x, kRayBlock, &visits, &tests, top, tl0, &witer, &wleaf);
         }
         f = h.f;
@@ -3730,6 +3760,9 @@ __global__ __launch_bounds__(kRayBlock, MCPT_CW8_WAVES) void k_rays_cw8(DScene S
     if (kCount && MCPT_TRACE_DIAG) wave_count2(cnt + 6, witer, cnt + 7, wleaf);
 }
 
+#ifndef MCPT_COMBINE_LAZY
+#define MCPT_COMBINE_LAZY 1
+#endif
 template <bool kStale>
 __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, Queue cur, int n, Aux A, Queue nxt, Slots T, int rp) {
     const DScene& S = P.S;
@@ -3749,11 +3782,16 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
     const d3 N = ld3(cur.n, cur.cap, ii);
     const int li = (c2 && (fl & 4) && hl >= 0) ? S.tri_light[hl] : -1;
     const double own[7] = {p.x, p.y, p.z, N.x, N.y, N.z, cur.wsum[ii]};
-    const d3 d1 = ld3(A.d1, A.cap, ii);
-    const d3 d2 = ld3(A.d2, A.cap, ii);
-    const d3 w1 = ld3(A.w1, A.cap, ii);
-    const d3 w2 = ld3(A.w2, A.cap, ii);
-    const double pdf = A.c2[2 * ii], cosb = A.c2[2 * ii + 1];
+    // a ray set's direction, throughput and (pdf, cos) matter only when that set hit (c1 / c2): the stale
+    // form reads them under that predicate, so a lane whose ray missed fetches none of its 48-104 B
+    // (MCPT_COMBINE_LAZY; the fresh form reads them all, as before)
+    const bool lz = MCPT_COMBINE_LAZY && kStale;
+    const d3 z3 = mk3(0, 0, 0);
+    const d3 d1 = (!lz || c1) ? ld3(A.d1, A.cap, ii) : z3;
+    const d3 w1 = (!lz || c1) ? ld3(A.w1, A.cap, ii) : z3;
+    const d3 d2 = (!lz || c2) ? ld3(A.d2, A.cap, ii) : z3;
+    const d3 w2 = (!lz || c2) ? ld3(A.w2, A.cap, ii) : z3;
+    const double pdf = (!lz || c2) ? A.c2[2 * ii] : 0.0, cosb = (!lz || c2) ? A.c2[2 * ii + 1] : 0.0;
     if (!kStale) {  // fresh light pdf (this node's own prep) and forward throughputs
         d3 tp2 = mk3(0, 0, 0);
         if (c2) tp2 = mul(w2, cosb / (pdf + state_light_pdf(S, li, own)) / MCPT_P_RR);
@@ -3762,12 +3800,15 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
                    2 * node + 1, nxt);
     } else {
         const int f1 = c1 ? h1 : -1, f2 = c2 ? h2 : -1;
-        const Entry e1 = entry_eval(P, c1, f1, A.hbg[2 * o1], A.hbg[2 * o1 + 1], mul(d1, -1), pixel, sample, 2 * node);
-        const Entry e2 = entry_eval(P, c2, f2, A.hbg[2 * o2], A.hbg[2 * o2 + 1], mul(d2, -1), pixel, sample, 2 * node + 1);
+        const double b1 = c1 ? A.hbg[2 * o1] : 0.0, g1 = c1 ? A.hbg[2 * o1 + 1] : 0.0;
+        const double b2 = c2 ? A.hbg[2 * o2] : 0.0, g2 = c2 ? A.hbg[2 * o2 + 1] : 0.0;
+        const double s1 = (!lz || c1) ? A.s1[ii] : 0.0;
+        const Entry e1 = entry_eval(P, c1, f1, b1, g1, mul(d1, -1), pixel, sample, 2 * node);
+        const Entry e2 = entry_eval(P, c2, f2, b2, g2, mul(d2, -1), pixel, sample, 2 * node + 1);
         const bool lsh = e1.kind == 2, bsh = e2.kind == 2;
         // light edge: an emitter child finishes it now (main.cpp:464 with the child's emission)
         d3 Llight = mk3(0, 0, 0);
-        if (e1.kind == 1) Llight = mul(hmul(mk3(S.light_rad[3 * e1.li], S.light_rad[3 * e1.li + 1], S.light_rad[3 * e1.li + 2]), w1), A.s1[ii]);
+        if (e1.kind == 1) Llight = mul(hmul(mk3(S.light_rad[3 * e1.li], S.light_rad[3 * e1.li + 1], S.light_rad[3 * e1.li + 2]), w1), s1);
         // BRDF edge scalar: without a shading light child the sampler state is this node's own
         double s2 = 0;
         if (c2 && !lsh) s2 = cosb / (pdf + state_light_pdf(S, li, own)) / MCPT_P_RR;
@@ -3790,7 +3831,7 @@ __global__ __launch_bounds__(256, MCPT_LB_COMBINE) void k_mis_combine(Params P, 
                                                     (int)lsh | ((int)bsh << 1) | ((e2.kind == 1) << 2) | ((int)c2 << 3) | ((int)need << 4),
                                                     li);
             double* w = r + 2;
-            w[0] = w1.x, w[1] = w1.y, w[2] = w1.z, w[3] = A.s1[ii];
+            w[0] = w1.x, w[1] = w1.y, w[2] = w1.z, w[3] = s1;
             w[4] = w2.x, w[5] = w2.y, w[6] = w2.z, w[7] = pdf, w[8] = cosb, w[9] = s2;
             if (!lsh) T.Ll[3 * q] = Llight.x, T.Ll[3 * q + 1] = Llight.y, T.Ll[3 * q + 2] = Llight.z;
             if (e2.kind == 1) r[12] = S.light_rad[3 * e2.li], r[13] = S.light_rad[3 * e2.li + 1], r[14] = S.light_rad[3 * e2.li + 2];
@@ -4892,7 +4933,7 @@ int validate_render(const mcpt_render_opts* o) {
     }
     if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
                      MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL |
-                     MCPT_DEBUG_SHARD_RANKS | MCPT_DEBUG_RAYS_PERSIST | MCPT_DEBUG_RAYS_CW8)) {
+                     MCPT_DEBUG_SHARD_RANKS | MCPT_DEBUG_RAYS_PERSIST | MCPT_DEBUG_RAYS_CW8 | MCPT_DEBUG_FUSED_CULL)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
@@ -5069,6 +5110,15 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         rl.pool = (double*)D.lit_pool.p;
     }
     if ((MCPT_RAYS_CW8 || (o->flags & MCPT_DEBUG_RAYS_CW8)) && (rc = ensure_bvh8(sc, &D))) return rc;
+    // which traversal the MIS / shade ray sets take: the persistent refilling waves for trees beyond an XCD's
+    // 4 MiB L2 and for shade-area's rays (k_rays_persistent, or k_rays_cw8 on the 8-wide trees), else one ray
+    // per thread (k_mis_rays)
+    const bool rays_pers = !grid && ((o->flags & MCPT_DEBUG_RAYS_PERSIST) || MCPT_RAYS_PERSISTENT > 0 ||
+                                     (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20)) ||
+                                     (MCPT_PERSIST_SHADE_AREA && o->mode == MCPT_MODE_SHADE_AREA));
+    // (round 6: k_rays_persistent handing the combine its hit points instead of (beta, gamma) was measured slower,
+    // C5 -2..-6%, shade-area -9%: profiles/round6_ab_hit_points.txt)
+    const bool rays_cw8 = rays_pers && (MCPT_RAYS_CW8 || (o->flags & MCPT_DEBUG_RAYS_CW8)) && D.d.bvh8 && D.d.lbvh8;
     // every buffer is allocated above (first-call hipMalloc of the cache is not device work); the
     // timed region (seconds, HIP events) starts at the primary-hit kernel
     HIP_OK(hipMemsetAsync(D.stats.p, 0, kStatBytes, st));
@@ -5248,10 +5298,12 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             if (pc.use || small_use) {  // children: full prep; roots: pick from the root-point cache
                 const int nc = (int)n_children, nr = ni - nc;
                 if (nc > 0) {
-                    nmask = prep_writes_masks(D.d, masks) ? nc : 0;
+                    // MCPT_DEBUG_FUSED_CULL (A/B): the cheap stages inside k_prep_pk2, wave per node (variant 8)
+                    uint64_t* cmasks = (o->flags & MCPT_DEBUG_FUSED_CULL) ? nullptr : masks;
+                    nmask = prep_writes_masks(D.d, cmasks) ? nc : 0;
                     HIP_OK(hipEventRecord(D.evp0, st));
                     HIP_OK(launch_prep(-1, D.d, o->seed, nc, cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr,
-                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, masks,
+                                       cur->wsum, cur->pick, nullptr, P.stats, (unsigned*)D.work.p, st, cx, cmasks,
                                        count_c1, fp32, corder));
                     HIP_OK(hipEventRecord(D.evp1, st));
                     timed = true;
@@ -5307,18 +5359,15 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
         const dim3 g256((ni + 255) / 256), b256(256);
         unsigned long long* tcnt = P.stats + 8;  // node visits, triangle tests (MCPT_DEBUG_COUNT_TRAVERSAL)
     auto launch_rays = [&](int first_set, int nsets, int seeded) {
-        const bool force_pers = (o->flags & MCPT_DEBUG_RAYS_PERSIST) != 0;
         // shade() with uniform-area light points: its shadow and bounce rays run 4% faster on the refilling
         // persistent waves even on the small stand-in (shade_area 2 104-2 126 -> 2 185-2 191 Msamples/s, same
         // binary, profiles/round5_ab_persistent_veach.txt); MIS and shade() are slower there (-1%, -1%)
-        const bool pers = force_pers || MCPT_RAYS_PERSISTENT > 0 || (MCPT_RAYS_PERSISTENT < 0 && accel > (4ull << 20)) ||
-                          (MCPT_PERSIST_SHADE_AREA && o->mode == MCPT_MODE_SHADE_AREA);
-        if (pers && !grid) {
+        if (rays_pers) {
             unsigned* pool = (unsigned*)D.work.p + 8;
             (void)hipMemsetAsync(pool, 0, sizeof(unsigned), st);
             const long long items = (long long)nsets * ni;
             const int blocks = (int)std::max<long long>(1, std::min<long long>((items + kRayBlock - 1) / kRayBlock, 2048));
-            if ((MCPT_RAYS_CW8 || (o->flags & MCPT_DEBUG_RAYS_CW8)) && D.d.bvh8 && D.d.lbvh8) {
+            if (rays_cw8) {
                 if (count_trav)
                     hipLaunchKernelGGL(k_rays_cw8<true>, dim3(blocks), dim3(kRayBlock), 0, st, D.d, *cur, ni, aux, first_set, nsets,
                                        pool, tcnt, MCPT_SEED_LIGHT ? seeded : 0);

@@ -1126,6 +1126,8 @@ typedef struct {
     uint64_t stats[4]; /* shading nodes, light preps, extension rays, light-only rays */
     int area_lights;  /* shade(): select_a_point_from_lights instead of the spherical sampler */
     int fresh_pdf;    /* counter RNG with the node's own light pdf (ORC_FLAG_FRESH_PDF) */
+    int max_depth;    /* counter RNG: deepest node depth evaluated (COUNTER_MAX_DEPTH; orc_depth_study varies it) */
+    uint64_t* depth_hist; /* orc_depth_study: MIS nodes past entry + RR by depth [0, 63); [63] nodes cut by the cap */
 } ctx;
 
 /* discrete_distribution over w[0..n) as libstdc++ (random.tcc): fewer than two weights -> index 0,
@@ -1236,7 +1238,11 @@ static __thread int g_dbg_n, g_dbg_cap;
 
 static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t node) {
     const orc_scene* s = C->s;
-    if (C->rng == ORC_RNG_COUNTER && node >= ((uint64_t)2 << COUNTER_MAX_DEPTH)) return mk(0, 0, 0); /* heap id */
+    const int depth = 63 - __builtin_clzll(node); /* heap id: root 1 at depth 0, children 2n / 2n + 1 */
+    if (C->rng == ORC_RNG_COUNTER && depth > C->max_depth) {
+        if (C->depth_hist) C->depth_hist[63]++;
+        return mk(0, 0, 0);
+    }
     C->stats[0]++;
     double a0 = 1.0 - beta - gamma;
     v3 p = vadd(vadd(vmul(fvert(s, f, 0), a0), vmul(fvert(s, f, 1), beta)), vmul(fvert(s, f, 2), gamma));
@@ -1257,6 +1263,7 @@ static v3 shade_mis(ctx* C, int f, double beta, double gamma, v3 wo, uint64_t no
         ksi = counter_u(key, 0);
     }
     if (ksi > P_RR) return mk(0, 0, 0);
+    if (C->depth_hist) C->depth_hist[depth]++;
 
     /* light branch (main.cpp:443-466) */
     v3 L_light = mk(0, 0, 0);
@@ -1463,6 +1470,7 @@ static void ctx_init(ctx* C, const orc_scene* s, int rng) {
     memset(C, 0, sizeof *C);
     C->s = s;
     C->rng = rng;
+    C->max_depth = COUNTER_MAX_DEPTH;
     ls_init(&C->L, s->NL);
 }
 
@@ -1532,6 +1540,63 @@ int orc_render(const orc_scene* s, const orc_camera* cam, int mode, uint64_t see
         ls_free(&C.L);
     }
     if (stats4) for (int k = 0; k < 4; k++) stats4[k] = tot[k];
+    return 0;
+}
+
+/* depth-cap study (test infrastructure): orc_render's MIS frame (counter RNG, the GPU's
+ * semantics) with the MIS tree cut below depth max_depth (<= 62: heap ids of depth 63 nodes' children overflow
+ * 64 bits) instead of COUNTER_MAX_DEPTH, and hist[64]: nodes past entry + RR per depth, hist[63] = nodes cut
+ * by the cap.  Samples of the same seed are the same trees down to the cap, so two caps' frames differ
+ * exactly by what the deeper levels contribute. */
+int orc_depth_study(const orc_scene* s, const orc_camera* cam, uint64_t seed, int spp, int stride, int offset,
+                    int nthreads, int max_depth, double* out, uint64_t* hist) {
+    if (!s->grid_ok) { set_err("grid not built"); return -1; }
+    if (max_depth < 0 || max_depth > 62) { set_err("max_depth must be in [0, 62]"); return -1; }
+    cam_frame fr = cam_setup(cam);
+    const int W = cam->width, H = cam->height;
+    if (stride < 1) stride = 1;
+    int nx = (W - offset + stride - 1) / stride, ny = (H - offset + stride - 1) / stride;
+    if (nx < 0) nx = 0;
+    if (ny < 0) ny = 0;
+    long npx = (long)nx * ny;
+    const double inv = 1.0 / spp;
+    for (int k = 0; k < 64; k++) hist[k] = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+    {
+        ctx C;
+        ctx_init(&C, s, ORC_RNG_COUNTER);
+        uint64_t h[64] = {0};
+        C.seed = seed;
+        C.max_depth = max_depth;
+        C.depth_hist = h;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+        for (long q = 0; q < npx; q++) {
+            int i = offset + (int)(q / nx) * stride, j = offset + (int)(q % nx) * stride;
+            v3 dir = cam_dir(&fr, i, j);
+            hitrec hh;
+            int f = grid_trace(s, fr.eye, dir, -1, 0, &hh);
+            double* px = out + 3 * ((size_t)i * W + j);
+            v3 sum = mk(px[0], px[1], px[2]);
+            if (f >= 0) {
+                C.pixel = (uint64_t)i * W + j;
+                for (int k = 0; k < spp; k++) {
+                    C.sample = (uint64_t)k;
+                    sum = vadd(sum, vmul(shade_root(&C, ORC_MODE_MIS, f, hh.beta, hh.gamma, vmul(dir, -1)), inv));
+                }
+            }
+            st3(px, sum);
+        }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        for (int k = 0; k < 64; k++) hist[k] += h[k];
+        ls_free(&C.L);
+    }
     return 0;
 }
 

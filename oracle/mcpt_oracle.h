@@ -108,6 +108,11 @@ void orc_shade_sample(const orc_scene* s, const orc_camera* cam, int mode, int r
 int orc_render(const orc_scene* s, const orc_camera* cam, int mode, uint64_t seed, int spp, int s0, int s1,
                int stride, int offset, int nthreads, double* out_rgb, uint64_t* stats4);
 
+/* depth-cap study: the MIS frame with the tree cut below depth max_depth (<= 62) and the nodes per depth
+ * (hist[64], [63] = nodes cut), see mcpt_oracle.c */
+int orc_depth_study(const orc_scene* s, const orc_camera* cam, uint64_t seed, int spp, int stride, int offset,
+                    int nthreads, int max_depth, double* out_rgb, uint64_t* hist);
+
 /* debugging aid: per-node records of one MIS camera sample (counter RNG), see mcpt_oracle.c */
 int orc_debug_mis_sample(const orc_scene* s, const orc_camera* cam, int mode, uint64_t seed, int i, int j, int sample,
                          double* rec, int max_nodes);

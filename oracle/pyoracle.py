@@ -78,6 +78,9 @@ def lib():
         L.orc_render.restype = C.c_int
         L.orc_render.argtypes = [P, C.POINTER(Camera), C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_int, dp, up]
+        L.orc_depth_study.restype = C.c_int
+        L.orc_depth_study.argtypes = [P, C.POINTER(Camera), C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      dp, up]
         L.orc_counter_uniform.restype = C.c_double
         L.orc_counter_uniform.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]
         _lib = L
@@ -181,6 +184,17 @@ class Scene:
         if rc != 0:
             raise RuntimeError(lib().orc_last_error().decode())
         return out, stats
+
+    def depth_study(self, cam, seed, spp, max_depth, stride=1, offset=0, nthreads=1):
+        """MIS frame with the tree cut below depth max_depth (<= 62) and the nodes per depth (64 counts, [63] =
+        nodes cut by the cap): orc_depth_study"""
+        out = np.zeros((cam.height, cam.width, 3))
+        hist = np.zeros(64, np.uint64)
+        rc = lib().orc_depth_study(self.h, C.byref(cam), int(seed), spp, stride, offset, nthreads, int(max_depth),
+                                   out.reshape(-1), hist)
+        if rc != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return out, hist
 
 
 def brdf_phong(n, wi, wr, kd, ks, ns):

@@ -142,6 +142,27 @@ def test_occluded_room_is_supercritical(tmp_path):
     assert ost[1] > 100 * 12  # prep nodes per camera sample, far above a subcritical tree's ~2
 
 
+def test_depth_cap_truncates_nothing_measurable(tmp_path):
+    """The counter-RNG trees stop below depth 48 (device_math.h MCPT_MAX_DEPTH, the oracle's COUNTER_MAX_DEPTH);
+    the reference has no cap (main.cpp:429-437).  On the supercritical room (m ~ 1.13 children per node, the
+    node count per level GROWS) the frame cut at 48 equals the frame cut at 62 to rounding, and already at 24
+    the deeper levels carry < 1e-12 of the frame: a level's contribution decays with the surfaces' albedo
+    (~0.15 per level here), not with the tree's size (tools/depth_cap_study.py, profiles/round6_depth_cap.json)."""
+    obj, xml = scenegen.occluded_room(str(tmp_path))
+    o = po.Scene(obj, xml)
+    c = o.camera()
+    c.width, c.height = 4, 3
+    e, _ = po.camera_ray(c, 0, 0)
+    o.build_grid(e)
+    f24, _ = o.depth_study(c, SEED, 2, 24, nthreads=8)
+    f48, h48 = o.depth_study(c, SEED, 2, 48, nthreads=8)
+    f62, h62 = o.depth_study(c, SEED, 2, 62, nthreads=8)
+    n = h62[:63].astype(float)
+    assert n[40] > n[20] > n[5] > 0  # supercritical: more nodes at every deeper level
+    assert h48[63] > 0  # the cap does cut nodes here
+    assert rel_l2(f48, f62) <= 1e-15 and rel_l2(f24, f62) <= 1e-12, (rel_l2(f48, f62), rel_l2(f24, f62))
+
+
 @pytest.mark.gpu
 def test_supercritical_tree_spills_and_matches_oracle(tmp_path):
     """Binary recursion main.cpp:455-491 with occluded lights: each generation outgrows the queue

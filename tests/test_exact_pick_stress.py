@@ -124,7 +124,9 @@ def test_cull_chunk_classes_change_no_candidate(scenes, name):
     plane skips the plane test / the whole chunk) and the node order that makes them wave-uniform change
     work only: 20 000 points area-sampled on both sides of every non-light facet (above, below and
     straddling chunks all occur), prep variant 17 (ordered, classes on) vs 18 (the plain cull) --
-    weights_sum and picks bit-identical."""
+    weights_sum and picks bit-identical.  Also prep variant 8 (the cheap stages inside k_prep_pk2, one wave per
+    node, chunks below the tangent plane skipped: MCPT_DEBUG_FUSED_CULL's form) -- the same candidates in the
+    same order, so the same bits."""
     if name == "veach":
         from conftest import SCENE_OBJ as obj, SCENE_XML as xml
     else:
@@ -135,9 +137,12 @@ def test_cull_chunk_classes_change_no_candidate(scenes, name):
     X, N, u = surface_points(po.Scene(obj, xml), 20000, seed=11)
     _, ws17, p17 = mcpt.debug_prep_bench(s, X, N, u, variant=17, iters=1)
     _, ws18, p18 = mcpt.debug_prep_bench(s, X, N, u, variant=18, iters=1)
+    _, ws8, p8 = mcpt.debug_prep_bench(s, X, N, u, variant=8, iters=1)
     assert (ws17 > 0).sum() >= 2000
     assert np.array_equal(ws17.view(np.int64), ws18.view(np.int64))
     assert np.array_equal(p17, p18)
+    assert np.array_equal(ws17.view(np.int64), ws8.view(np.int64))
+    assert np.array_equal(p17, p8)
 
 
 def test_cull_order_at_scale_changes_no_candidate():

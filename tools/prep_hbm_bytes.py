@@ -46,9 +46,12 @@ def main():
     fetch, nf = per_kernel(a.fetch, "FETCH_SIZE")
     write, _ = per_kernel(a.write, "WRITE_SIZE")
     tot = None
+    line_json = {}
     for line in open(a.log):
         if line.startswith("rank 0 totals:"):
             tot = json.loads(line.split(":", 1)[1])
+        if line.startswith("{"):
+            line_json = json.loads(line)
     # totals cover the timed steps; the profile also saw the warmup steps and bench.py's untimed
     # replay of the timed steps (the cull statistic pass, MIS/shade) -- same work per step
     nodes = tot["prep_full_nodes"] * ((1 + a.replay) * a.steps + a.warmup) / a.steps
@@ -66,6 +69,9 @@ def main():
         "per_kernel_bytes_per_node": {k: round((mult[k] * fetch[k] + write.get(k, 0.0)) / nodes, 1) for k in kernels},
         "dispatches": {k: nf[k] for k in kernels},
         "full_prep_nodes": int(nodes),
+        # the profiled binary (bench.py's line names the library it loaded), so a bench line can tell whether these
+        # bytes are its own binary's
+        "lib_sha256": line_json.get("lib_sha256"),
         "method": "rocprofv3 --pmc FETCH_SIZE (x2 for k_prep_pk2's 16-B-per-lane record loads, gfx950's 64-B tally of 128-B requests; x1 for the cull's scalar loads) and --pmc WRITE_SIZE in "
                   "separate passes over `bench.py --steps %d --warmup %d --no-cpu`; bytes of both kernels over all "
                   "dispatches / full-prep nodes (timed-step count scaled to the profiled steps: warmup + timed%s); "

@@ -55,6 +55,31 @@ def counters(d):
     return {k: dict(v, dispatches=len(disp[k])) for k, v in agg.items()}
 
 
+def provenance(lib_path, bench_line=None):
+    """what the profiled binary was: the sha256 of the library the GPU run loaded (bench.py prints it in its line;
+    else the in-tree file now), the git commit and the tree hash of the library's sources at summarization time
+    (the tree hash stays the same across later documentation-only commits)"""
+    import hashlib
+    import subprocess
+    out = {}
+    sha = (bench_line or {}).get("lib_sha256")
+    if not sha and os.path.exists(lib_path):
+        with open(lib_path, "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()
+    out["lib_sha256"] = sha
+
+    def git(*a):
+        try:
+            return subprocess.run(["git", "-C", ROOT] + list(a), capture_output=True, text=True, check=True).stdout.strip()
+        except (OSError, subprocess.CalledProcessError):
+            return None
+    out["head"] = git("rev-parse", "HEAD")
+    out["code_tree"] = git("rev-parse", "HEAD:monte_carlo_path_tracing_amd/csrc")
+    dirty = git("status", "--porcelain", "--", "monte_carlo_path_tracing_amd/csrc", "include")
+    out["code_dirty"] = bool(dirty) if dirty is not None else None
+    return out
+
+
 def pmc_latest(tag, summary):
     """Per-kernel PMC figures bench.py attaches to its roofline objects (profiles/pmc_latest.json):
     valu_issue_frac (module docstring), the effective clock GRBM_GUI_ACTIVE / 8 / duration, and
@@ -62,7 +87,7 @@ def pmc_latest(tag, summary):
     GRBM counters come from separate passes over the same workload, so both are taken per dispatch."""
     ks, sq, hbm = summary.get("kernel_stats", {}), summary.get("sq", {}), summary.get("hbm", {})
     out = {"source": "profiles/%s_summary.json (rocprofv3 --pmc passes; tools/summarize_profiles.py)" % tag,
-           "kernels": {}}
+           "kernels": {}, "provenance": summary.get("provenance")}
     for k, h in hbm.items():
         if not k.startswith("k_") or k not in sq or not h.get("grbm_gui_active"):
             continue
@@ -95,6 +120,7 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--sq")
     ap.add_argument("--bench")
+    ap.add_argument("--lib", default=os.path.join(ROOT, "monte_carlo_path_tracing_amd", "libmcpt_hip.so"))
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -136,6 +162,7 @@ def main():
                 summary["bench"] = json.loads(line)
             if line.startswith("rank 0 totals:"):
                 summary["bench_totals"] = json.loads(line.split(":", 1)[1])
+    summary["provenance"] = provenance(a.lib, summary.get("bench"))
     with open(os.path.join(out, "%s_summary.json" % a.tag), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     latest = pmc_latest(a.tag, summary)
@@ -153,15 +180,20 @@ def main():
         # entries.  "kernels" is the headline's, with kernels only other workloads run added
         wl = a.tag.split("_", 1)[1] if "_" in a.tag else "c3"
         configs = dict(old.get("configs", {}))
-        configs[wl] = {"source": latest["source"],
-                       "kernels": {k: dict(v, source=latest["source"]) for k, v in latest["kernels"].items()}}
+        prov = latest.get("provenance") or {}
+        configs[wl] = {"source": latest["source"], "provenance": prov,
+                       "kernels": {k: dict(v, source=latest["source"], lib_sha256=prov.get("lib_sha256"),
+                                          head=prov.get("head")) for k, v in latest["kernels"].items()}}
         kernels = {}
         for name in sorted(configs, key=lambda c: c != "c3"):
             for k, v in configs[name]["kernels"].items():
                 kernels.setdefault(k, v)
         srcs = sorted({c["source"] for c in configs.values()})
-        latest = {"source": configs.get("c3", configs[wl])["source"], "sources": srcs, "kernels": kernels,
-                  "configs": configs}
+        head_cfg = configs.get("c3", configs[wl])
+        latest = {"source": head_cfg["source"], "sources": srcs, "kernels": kernels, "configs": configs,
+                  "head": (head_cfg.get("provenance") or {}).get("head"),
+                  "code_tree": (head_cfg.get("provenance") or {}).get("code_tree"),
+                  "lib_sha256": (head_cfg.get("provenance") or {}).get("lib_sha256")}
         with open(path, "w") as f:
             json.dump(latest, f, indent=1, sort_keys=True)
     print(json.dumps({k: summary[k] for k in summary if k != "sq"}, indent=1)[:3000])
