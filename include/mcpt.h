@@ -25,7 +25,9 @@ extern "C" {
 
 #define MCPT_VERSION 20200 /* 2.2.0: mcpt_stats gains comm_init_seconds, device_setup_seconds and
                                * device_seconds[MCPT_STATS_MAX_DEVICES] (appended): where a multi-device call's
-                               * time went;
+                               * time went; mcpt_render_opts gains stats_size (appended: a caller built against
+                               * an older header is refused by struct_size instead of having its smaller
+                               * mcpt_stats overrun);
                                * 2.1.0: mcpt_stats gains prep_exact_nodes, cache_build_seconds and prep_band_nodes
                                * (appended);
                                * 2.0.0: mcpt_render_opts carries struct_size (checked first), a device list
@@ -138,6 +140,8 @@ typedef struct {
      * communicator and returns, and under RCCL its peers then block in ncclReduce (RCCL has no way to
      * release them from one rank).  Leave that buffer's room free on every device. */
     mcpt_comm* comm;
+    uint32_t stats_size;    /* sizeof(mcpt_stats) of the caller's header (mcpt_render_opts_init sets it): the
+                             * library writes at most this many bytes of the stats (0: none) */
 } mcpt_render_opts;
 /* mcpt_render_opts.flags: skip the light-side cull statistic in the hot loop of the split light cull;
  * mcpt_stats.light_evals_culled_backface then reads 0 and _culled_plane holds both cheap-stage culls
@@ -159,7 +163,7 @@ enum { MCPT_RENDER_FRESH_PDF = 2 };
  * light triangles (the split prep); cheap culls, pick, sampling, pdf and shading stay fp64. */
 enum { MCPT_RENDER_PRECISION_FP32 = 4 };
 
-/* zero-fills *opts and sets struct_size, device = -1, seed = 20240430, spp = 10 (main.cpp:567),
+/* zero-fills *opts and sets struct_size, stats_size, device = -1, seed = 20240430, spp = 10 (main.cpp:567),
  * mode = MCPT_MODE_MIS */
 void mcpt_render_opts_init(mcpt_render_opts* opts);
 

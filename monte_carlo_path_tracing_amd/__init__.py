@@ -59,7 +59,7 @@ class RenderOpts(C.Structure):
                 ("seed", C.c_uint64), ("samples_per_launch", C.c_int32), ("queue_factor", C.c_int32),
                 ("device", C.c_int32), ("accel", C.c_int32), ("progress", C.c_void_p),
                 ("progress_user", C.c_void_p), ("flags", C.c_int32), ("num_devices", C.c_int32),
-                ("devices", C.POINTER(C.c_int32)), ("comm", C.c_void_p)]
+                ("devices", C.POINTER(C.c_int32)), ("comm", C.c_void_p), ("stats_size", C.c_uint32)]
 RENDER_NO_BACKFACE_STATS = 1  # mcpt_render_opts.flags (include/mcpt.h)
 RENDER_FRESH_PDF = 2  # shade_with_mis: the node's own light pdf instead of the reference's stale one
 RENDER_PRECISION_FP32 = 4  # opt-in FP32_STABLE light prep (packed-fp32 weights, fp64 sums); default FP64_LIGHT

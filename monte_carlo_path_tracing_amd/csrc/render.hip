@@ -6148,14 +6148,37 @@ void mcpt_render_opts_init(mcpt_render_opts* o) {
     if (!o) return;
     std::memset((void*)o, 0, sizeof *o);
     o->struct_size = sizeof *o;
+    o->stats_size = sizeof(mcpt_stats);
     o->spp = 10;  // main.cpp:567
     o->mode = MCPT_MODE_MIS;
     o->seed = 20240430;
     o->device = -1;
 }
 
+// the caller's stats: at most opts->stats_size bytes of the library's (a caller built against an older mcpt.h
+// passes a smaller struct; its prefix is the same fields)
+static void copy_stats(const mcpt_render_opts* o, const mcpt_stats& st, mcpt_stats* out) {
+    if (out) std::memcpy((void*)out, &st, std::min<size_t>(o->stats_size, sizeof st));
+}
+static int render_device_impl(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* dev_out,
+                              mcpt_stats* stats);
+static int render_impl(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* out_rgb,
+                       mcpt_stats* stats);
 int mcpt_render_device(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* dev_out,
                        mcpt_stats* stats) {
+    mcpt_stats st{};
+    const int rc = render_device_impl(sc, cam, o, dev_out, &st);
+    if (rc == MCPT_OK) copy_stats(o, st, stats);
+    return rc;
+}
+int mcpt_render(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* out_rgb, mcpt_stats* stats) {
+    mcpt_stats st{};
+    const int rc = render_impl(sc, cam, o, out_rgb, &st);
+    if (rc == MCPT_OK) copy_stats(o, st, stats);
+    return rc;
+}
+static int render_device_impl(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* dev_out,
+                              mcpt_stats* stats) {
     if (!sc || !o || !dev_out) {
         set_error("null argument");
         return MCPT_E_INVALID;
@@ -6181,8 +6204,8 @@ int mcpt_render_device(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render
     return render_on_device(sc, *D, cam, o, dev_out, stats);
 }
 
-int mcpt_render(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* out_rgb,
-                mcpt_stats* stats) {
+static int render_impl(mcpt_scene* sc, const mcpt_camera* cam, const mcpt_render_opts* o, double* out_rgb,
+                       mcpt_stats* stats) {
     if (!sc || !o || !out_rgb) {
         set_error("null argument");
         return MCPT_E_INVALID;

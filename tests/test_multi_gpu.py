@@ -88,6 +88,22 @@ def test_device_list_reports_where_the_time_went():
     sc.close()
 
 
+def test_stats_written_only_up_to_the_callers_size(scene):
+    """mcpt_render_opts.stats_size (ABI 2.2): a caller whose mcpt.h has a smaller mcpt_stats (2.1: up to
+    prep_band_nodes) gets that prefix filled and nothing written past it"""
+    import ctypes as C
+    cam = mcpt.Camera.reference(16, 12)
+    o = mcpt._opts(2, "mis", SEED, None, 0, 0, 0)
+    o.stats_size = mcpt.Stats.comm_init_seconds.offset  # the 2.1 struct
+    buf = (C.c_uint8 * (C.sizeof(mcpt.Stats) + 64))(*([0xAB] * (C.sizeof(mcpt.Stats) + 64)))
+    out = np.zeros((12, 16, 3))
+    rc = mcpt.lib().mcpt_render(scene.h, C.byref(cam), C.byref(o), out.reshape(-1), C.cast(buf, C.POINTER(mcpt.Stats)))
+    assert rc == 0, mcpt.lib().mcpt_last_error()
+    st = mcpt.Stats.from_buffer_copy(bytes(buf[:C.sizeof(mcpt.Stats)]))
+    assert st.camera_samples == 16 * 12 * 2 and st.seconds > 0
+    assert all(b == 0xAB for b in buf[o.stats_size:])
+
+
 def test_device_list_into_device_buffer(scene, single):
     import torch
     cam = mcpt.Camera.reference(80, 60)

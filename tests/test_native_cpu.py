@@ -54,6 +54,7 @@ def test_abi_struct_layouts_match_header(tmp_path):
     o = mcpt.RenderOpts()
     mcpt.lib().mcpt_render_opts_init(C.byref(o))
     assert o.struct_size == C.sizeof(mcpt.RenderOpts) and o.device == -1 and o.spp == 10
+    assert o.stats_size == C.sizeof(mcpt.Stats)
 
 
 def test_render_rejects_a_foreign_struct_size():
