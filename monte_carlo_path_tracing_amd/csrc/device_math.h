@@ -492,9 +492,10 @@ __device__ inline double light_weight_bf(d3 p0, d3 p1, d3 p2, double lsum2, d3 x
 // slivers (a spherical triangle seen nearly edge-on: an angle near 0 or pi, where acos is
 // ill-conditioned).  Slivers -- 4 - den > kBandTau num, i.e. the sum of 1/sin of the angles above
 // ~2 kBandTau -- are flagged here (one FMA and one compare per candidate) and carry their error term
-// into the band; the others are covered by the per-chunk bound.
+// into the band; the others are covered by the per-chunk bound.  tau 300 (round 6; was 1000): many
+// near-slivers just below 1000 together exceeded the per-chunk bound (tools/band_margin_study.py).
 #ifndef MCPT_BAND_TAU
-#define MCPT_BAND_TAU 1000.0
+#define MCPT_BAND_TAU 300.0
 #endif
 struct WeightBx {
     double w;     // weight (0 if culled)

@@ -179,8 +179,39 @@ def tiny_far(outdir):
     return _write(outdir, "tinyfar", obj, mtls, lights, CAM)
 
 
+def light_soup(outdir, n=1500, seed=3):
+    """n unrelated light triangles (round 6): random positions 0.3-40 units above / around the floor, random
+    orientations, sizes spanning 1e-4 .. 1 (log-uniform) and shapes from equilateral to slivers (one vertex pulled
+    to within 1e-3 of the opposite edge), one of five radiances each -- no tessellated sphere, no shared edges, so
+    the spherical triangles of a shading point cover every size, aspect and viewing angle the band must bound"""
+    import random
+    rng = random.Random(seed)
+    obj, mtls = gv.Obj(), []
+    _floor(obj, mtls)
+    groups = {k: [] for k in range(5)}
+    for _ in range(n):
+        c = (rng.uniform(-8.0, 8.0), 0.3 + 40.0 * rng.random() ** 2, rng.uniform(-8.0, 8.0))
+        size = 10.0 ** rng.uniform(-4.0, 0.0)
+        u = gv.norm((rng.gauss(0, 1), rng.gauss(0, 1), rng.gauss(0, 1)))
+        w = gv.norm(gv.cross(u, gv.norm((rng.gauss(0, 1), rng.gauss(0, 1), rng.gauss(0, 1)))))
+        a = gv.add(c, gv.mul(u, -size))
+        b = gv.add(c, gv.mul(u, size))
+        h = size * (1e-3 if rng.random() < 0.2 else rng.uniform(0.2, 1.7))
+        d = gv.add(gv.add(c, gv.mul(u, size * rng.uniform(-0.9, 0.9))), gv.mul(w, h))
+        nrm = gv.norm(gv.cross(gv.sub(b, a), gv.sub(d, a)))
+        ni = obj.normal(nrm)
+        groups[rng.randrange(5)].append(((obj.vert(a), ni), (obj.vert(b), ni), (obj.vert(d), ni)))
+    lights = []
+    for k, faces in groups.items():
+        name = "soup%d" % k
+        obj.groups.append((name, name, faces))
+        mtls.append((name, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0))
+        lights.append((name, (3.0 * (k + 1), 2.0 * (k + 1), 1.0 * (k + 1))))
+    return _write(outdir, "soup", obj, mtls, lights, CAM)
+
+
 STRESS = {"sphmix": (sphere_mix, 5200), "slivers": (slivers, 8 * 24 * 2 + 80), "tinyfar": (tiny_far, 12 * 48 + 224),
-          "dense": (dense_sphere, 14160)}
+          "dense": (dense_sphere, 14160), "soup": (light_soup, 1500)}
 
 
 def needles(outdir, n=70000, seed=7, length=1.0):

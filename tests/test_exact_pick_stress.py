@@ -16,8 +16,9 @@ On each: 2 000 surface points through mcpt_light_prep vs the oracle -- survivor 
 weights_sum within 1e-3 relative (the reference's own rounding noise; the literal fallback's nodes are
 bit-exact up to glibc's misrounded acos) -- and a 64x48 MIS frame vs the oracle at the same seed:
 relative L2 <= 1e-3 and every pixel <= 1e-3 (north star).  tools/band_margin_study.py --stress reports
-each scene's band margin (measured: veach x38, sphmix x11, slivers x2.7, dense x18; tinyfar: the band
-always covers the pick, every node takes the literal fallback).
+each scene's band margin (round 6, 8 seeds: veach x10, sphmix x17, slivers x2.7 (x2.1 over 32 seeds), dense x24,
+soup x111; tinyfar: the band always covers the pick, every node takes the literal fallback);
+tests/test_band_margin.py checks the margin on CPU.
 """
 import numpy as np
 import pytest

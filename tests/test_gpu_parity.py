@@ -331,6 +331,18 @@ def test_batching_is_invariant(scene):
     assert rel_l2(a, b) < 1e-12
 
 
+def test_fused_cull_switch_changes_no_pick(scene):
+    """MCPT_DEBUG_FUSED_CULL (the round-6 A/B of the fused cull, prep variant 8: cheap stages inside k_prep_pk2, one
+    wave per node) gives the renderer the same candidates, weights and picks as the default split cull, so the same
+    shading nodes and the same frame up to fp64 atomic order; a debug switch must not change the image"""
+    cam = mcpt.Camera.reference(96, 72)
+    a, sa = mcpt.render(scene, cam, 4, seed=SEED)
+    b, sb = mcpt.render(scene, cam, 4, seed=SEED, flags=mcpt.DEBUG_FUSED_CULL)
+    assert sa.shading_nodes == sb.shading_nodes and sa.prep_full_nodes == sb.prep_full_nodes
+    assert sa.light_evals_candidates == sb.light_evals_candidates
+    assert rel_l2(a, b) < 1e-12
+
+
 def test_seed_changes_image(scene):
     cam = mcpt.Camera.reference(64, 48)
     a, _ = mcpt.render(scene, cam, 2, seed=1)

@@ -6,7 +6,7 @@ pi).  A pick is taken from the fast weights only when its slack exceeds the band
 
     band = 8 u sqrt(sum_c n_c m_c^2)                      (per 64-light chunk: n_c candidates,
                                                            m_c = S_c + K_c (|x1 - c_c| + R_c))
-         + 0.25 u/2 sum_slivers 2 sum L sqrt(2 (4 - den)) / num   (candidates with 4 - den > 1000 num)
+         + 0.5 u/2 sum_slivers 2 sum L sqrt(2 (4 - den)) / num    (candidates with 4 - den > 300 num)
          + (2 ncand + 4096) u W,
 
 with the constants of render.hip (MCPT_BAND_KAPPA, MCPT_BAND_SLIVER, MCPT_BAND_TAU; chunk constants as
@@ -19,9 +19,12 @@ Test infrastructure only (loads the oracle).
 
     python tools/band_margin_study.py [--points N] [obj xml ...]        (default: the Veach stand-in)
     python tools/band_margin_study.py --stress                          (tests/scenegen.py STRESS scenes)
+    --seeds K: K independent point sets per scene, the worst reported (round 6: 32 seeds on the sliver
+    scene found a point at 1.48x the band of the round-3 constants, sliver 0.25 / tau 1000)
 """
 import argparse
 import os
+import re
 import sys
 import tempfile
 
@@ -33,7 +36,16 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from oracle import pyoracle as po  # noqa: E402
 
 U = 2.0 ** -53
-KAPPA, SLIVER, TAU = 8.0, 0.25, 1000.0
+
+
+def kernel_constants():
+    """MCPT_BAND_KAPPA, MCPT_BAND_SLIVER, MCPT_BAND_TAU as the library is built with them (csrc defaults)"""
+    csrc = os.path.join(ROOT, "monte_carlo_path_tracing_amd", "csrc")
+    text = open(os.path.join(csrc, "render.hip")).read() + open(os.path.join(csrc, "device_math.h")).read()
+    return tuple(float(re.search(r"#define MCPT_BAND_%s ([0-9.]+)" % k, text).group(1)) for k in ("KAPPA", "SLIVER", "TAU"))
+
+
+KAPPA, SLIVER, TAU = kernel_constants()
 
 
 def chunk_constants(P, lsum):
@@ -113,7 +125,9 @@ def study(obj, xml, npts, seed=11):
         numf, denf = num.astype(np.float64), den.astype(np.float64)
         slv = TAU * numf + denf < 4.0
         if slv.any():
-            band += SLIVER * 0.5 * U * float(np.sum(np.sqrt(2 * (4 - denf[slv])) / numf[slv] * 1.01 * 2 * lsum[cand][slv]))
+            with np.errstate(divide="ignore"):  # num 0: an infinite band, the literal fallback
+                band += SLIVER * 0.5 * U * float(np.sum(np.sqrt(2 * (4 - denf[slv])) / numf[slv] * 1.01 * 2 *
+                                                        lsum[cand][slv]))
         band += (2 * len(cand) + 4096) * U * abs(ws)
         worst = max(worst, err / band)
         wide += band > 1e-3 * abs(ws)
@@ -125,6 +139,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=400)
     ap.add_argument("--stress", action="store_true")
+    ap.add_argument("--seeds", type=int, default=1)
     ap.add_argument("files", nargs="*")
     a = ap.parse_args()
     scenes = []
@@ -138,11 +153,15 @@ def main():
     if not scenes:
         scenes = [("veach", os.path.join(ROOT, "scenes/veach-mis/veach-mis.obj"), os.path.join(ROOT, "scenes/veach-mis/veach-mis.xml"))]
     for name, obj, xml in scenes:
-        r = study(obj, xml, a.points)
+        runs = [study(obj, xml, a.points, seed=11 + k) for k in range(a.seeds)]
+        r = None if runs[0] is None else min(runs, key=lambda q: q["margin"])
+        if r is not None:
+            r["points"] = sum(q["points"] for q in runs)
+            r["wide_band_share"] = max(q["wide_band_share"] for q in runs)
         if r is None:
             print("%-8s no lights" % name)
             continue
-        print("%-8s N_L %5d, %4d points: max prefix error / band %.3f (margin x%.1f); band > 1e-3 W on %.3f of points" % (
+        print("%-8s N_L %5d, %5d points: max prefix error / band %.3f (margin x%.1f); band > 1e-3 W on %.3f of points" % (
             name, r["nlights"], r["points"], r["worst_err_over_band"], r["margin"], r["wide_band_share"]))
 
 
