@@ -1550,6 +1550,9 @@ constexpr int kPrepQueue = 128;  // per-wave candidate queue (ints)
 #ifndef MCPT_LB_EXACT
 #define MCPT_LB_EXACT 4  // k_prep_exact: 4 waves/SIMD (128 VGPRs)
 #endif
+#ifndef MCPT_EXACT_DEFER
+#define MCPT_EXACT_DEFER 1  // k_prep_exact: a root whose pixel another wave of the launch computes waits for a follow-up launch
+#endif
 #ifndef MCPT_PREP_GRAB
 #define MCPT_PREP_GRAB 8  // A/B (profiles/round3_ab_launch_params.txt): 4 -> 8 lowers the prep launch 20.65 -> 20.37-20.52 ms
 #endif
@@ -2909,7 +2912,7 @@ __global__ __launch_bounds__(kExactBlock, MCPT_LB_EXACT) void k_prep_exact(DScen
                                                          unsigned long long* stats, double* __restrict__ scratch,
                                                          const uint64_t* __restrict__ masks, int nmask, int nchunks,
                                                          const unsigned short* __restrict__ clst, const int4* __restrict__ cinfo,
-                                                         int lstride, int root_off, RootLit RL) {
+                                                         int lstride, int root_off, RootLit RL, int* __restrict__ defer) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (kExactBlock / 64);
     const int gw = blockIdx.x * (kExactBlock / 64) + (threadIdx.x >> 6);
@@ -2936,13 +2939,24 @@ __global__ __launch_bounds__(kExactBlock, MCPT_LB_EXACT) void k_prep_exact(DScen
             if (RL.slot) {
                 const int sv = __builtin_amdgcn_readfirstlane(
                     __hip_atomic_load(RL.slot + 16 + px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                bool later = false;  // another wave of this launch has the pixel (claimed or already stored)
                 if (sv >= 0 && (sv >> 20) < RL.launch) {  // stored by an earlier launch of this call
                     cum = RL.pool + (size_t)(sv & 0xfffff) * RL.stride;
                     run = cum[lstride];
                 } else if (sv == -1) {
                     int old = 0;
                     if (lane == 0) old = atomicCAS(RL.slot + 16 + px, -1, -2);
-                    claimed = __shfl(old, 0) == -1;
+                    old = __shfl(old, 0);
+                    claimed = old == -1;
+                    later = !claimed && old != -3;
+                } else {
+                    later = sv != -3;
+                }
+                // MCPT_EXACT_DEFER: rather than redo the literal sums another wave of this launch is computing,
+                // the root waits for the follow-up launch (defer list), which only searches them
+                if (later && defer) {
+                    if (lane == 0) defer[kExactHead + atomicAdd(defer, 1)] = node;
+                    continue;
                 }
             }
         }
@@ -5347,11 +5361,21 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
             if (exact_pick) {  // the band's nodes: the reference's literal prep and pick
                 hipLaunchKernelGGL(k_prep_band, dim3(kBandBlocks), dim3(256), 0, st, D.d, maybe_list, slack, cur->p, cur->cap,
                                    masks, nmask, nchunks, exact_list, P.stats);
+                // launch ids 2g and 2g + 1 (generation g): the follow-up launch reads what the first one stored
+                const int lid = (int)std::min<uint64_t>(2 * gens, 2046);
+                int* defer = MCPT_EXACT_DEFER && rl.slot ? maybe_list : nullptr;  // k_prep_band has consumed it
+                if (defer) HIP_OK(hipMemsetAsync(defer, 0, 4, st));
                 hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D.d.NL)), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
                                    cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,
                                    nullptr, P.stats, exact_scr, masks, nmask, nchunks, pc.use ? pc.lst : nullptr,
                                    pc.use ? pc.info : nullptr, pc.lstride, root_off,
-                                   RootLit{rl.slot, rl.pool, rl.cap, rl.stride, (int)std::min<uint64_t>(gens, 2047)});
+                                   RootLit{rl.slot, rl.pool, rl.cap, rl.stride, lid}, defer);
+                if (defer)  // the deferred roots (counted above already: no stats)
+                    hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D.d.NL)), dim3(kExactBlock), 0, st, D.d, o->seed, defer,
+                                       cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum,
+                                       cur->pick, nullptr, nullptr, exact_scr, masks, nmask, nchunks, pc.use ? pc.lst : nullptr,
+                                       pc.use ? pc.info : nullptr, pc.lstride, root_off,
+                                       RootLit{rl.slot, rl.pool, rl.cap, rl.stride, lid + 1}, nullptr);
                 HIP_OK(hipGetLastError());
             }
         }
@@ -5967,7 +5991,7 @@ int light_prep_query(mcpt_scene* sc, int32_t n, const double* x1, const double* 
                            (const int*)dl, (const double*)dp, (const double*)dn, n, nullptr, nullptr, nullptr,
                            (const double*)du, (double*)dw, (int*)dk, (int*)dc, nullptr, (double*)ds,
                            all_exact ? nullptr : (const uint64_t*)dm, prep_writes_masks(D->d, (const uint64_t*)dm) ? n : 0,
-                           prep_chunks(D->d.NL), nullptr, nullptr, 0, INT_MAX, RootLit{});
+                           prep_chunks(D->d.NL), nullptr, nullptr, 0, INT_MAX, RootLit{}, nullptr);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(D->stream));
     HIP_OK(hipMemcpy(wsum, dw, 8ull * n, hipMemcpyDeviceToHost));
