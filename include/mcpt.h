@@ -196,8 +196,9 @@ typedef struct {
                                 * boundary and were redone with the reference's literal formulas and
                                 * summation order (Mylight.cpp:335-438), so the pick is the reference's.
                                 * The band's constants are calibrated, not a proven bound (DESIGN.md
-                                * §4.3.3: tools/prep_error_study.py on the stand-in, margins x2.7-x38 on
-                                * the stress scenes of tests/test_exact_pick_stress.py) */
+                                * §4.3.3: tools/prep_error_study.py on the stand-in, tools/band_margin_study.py
+                                * on the stress scenes: margins x2.1 (slivers, 32 seeds) to x111, x10 on the
+                                * stand-in; tests/test_band_margin.py) */
     double cache_build_seconds; /* device time building the per-pixel root-point cache (in prep_seconds) */
     uint64_t prep_band_nodes;   /* light preps whose slack the whole-table band bound could not clear and
                                  * that took the per-chunk band test (prep_exact_nodes of them failed it) */
