@@ -19,8 +19,12 @@ enum {
     MCPT_DEBUG_SHARD_RANKS = 1 << 19,
     MCPT_DEBUG_RAYS_PERSIST = 1 << 20,
     MCPT_DEBUG_RAYS_CW8 = 1 << 21,
-    MCPT_DEBUG_FUSED_CULL = 1 << 22
+    MCPT_DEBUG_FUSED_CULL = 1 << 22,
+    MCPT_DEBUG_NO_EXACT_DEFER = 1 << 23
 };
+/* MCPT_DEBUG_NO_EXACT_DEFER: k_prep_exact recomputes a root's literal sums even when another wave of the same
+ * launch is computing its pixel's, instead of deferring the root to the follow-up launch that only searches the
+ * stored sums (the default since round 6; picks and sums are the same either way). */
 /* MCPT_DEBUG_FUSED_CULL: the MIS children's light prep runs its cheap stages inside k_prep_pk2, one wave per
  * node (prep variant 8, chunks below the node's tangent plane skipped), instead of k_prep_cull_lanes' lane per
  * node writing candidate words that k_prep_pk2 reads back (variant 17). */

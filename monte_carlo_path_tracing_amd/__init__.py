@@ -68,6 +68,7 @@ DEBUG_SHARD_RANKS = 1 << 19  # device lists: every entry its own communicator ra
 DEBUG_RAYS_PERSIST = 1 << 20  # MIS / shade ray sets through the persistent refilling traversal on every scene
 DEBUG_RAYS_CW8 = 1 << 21  # the persistent traversal walks the 8-wide compressed trees (k_rays_cw8)
 DEBUG_FUSED_CULL = 1 << 22  # MIS children's prep: cheap stages inside k_prep_pk2 (variant 8) instead of k_prep_cull_lanes
+DEBUG_NO_EXACT_DEFER = 1 << 23  # k_prep_exact recomputes same-launch duplicate roots instead of deferring them
 DEBUG_HIT_CW8 = 1 << 8  # mcpt_closest_hit: trace through the 8-wide trees
 
 

@@ -4947,7 +4947,8 @@ int validate_render(const mcpt_render_opts* o) {
     }
     if (o->flags & ~(MCPT_RENDER_NO_BACKFACE_STATS | MCPT_RENDER_FRESH_PDF | MCPT_RENDER_PRECISION_FP32 |
                      MCPT_DEBUG_SPLIT_BRDF | MCPT_DEBUG_NO_ROOT_CACHE | MCPT_DEBUG_COUNT_TRAVERSAL |
-                     MCPT_DEBUG_SHARD_RANKS | MCPT_DEBUG_RAYS_PERSIST | MCPT_DEBUG_RAYS_CW8 | MCPT_DEBUG_FUSED_CULL)) {
+                     MCPT_DEBUG_SHARD_RANKS | MCPT_DEBUG_RAYS_PERSIST | MCPT_DEBUG_RAYS_CW8 | MCPT_DEBUG_FUSED_CULL |
+                     MCPT_DEBUG_NO_EXACT_DEFER)) {
         set_error("unknown mcpt_render_opts.flags bits 0x%x", (unsigned)o->flags);
         return MCPT_E_INVALID;
     }
@@ -5363,7 +5364,8 @@ int render_on_device(mcpt_scene* sc, DeviceState& D, const mcpt_camera* cam, con
                                    masks, nmask, nchunks, exact_list, P.stats);
                 // launch ids 2g and 2g + 1 (generation g): the follow-up launch reads what the first one stored
                 const int lid = (int)std::min<uint64_t>(2 * gens, 2046);
-                int* defer = MCPT_EXACT_DEFER && rl.slot ? maybe_list : nullptr;  // k_prep_band has consumed it
+                int* defer = MCPT_EXACT_DEFER && rl.slot && !(o->flags & MCPT_DEBUG_NO_EXACT_DEFER) ? maybe_list
+                                                                                                    : nullptr;  // k_prep_band has consumed it
                 if (defer) HIP_OK(hipMemsetAsync(defer, 0, 4, st));
                 hipLaunchKernelGGL(k_prep_exact, dim3(exact_blocks(D.d.NL)), dim3(kExactBlock), 0, st, D.d, o->seed, exact_list,
                                    cur->p, cur->n, cur->cap, cur->pixel, cur->sample, cur->node, nullptr, cur->wsum, cur->pick,

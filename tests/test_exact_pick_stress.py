@@ -158,3 +158,21 @@ def test_cull_order_at_scale_changes_no_candidate():
     assert (ws17 > 0).sum() >= 100000
     assert np.array_equal(ws17.view(np.int64), ws18.view(np.int64))
     assert np.array_equal(p17, p18)
+
+
+def test_deferred_duplicate_roots_change_nothing(scenes):
+    """k_prep_exact defers a root whose pixel another wave of the same launch is computing to a follow-up launch
+    that only searches the stored literal sums (MCPT_EXACT_DEFER, round 6).  On tinyfar every pick is inside the
+    band, so every root takes the literal fallback and most of a pixel's roots share a launch: the render with the
+    deferral and the one that recomputes every root (MCPT_DEBUG_NO_EXACT_DEFER) list the same nodes, shade the same
+    nodes and give the same frame up to fp64 atomic order."""
+    obj, xml, _ = scenes["tinyfar"]
+    s = mcpt.Scene.load(obj, xml)
+    cam = s.camera()
+    cam.width, cam.height = 32, 24
+    a, sa = mcpt.render(s, cam, 64, mode="mis", seed=SEED)
+    b, sb = mcpt.render(s, cam, 64, mode="mis", seed=SEED, flags=mcpt.DEBUG_NO_EXACT_DEFER)
+    print("tinyfar 32x24x64: %d exact preps, %d cached roots" % (sa.prep_exact_nodes, sa.prep_cached_nodes))
+    assert sa.prep_exact_nodes == sb.prep_exact_nodes and sa.prep_exact_nodes > 10000
+    assert sa.shading_nodes == sb.shading_nodes and sa.prep_cached_nodes > 0
+    assert rel_l2(a, b) < 1e-12 and max_px_rel(a, b) < 1e-10
