@@ -268,6 +268,24 @@ def test_c3_full_frame_vs_oracle(scene, oscene):
     assert err <= TIGHT_L2 and mx <= TIGHT_PX_FRAME, (err, mx)
 
 
+@pytest.mark.parametrize("mode,spp", [("brdf", 4), ("shade_area", 2)])
+def test_full_frame_other_modes_vs_oracle(scene, oscene, mode, spp):
+    """C2's frame (800x600 BRDF-only) and shade() with uniform-area light sampling at 800x600 in full, every
+    pixel against the oracle at the same seed (the counter-RNG samples on both sides; the oracle on 16 host
+    threads, ~10 s): relative L2 and every pixel <= 1e-3 (north star), and what the build achieves
+    (tests/conftest.py).  shade()'s spherical sampler stays on the stride-20 subset above (its oracle frame
+    would take ~1 min)."""
+    cam = mcpt.Camera.reference(800, 600)
+    g, st = mcpt.render(scene, cam, spp, mode=mode, seed=SEED)
+    c, _ = oscene.render(po.reference_camera(800, 600), OMODE[mode], SEED, spp, nthreads=16)
+    err, mx = rel_l2(g, c), max_px_rel(g, c)
+    print("%s 800x600x%d full frame: rel L2 %.3e, max per-pixel %.3e; %d shading nodes" % (
+        mode, spp, err, mx, st.shading_nodes))
+    assert np.isfinite(g).all() and (g >= 0).all() and c.sum() > 0
+    assert err <= L2_TOL and mx <= L2_TOL
+    assert err <= TIGHT_L2 and mx <= TIGHT_PX_FRAME, (err, mx)
+
+
 @pytest.mark.parametrize("W,H,spp", [(80, 60, 8), (800, 600, 16)])
 def test_mis_fresh_pdf_flag_vs_oracle(scene, oscene, W, H, spp):
     """MCPT_RENDER_FRESH_PDF (the node's own light pdf, not the reference's stale sampler state,
